@@ -1,0 +1,238 @@
+// ref_harness.cpp -- TEST INFRASTRUCTURE ONLY (never shipped in the product).
+//
+// Drives the UNMODIFIED reference sources (compiled in place from
+// /root/reference/src by oracle/Makefile, output only into oracle/_ref/) on
+// fixed inputs, to produce golden vectors and a CPU timing baseline.
+// Setup mirrors src/main.cpp:13-78 (MPI_Init -> initializeMPI ->
+// allocate_lattice_arrays -> periodic_boundary); the lattice size is the
+// reference's compile-time NS/NT (-DCONFIG_H -DNS=.. -DNT=..).
+//
+// Modes
+//   fixture <dir> <ranks_x> <ranks_t> <m0> <tol> <max_iter>
+//       reads <dir>/U.bin psi.bin chi.bin (global fields, two planes of
+//       interleaved complex<double>, n = x*Nt + t), writes ref_Dpsi.bin,
+//       ref_Ddagchi.bin, ref_DDdagpsi.bin, ref_force.bin (psi, chi),
+//       ref_cgx.bin (CG on phi = psi) and prints one JSON line.
+//   gen <dir> <seed_U> <sigma> <seed_psi> <seed_chi>
+//       writes <dir>/U.bin psi.bin chi.bin from the synthetic generator
+//       (sm_fields.h) for the compiled-in lattice (single process).
+//   bench <ranks_x> <ranks_t> <seed_U> <sigma> <seed_psi> <m0> <napply> <ncg>
+//       generates the synthetic fields per rank (sm_fields.h), times napply
+//       D_phi applies and ncg CG iterations (tol = 0), prints one JSON line.
+#include "conjugate_gradient.h"
+#include "mpi_setup.h"
+#include "sm_fields.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+static long g_ddag_calls = 0;
+extern "C" void __real__Z14D_D_dagger_phiRK6spinorS1_RS_RKd(const spinor &, const spinor &,
+                                                             spinor &, const double &);
+// Counts D_D_dagger_phi calls made by conjugate_gradient (linked with
+// -Wl,--wrap=_Z14D_D_dagger_phiRK6spinorS1_RS_RKd): CG iterations = calls - 1.
+extern "C" void __wrap__Z14D_D_dagger_phiRK6spinorS1_RS_RKd(const spinor &U, const spinor &phi,
+                                                             spinor &Dphi, const double &m0) {
+    g_ddag_calls++;
+    __real__Z14D_D_dagger_phiRK6spinorS1_RS_RKd(U, phi, Dphi, m0);
+}
+
+static void setup(int rx, int rt) {
+    MPI_Comm_size(MPI_COMM_WORLD, &mpi::size);
+    MPI_Comm_rank(MPI_COMM_WORLD, &mpi::rank);
+    mpi::ranks_x = rx;
+    mpi::ranks_t = rt;
+    initializeMPI();
+    allocate_lattice_arrays();
+    periodic_boundary();
+}
+
+static int x_begin() { return mpi::coords[0] * mpi::width_x; }
+static int t_begin() { return mpi::coords[1] * mpi::width_t; }
+
+// Read this rank's block of a global two-plane complex field.
+static bool read_block(const std::string &path, spinor &s) {
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) return false;
+    std::vector<double> g((size_t)4 * LV::Ntot);
+    size_t got = fread(g.data(), sizeof(double), g.size(), f);
+    fclose(f);
+    if (got != g.size()) return false;
+    for (int x = 0; x < mpi::width_x; x++)
+        for (int t = 0; t < mpi::width_t; t++) {
+            long ng = (long)(x_begin() + x) * LV::Nt + t_begin() + t;
+            int n = x * mpi::width_t + t;
+            s.mu0[n] = c_double(g[2 * ng], g[2 * ng + 1]);
+            s.mu1[n] = c_double(g[2 * LV::Ntot + 2 * ng], g[2 * LV::Ntot + 2 * ng + 1]);
+        }
+    return true;
+}
+
+// Gather per-rank blocks of (plane0, plane1) with `ncomp` doubles per site to
+// rank 0 and write the global field.
+static void write_global(const std::string &path, const double *p0, const double *p1, int ncomp) {
+    const int blk = mpi::maxSize * ncomp;
+    std::vector<double> mine((size_t)2 * blk);
+    memcpy(mine.data(), p0, sizeof(double) * blk);
+    memcpy(mine.data() + blk, p1, sizeof(double) * blk);
+    std::vector<double> all;
+    std::vector<int> coords((size_t)2 * mpi::size);
+    int my[2] = {mpi::coords[0], mpi::coords[1]};
+    MPI_Gather(my, 2, MPI_INT, coords.data(), 2, MPI_INT, 0, MPI_COMM_WORLD);
+    if (mpi::rank == 0) all.resize((size_t)2 * blk * mpi::size);
+    MPI_Gather(mine.data(), 2 * blk, MPI_DOUBLE, all.data(), 2 * blk, MPI_DOUBLE, 0, MPI_COMM_WORLD);
+    if (mpi::rank != 0) return;
+    std::vector<double> g((size_t)2 * ncomp * LV::Ntot);
+    for (int r = 0; r < mpi::size; r++) {
+        const double *b = all.data() + (size_t)2 * blk * r;
+        int xb = coords[2 * r] * mpi::width_x, tb = coords[2 * r + 1] * mpi::width_t;
+        for (int x = 0; x < mpi::width_x; x++)
+            for (int t = 0; t < mpi::width_t; t++) {
+                long ng = (long)(xb + x) * LV::Nt + tb + t;
+                int n = x * mpi::width_t + t;
+                for (int c = 0; c < ncomp; c++) {
+                    g[(size_t)ncomp * ng + c] = b[(size_t)ncomp * n + c];
+                    g[(size_t)ncomp * LV::Ntot + (size_t)ncomp * ng + c] = b[blk + (size_t)ncomp * n + c];
+                }
+            }
+    }
+    FILE *f = fopen(path.c_str(), "wb");
+    fwrite(g.data(), sizeof(double), g.size(), f);
+    fclose(f);
+}
+
+static void write_spinor(const std::string &path, const spinor &s) {
+    write_global(path, reinterpret_cast<const double *>(s.mu0), reinterpret_cast<const double *>(s.mu1), 2);
+}
+
+static int run_fixture(const std::string &dir, double m0, double tol, int max_iter) {
+    spinor U(mpi::maxSize), psi(mpi::maxSize), chi(mpi::maxSize);
+    int ok = read_block(dir + "/U.bin", U) && read_block(dir + "/psi.bin", psi) &&
+             read_block(dir + "/chi.bin", chi);
+    if (!ok) {
+        if (mpi::rank == 0) fprintf(stderr, "cannot read inputs in %s\n", dir.c_str());
+        return 1;
+    }
+    spinor Dpsi(mpi::maxSize), Ddchi(mpi::maxSize), DDpsi(mpi::maxSize), x(mpi::maxSize);
+    D_phi(U, psi, Dpsi, m0);
+    D_dagger_phi(U, chi, Ddchi, m0);
+    D_D_dagger_phi(U, psi, DDpsi, m0);
+    re_field F = phi_dag_partialD_phi(U, psi, chi);
+    c_double z1 = dot(chi, Dpsi), z2 = dot(Ddchi, psi);
+    CG::tol = tol;
+    CG::max_iter = max_iter;
+    long before = g_ddag_calls;
+    double t0 = MPI_Wtime();
+    int conv = conjugate_gradient(U, psi, x, m0);
+    double t1 = MPI_Wtime();
+    long cg_calls = g_ddag_calls - before;
+    // final true residual |psi - DD^dag x| / |psi|
+    spinor Ax(mpi::maxSize), res(mpi::maxSize);
+    D_D_dagger_phi(U, x, Ax, m0);
+    for (int n = 0; n < mpi::maxSize; n++) {
+        res.mu0[n] = psi.mu0[n] - Ax.mu0[n];
+        res.mu1[n] = psi.mu1[n] - Ax.mu1[n];
+    }
+    double rr = std::real(dot(res, res)), pp = std::real(dot(psi, psi));
+    write_spinor(dir + "/ref_Dpsi.bin", Dpsi);
+    write_spinor(dir + "/ref_Ddagchi.bin", Ddchi);
+    write_spinor(dir + "/ref_DDdagpsi.bin", DDpsi);
+    write_spinor(dir + "/ref_cgx.bin", x);
+    write_global(dir + "/ref_force.bin", F.mu0, F.mu1, 1);
+    if (mpi::rank == 0) {
+        printf("{\"Nx\": %d, \"Nt\": %d, \"ranks_x\": %d, \"ranks_t\": %d, \"m0\": %.17g, "
+               "\"cg_converged\": %d, \"cg_iters\": %ld, \"cg_true_relres\": %.17g, "
+               "\"cg_seconds\": %.6f, "
+               "\"dot_chi_Dpsi\": [%.17g, %.17g], \"dot_Ddagchi_psi\": [%.17g, %.17g]}\n",
+               LV::Nx, LV::Nt, mpi::ranks_x, mpi::ranks_t, m0, conv, cg_calls - 1,
+               sqrt(rr / pp), t1 - t0, z1.real(), z1.imag(), z2.real(), z2.imag());
+    }
+    return 0;
+}
+
+static int run_bench(unsigned long long seedU, double sigma, unsigned long long seedP, double m0,
+                     int napply, int ncg) {
+    spinor U(mpi::maxSize), psi(mpi::maxSize), out(mpi::maxSize), x(mpi::maxSize);
+    // Per-rank block of the same global synthetic fields the GPU bench uses.
+    {
+        std::vector<double> u0(2 * (size_t)mpi::maxSize), u1(u0.size()), p0(u0.size()), p1(u0.size());
+        sm_fields_fill_gauge(seedU, sigma, LV::Nt, x_begin(), mpi::width_x, t_begin(), mpi::width_t,
+                             u0.data(), u1.data());
+        sm_fields_fill_spinor(seedP, LV::Nt, x_begin(), mpi::width_x, t_begin(), mpi::width_t,
+                              p0.data(), p1.data());
+        for (int n = 0; n < mpi::maxSize; n++) {
+            U.mu0[n] = c_double(u0[2 * n], u0[2 * n + 1]);
+            U.mu1[n] = c_double(u1[2 * n], u1[2 * n + 1]);
+            psi.mu0[n] = c_double(p0[2 * n], p0[2 * n + 1]);
+            psi.mu1[n] = c_double(p1[2 * n], p1[2 * n + 1]);
+        }
+    }
+    MPI_Barrier(MPI_COMM_WORLD);
+    double t0 = MPI_Wtime();
+    for (int i = 0; i < napply; i++) D_phi(U, psi, out, m0);
+    MPI_Barrier(MPI_COMM_WORLD);
+    double t1 = MPI_Wtime();
+    CG::tol = 0.0;
+    CG::max_iter = ncg;
+    long before = g_ddag_calls;
+    MPI_Barrier(MPI_COMM_WORLD);
+    double t2 = MPI_Wtime();
+    conjugate_gradient(U, psi, x, m0);
+    MPI_Barrier(MPI_COMM_WORLD);
+    double t3 = MPI_Wtime();
+    long it = g_ddag_calls - before - 1;
+    if (mpi::rank == 0) {
+        double sites = (double)LV::Ntot;
+        double dt_apply = napply ? (t1 - t0) / napply : 0.0;
+        printf("{\"Nx\": %d, \"Nt\": %d, \"ranks\": %d, \"ranks_x\": %d, \"ranks_t\": %d, "
+               "\"apply_s\": %.6g, \"apply_GBps\": %.6g, \"cg_iters\": %ld, \"cg_s\": %.6g, "
+               "\"cg_it_per_s\": %.6g}\n",
+               LV::Nx, LV::Nt, mpi::size, mpi::ranks_x, mpi::ranks_t, dt_apply,
+               napply ? 96.0 * sites / dt_apply / 1e9 : 0.0, it, t3 - t2,
+               it > 0 ? it / (t3 - t2) : 0.0);
+    }
+    return 0;
+}
+
+static int run_gen(const std::string &dir, unsigned long long seedU, double sigma,
+                   unsigned long long seedP, unsigned long long seedC) {
+    const size_t S = (size_t)LV::Ntot;
+    std::vector<double> a(4 * S);
+    FILE *f;
+    sm_fields_fill_gauge(seedU, sigma, LV::Nt, 0, LV::Nx, 0, LV::Nt, a.data(), a.data() + 2 * S);
+    if (!(f = fopen((dir + "/U.bin").c_str(), "wb"))) return 1;
+    fwrite(a.data(), sizeof(double), a.size(), f);
+    fclose(f);
+    sm_fields_fill_spinor(seedP, LV::Nt, 0, LV::Nx, 0, LV::Nt, a.data(), a.data() + 2 * S);
+    if (!(f = fopen((dir + "/psi.bin").c_str(), "wb"))) return 1;
+    fwrite(a.data(), sizeof(double), a.size(), f);
+    fclose(f);
+    sm_fields_fill_spinor(seedC, LV::Nt, 0, LV::Nx, 0, LV::Nt, a.data(), a.data() + 2 * S);
+    if (!(f = fopen((dir + "/chi.bin").c_str(), "wb"))) return 1;
+    fwrite(a.data(), sizeof(double), a.size(), f);
+    fclose(f);
+    return 0;
+}
+
+int main(int argc, char **argv) {
+    MPI_Init(&argc, &argv);
+    int rc = 2;
+    if (argc >= 7 && !strcmp(argv[1], "gen")) {
+        rc = run_gen(argv[2], strtoull(argv[3], 0, 10), atof(argv[4]), strtoull(argv[5], 0, 10),
+                     strtoull(argv[6], 0, 10));
+    } else if (argc >= 8 && !strcmp(argv[1], "fixture")) {
+        setup(atoi(argv[3]), atoi(argv[4]));
+        rc = run_fixture(argv[2], atof(argv[5]), atof(argv[6]), atoi(argv[7]));
+    } else if (argc >= 10 && !strcmp(argv[1], "bench")) {
+        setup(atoi(argv[2]), atoi(argv[3]));
+        rc = run_bench(strtoull(argv[4], 0, 10), atof(argv[5]), strtoull(argv[6], 0, 10),
+                       atof(argv[7]), atoi(argv[8]), atoi(argv[9]));
+    } else {
+        fprintf(stderr, "usage: gen <dir> seedU sigma seedP seedC | fixture <dir> rx rt m0 tol max_iter | bench rx rt seedU sigma seedP m0 napply ncg\n");
+    }
+    MPI_Finalize();
+    return rc;
+}

@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ from the REFERENCE itself.
+
+Test infrastructure only. Runs in the dev container, where /root/reference
+exists: `make -C oracle ref` compiles the unmodified reference sources
+(src/variables.cpp, src/dirac_operator.cpp, src/conjugate_gradient.cpp) with
+our driver oracle/ref_harness.cpp into oracle/_ref/sm_ref_<Nx>x<Nt>. For each
+fixture this script
+
+  1. writes the inputs U, psi, chi with the counter-based generator
+     (`sm_ref_* gen`, schwingermodel_amd/csrc/sm_fields.h),
+  2. runs the reference on them (`sm_ref_* fixture`, single rank) and keeps
+     D psi, D^dag chi, D D^dag psi, phi_dag_partialD_phi(U, psi, chi) and the
+     CG solution of D D^dag x = psi (tol 1e-10, max_iter 10000 as
+     src/main.cpp:26-27) plus the CG iteration count,
+  3. optionally re-runs on a 2x2 MPI decomposition (`--mpi`) and records that
+     the reference is decomposition-invariant (bitwise for D/D^dag/force).
+
+Output: tests/golden/<name>.npz (inputs + outputs, float64, the reference's
+global layout: two planes of interleaved complex, n = x*Nt + t) and
+tests/golden/manifest.json. The fixtures are data, not reference source.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF_DIR = os.path.join(REPO, "oracle", "_ref")
+
+SEED_U, SEED_PSI, SEED_CHI = 4321, 5678, 91011
+
+# name, Nx, Nt, sigma (>0 Gaussian theta, <0 hot, 0 cold), m0
+FIXTURES = [
+    ("l4x2_hot_m0p2", 4, 2, -1.0, 0.2),
+    ("l8x8_hot_m0p2", 8, 8, -1.0, 0.2),
+    ("l8x8_cold_m0", 8, 8, 0.0, 0.0),
+    ("l16x16_b2_m-0p19", 16, 16, 0.4242, -0.19),
+    ("l32x48_b3_m-0p10", 32, 48, 0.3246, -0.10),
+    ("l32x48_hot_m0", 32, 48, -1.0, 0.0),
+    ("l40x24_hot_m0p2", 40, 24, -1.0, 0.2),
+    ("l64x64_b2_m0", 64, 64, 0.4242, 0.0),
+    ("l64x64_b5_m-0p06", 64, 64, 0.2374, -0.06),
+]
+
+OUTS = ["ref_Dpsi", "ref_Ddagchi", "ref_DDdagpsi", "ref_force", "ref_cgx"]
+
+
+def run(cmd, **kw):
+    env = dict(os.environ, HOSTNAME=os.environ.get("HOSTNAME", "localhost"))
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, **kw)
+    if r.returncode != 0:
+        raise RuntimeError(f"{cmd} failed: {r.stderr}")
+    return r.stdout
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mpi", action="store_true", help="also run 2x2 ranks (mpirun)")
+    ap.add_argument("--mpirun", default="/opt/conda/bin/mpirun")
+    args = ap.parse_args()
+    sizes = sorted({f"{nx}x{nt}" for _, nx, nt, _, _ in FIXTURES})
+    subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref", "oracle",
+                    "REF_SIZES=" + " ".join(sizes)], check=True)
+    manifest = {"generator": "tests/golden/make_golden.py",
+                "reference": "Fabian2598/SchwingerModel (unmodified src/, compiled by oracle/Makefile)",
+                "layout": "two planes of interleaved complex<double>, n = x*Nt + t; force: two real planes",
+                "seeds": {"U": SEED_U, "psi": SEED_PSI, "chi": SEED_CHI},
+                "cg": {"tol": 1e-10, "max_iter": 10000, "rhs": "psi"},
+                "fixtures": {}}
+    for name, nx, nt, sigma, m0 in FIXTURES:
+        exe = os.path.join(REF_DIR, f"sm_ref_{nx}x{nt}")
+        with tempfile.TemporaryDirectory() as d:
+            run([exe, "gen", d, str(SEED_U), repr(sigma), str(SEED_PSI), str(SEED_CHI)])
+            meta = json.loads(run([exe, "fixture", d, "1", "1", repr(m0), "1e-10", "10000"]))
+            arrs = {k: np.fromfile(os.path.join(d, k + ".bin"), dtype=np.float64)
+                    for k in ["U", "psi", "chi"] + OUTS}
+            if args.mpi and nx % 2 == 0 and nt % 2 == 0 and nx >= 4 and nt >= 4:
+                for k in OUTS:
+                    os.rename(os.path.join(d, k + ".bin"), os.path.join(d, k + ".1rank"))
+                meta2 = json.loads(run([args.mpirun, "-n", "4", exe, "fixture", d, "2", "2",
+                                        repr(m0), "1e-10", "10000"], timeout=600))
+                dec = {}
+                for k in OUTS:
+                    a = np.fromfile(os.path.join(d, k + ".bin"), dtype=np.float64)
+                    b = arrs[k]
+                    dec[k] = "bitwise" if np.array_equal(a.view(np.uint64), b.view(np.uint64)) \
+                        else f"max_abs={np.abs(a - b).max():.3e}"
+                dec["cg_iters_2x2"] = meta2["cg_iters"]
+                meta["decomposition_2x2"] = dec
+        meta.update({"sigma": sigma, "file": name + ".npz"})
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
+        manifest["fixtures"][name] = meta
+        print(name, json.dumps(meta), file=sys.stderr)
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
