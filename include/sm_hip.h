@@ -1,0 +1,134 @@
+/*
+ * sm_hip.h -- C-ABI of the MI355X-native Wilson-Dirac / CG hot path
+ * (libsm_hip.so). Plain pointers and sizes only; no HIP, RCCL or torch types.
+ *
+ * This is the drop-in boundary for Fabian2598/SchwingerModel's
+ *   src/dirac_operator.cpp   (D_phi, D_dagger_phi, D_D_dagger_phi,
+ *                             phi_dag_partialD_phi)
+ *   src/conjugate_gradient.cpp (conjugate_gradient)
+ *   include/variables.h:181-192 (dot)
+ * Each entry point below names the reference function it replaces. A C++
+ * shim with the reference's exact signatures (schwingermodel_amd/csrc/
+ * dirac_operator_hip.cpp) is built on top of it; see INTEGRATION.md.
+ *
+ * Host field layout = the reference's spinor (include/variables.h:54-100):
+ * for every field two separate arrays (mu0, mu1) of complex<double>, each
+ * complex stored as (re, im) doubles, site n = x*Wt + t over this shard's
+ * block (all Nx rows, Wt = Nt/nshard t-values starting at t0 = shard*Wt).
+ * U: mu0 = U_t (mu = 0, t-direction), mu1 = U_x. re_field (force) = two
+ * arrays of doubles.
+ *
+ * Device ("_dev") variants take ONE device buffer per field: plane mu0
+ * followed by plane mu1 (2*Nx*Wt complex<double>), already resident in HBM.
+ *
+ * Multi-GPU: the lattice is sharded along t over nshard processes (one GPU
+ * each), neighbours t+-1 exchanged over RCCL (xGMI). Every rank must call
+ * every operator/CG entry point in lockstep, as in the reference (SPMD).
+ *
+ * Return codes: 0 = OK, nonzero = error (sm_last_error() describes it).
+ * No C++ exceptions cross this boundary.
+ */
+#ifndef SM_HIP_H
+#define SM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SM_OK 0
+#define SM_ERR_ARG 1    /* bad argument / geometry                      */
+#define SM_ERR_HIP 2    /* HIP runtime error (incl. no GPU)             */
+#define SM_ERR_RCCL 3   /* RCCL error                                   */
+#define SM_ERR_STATE 4  /* call out of order (e.g. no gauge uploaded)   */
+
+typedef struct sm_ctx sm_ctx;
+
+/* CG outcome (the reference returns only 1/0; it also prints err on failure,
+ * src/conjugate_gradient.cpp:64-65). */
+typedef struct {
+    int converged;     /* 1 = ||r|| < tol*||phi||, 0 = max_iter reached   */
+    int iterations;    /* loop passes (D D^dag applications in the loop)  */
+    double residual;   /* ||r|| of the last iteration (reference "err")    */
+    double phi_norm;   /* ||phi||                                          */
+} sm_cg_result;
+
+/* ---- library / host-only helpers (no GPU needed) ------------------------ */
+int sm_abi_version(void);
+const char *sm_last_error(void);
+
+/* t-shard geometry: replaces include/mpi_setup.h:6-23 (assignWidth) for the
+ * ranks_x = 1, ranks_t = nshard decomposition. */
+int sm_shard_plan(int Nt, int nshard, int shard, int *t0, int *Wt);
+
+/* Counter-based synthetic fields: gauge U = exp(i theta),
+ * theta ~ N(0, sigma^2) (sigma > 0), uniform (sigma < 0, "hot"), 0 ("cold");
+ * spinor as HMC::RandomCHI (src/hmc.cpp:19-28). Writes rows [x0, x0+nx),
+ * t in [t0, t0+Wt) of the global Nx x Nt_global field. */
+void sm_fill_gauge(uint64_t seed, double sigma, int Nt_global, int x0, int nx, int t0, int Wt,
+                   double *U0, double *U1);
+void sm_fill_spinor(uint64_t seed, int Nt_global, int x0, int nx, int t0, int Wt, double *p0,
+                    double *p1);
+
+/* 28-byte-record binary gauge configuration (src/gauge_conf.cpp:378-423
+ * SaveConf / :495-546 readBinary): per site x-major, t-minor, mu = 0,1:
+ * int32 x, int32 t, int32 mu, float64 re, float64 im. Global field. */
+int sm_conf_write(const char *path, int Nx, int Nt, const double *U0, const double *U1);
+int sm_conf_read(const char *path, int Nx, int Nt, double *U0, double *U1);
+
+/* RCCL unique id for nshard > 1 (rank 0 creates, all ranks receive it). */
+int sm_comm_unique_id(void *id_out, int id_bytes);  /* id_bytes >= 128 */
+
+/* ---- context -------------------------------------------------------------- */
+/* One context = one t-shard on one GPU. unique_id is ignored for nshard == 1. */
+int sm_create(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device,
+              const void *unique_id);
+int sm_destroy(sm_ctx *ctx);
+/* Launch on a caller stream (a hipStream_t, e.g. torch's current stream);
+ * NULL restores the context's own stream. */
+int sm_set_stream(sm_ctx *ctx, void *hip_stream);
+int sm_synchronize(sm_ctx *ctx);
+int sm_local_sites(const sm_ctx *ctx, long *V, int *Nx, int *Wt, int *t0);
+
+/* Gauge field (host / device). Must precede every operator call; re-upload
+ * whenever the caller changes U (the reference mutates U between calls,
+ * src/hmc.cpp:69-99). */
+int sm_upload_gauge(sm_ctx *ctx, const double *U0, const double *U1);
+int sm_upload_gauge_dev(sm_ctx *ctx, const double *U_dev);
+
+/* ---- operators, host pointers (drop-in; synchronous) ---------------------- */
+/* D_phi (dagger = 0), src/dirac_operator.cpp:24; D_dagger_phi (dagger = 1), :247 */
+int sm_dirac(sm_ctx *ctx, const double *in0, const double *in1, double *out0, double *out1,
+             double m0, int dagger);
+/* D_D_dagger_phi, src/dirac_operator.cpp:477 */
+int sm_ddag(sm_ctx *ctx, const double *in0, const double *in1, double *out0, double *out1,
+            double m0);
+/* phi_dag_partialD_phi(U, left, right) -> re_field, src/dirac_operator.cpp:486 */
+int sm_force(sm_ctx *ctx, const double *l0, const double *l1, const double *r0, const double *r1,
+             double *F0, double *F1);
+/* dot(a, b) = sum a conj(b) over all shards, include/variables.h:181. out = (re, im) */
+int sm_dot(sm_ctx *ctx, const double *a0, const double *a1, const double *b0, const double *b1,
+           double *out);
+/* conjugate_gradient(U, phi, x, m0), src/conjugate_gradient.cpp:4: solves
+ * D D^dag x = phi with x0 = phi and the stop test ||r|| < tol ||phi||. */
+int sm_cg(sm_ctx *ctx, const double *phi0, const double *phi1, double *x0, double *x1, double m0,
+          double tol, int max_iter, sm_cg_result *res);
+
+/* ---- operators, device-resident fields (asynchronous on the ctx stream) --- */
+int sm_dirac_dev(sm_ctx *ctx, const double *in, double *out, double m0, int dagger);
+int sm_ddag_dev(sm_ctx *ctx, const double *in, double *out, double m0);
+int sm_force_dev(sm_ctx *ctx, const double *l, const double *r, double *F);
+int sm_dot_dev(sm_ctx *ctx, const double *a, const double *b, double *out_host); /* syncs */
+int sm_cg_dev(sm_ctx *ctx, const double *phi, double *x, double m0, double tol, int max_iter,
+              sm_cg_result *res);
+/* Stepwise CG for benchmarking: begin (x = phi, r, d, norms), enqueue n
+ * iterations without host synchronisation, then read the status (syncs). */
+int sm_cg_begin(sm_ctx *ctx, const double *phi, double *x, double m0, double tol);
+int sm_cg_iterate(sm_ctx *ctx, int n);
+int sm_cg_status(sm_ctx *ctx, sm_cg_result *res);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,74 @@
+"""ctypes binding of libsm_hip.so (include/sm_hip.h).
+
+The product path is the HIP library; there is no CPU fallback. If the shared
+object is missing or fails to load, importing this module raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsm_hip.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "sm_hip.h")
+
+
+class SMError(RuntimeError):
+    pass
+
+
+class CGResult(ctypes.Structure):
+    _fields_ = [("converged", ctypes.c_int), ("iterations", ctypes.c_int),
+                ("residual", ctypes.c_double), ("phi_norm", ctypes.c_double)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`"
+                          " (the HIP path has no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, ci, cd, cl = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_long
+    u64 = ctypes.c_uint64
+    sig = {
+        "sm_abi_version": ([], ci),
+        "sm_last_error": ([], ctypes.c_char_p),
+        "sm_shard_plan": ([ci, ci, ci, ctypes.POINTER(ci), ctypes.POINTER(ci)], ci),
+        "sm_fill_gauge": ([u64, cd, ci, ci, ci, ci, ci, vp, vp], None),
+        "sm_fill_spinor": ([u64, ci, ci, ci, ci, ci, vp, vp], None),
+        "sm_conf_write": ([ctypes.c_char_p, ci, ci, vp, vp], ci),
+        "sm_conf_read": ([ctypes.c_char_p, ci, ci, vp, vp], ci),
+        "sm_comm_unique_id": ([vp, ci], ci),
+        "sm_create": ([ctypes.POINTER(vp), ci, ci, ci, ci, ci, vp], ci),
+        "sm_destroy": ([vp], ci),
+        "sm_set_stream": ([vp, vp], ci),
+        "sm_synchronize": ([vp], ci),
+        "sm_local_sites": ([vp, ctypes.POINTER(cl), ctypes.POINTER(ci), ctypes.POINTER(ci),
+                            ctypes.POINTER(ci)], ci),
+        "sm_upload_gauge": ([vp, vp, vp], ci),
+        "sm_upload_gauge_dev": ([vp, vp], ci),
+        "sm_dirac": ([vp, vp, vp, vp, vp, cd, ci], ci),
+        "sm_ddag": ([vp, vp, vp, vp, vp, cd], ci),
+        "sm_force": ([vp, vp, vp, vp, vp, vp, vp], ci),
+        "sm_dot": ([vp, vp, vp, vp, vp, vp], ci),
+        "sm_cg": ([vp, vp, vp, vp, vp, cd, cd, ci, ctypes.POINTER(CGResult)], ci),
+        "sm_dirac_dev": ([vp, vp, vp, cd, ci], ci),
+        "sm_ddag_dev": ([vp, vp, vp, cd], ci),
+        "sm_force_dev": ([vp, vp, vp, vp], ci),
+        "sm_dot_dev": ([vp, vp, vp, vp], ci),
+        "sm_cg_dev": ([vp, vp, vp, cd, cd, ci, ctypes.POINTER(CGResult)], ci),
+        "sm_cg_begin": ([vp, vp, vp, cd, cd], ci),
+        "sm_cg_iterate": ([vp, ci], ci),
+        "sm_cg_status": ([vp, ctypes.POINTER(CGResult)], ci),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    return lib
+
+
+lib = _load()
+
+
+def check(rc):
+    if rc != 0:
+        raise SMError(f"sm_hip error {rc}: {lib.sm_last_error().decode(errors='replace')}")
+    return rc

@@ -1,0 +1,64 @@
+"""In-tree build of libsm_hip.so for gfx950 (hipcc; no JIT cache, no pip install).
+
+    python -m schwingermodel_amd.build          # library only
+The .so lands next to this file, so it travels with the repo snapshot to the
+GPU box and is the one the tests / bench / smoke load.
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libsm_hip.so")
+SOURCES = ["sm_kernels.hip", "sm_capi.cpp"]
+HEADERS = ["sm_internal.h", "sm_fields.h"]
+
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.path.join(ROCM, "bin", "hipcc")
+ARCH = os.environ.get("SM_OFFLOAD_ARCH", "gfx950")
+
+# -ffp-contract=off: no FMA contraction, so D / D^dag / force are bit-identical
+# to the reference's x86-64 (non-FMA) std::complex arithmetic.
+CFLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-Wall",
+          f"--offload-arch={ARCH}", f"-I{ROCM}/include", f"-I{os.path.join(REPO, 'include')}"]
+LDFLAGS = ["-shared", f"-L{ROCM}/lib", "-lrccl", f"-Wl,-rpath,{ROCM}/lib"]
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_library(force=False, verbose=True):
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
+    deps.append(os.path.join(REPO, "include", "sm_hip.h"))
+    if not force and not _stale(LIB, deps):
+        return LIB
+    if not os.path.exists(HIPCC):
+        raise RuntimeError(f"hipcc not found at {HIPCC}")
+    tmp = LIB + ".tmp"
+    cmd = [HIPCC] + CFLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", tmp] + LDFLAGS
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def build_oracle(with_reference=None):
+    """Test checker: oracle/liboracle.so, plus oracle/_ref/ when /root/reference exists."""
+    oracle_dir = os.path.join(REPO, "oracle")
+    subprocess.run(["make", "-s", "-C", oracle_dir, "oracle"], check=True)
+    if with_reference is None:
+        with_reference = os.path.isdir("/root/reference/src")
+    if with_reference and shutil.which("g++"):
+        subprocess.run(["make", "-s", "-C", oracle_dir, "ref"], check=True)
+
+
+if __name__ == "__main__":
+    build_library(force="--force" in sys.argv)

@@ -1,0 +1,573 @@
+// sm_capi.cpp -- host side of libsm_hip.so: the C-ABI of include/sm_hip.h.
+//
+// Owns one t-shard of the lattice on one GPU: device-resident gauge field,
+// CG work fields, halo faces, reduction partials and the device CG scalars.
+// Kernels are in sm_kernels.hip; the multi-GPU transport is RCCL (xGMI).
+#include "../../include/sm_hip.h"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "sm_fields.h"
+#include "sm_internal.h"
+
+using namespace sm;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return fail(SM_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                        __FILE__, __LINE__);                                            \
+    } while (0)
+
+#define NCCL_TRY(expr)                                                                     \
+    do {                                                                                   \
+        ncclResult_t r_ = (expr);                                                          \
+        if (r_ != ncclSuccess)                                                             \
+            return fail(SM_ERR_RCCL, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(r_), \
+                        __FILE__, __LINE__);                                               \
+    } while (0)
+
+#define TRY(expr)                  \
+    do {                           \
+        int rc_ = (expr);          \
+        if (rc_ != SM_OK) return rc_; \
+    } while (0)
+
+}  // namespace
+
+// Work fields, each 2*V complex (plane mu0 then mu1).
+enum { F_IN, F_OUT, F_TMP, F_X, F_R, F_D, F_T, F_AD, F_PHI, F_L, F_RR, NFIELDS };
+
+struct sm_ctx {
+    int device = 0;
+    int nshard = 1, shard = 0;
+    Geometry g{};
+    LaunchCfg cfg{};
+    hipStream_t own_stream = nullptr, stream = nullptr;
+    ncclComm_t comm = nullptr;
+    bool have_gauge = false;
+    double2 *U = nullptr;          // 2V
+    double2 *ghostU = nullptr;     // Nx: U_t at local t = -1 (lower neighbour's last column)
+    double2 *fields = nullptr;     // NFIELDS * 2V
+    double2 *faces = nullptr;      // 4 * 2Nx per spinor being exchanged (x2 for force)
+    double2 *partials = nullptr;   // 2 * max(nparts)
+    double2 *sums = nullptr;       // 4 complex scratch (allreduce)
+    double *Fbuf = nullptr;        // 2V doubles (force)
+    CGScalars *sc = nullptr;       // device
+    CGScalars *h_sc = nullptr;     // pinned host mirror
+    double2 *h_sums = nullptr;     // pinned host
+    int nparts_dslash = 0, nparts_red = 0;
+    // active CG
+    double cg_mass = 0.0;
+    const double2 *cg_phi = nullptr;
+    double2 *cg_x = nullptr;
+    int cg_active = 0;
+
+    double2 *field(int i) { return fields + (size_t)i * 2 * g.V; }
+};
+
+namespace {
+
+// Neighbour sources for `in`: periodic aliases (1 GPU) or received faces.
+TFaces faces_for(sm_ctx *c, const double2 *in, const double2 *recv_lo, const double2 *recv_hi) {
+    TFaces f;
+    if (c->nshard == 1) {
+        f.lo = in + (c->g.Wt - 1);
+        f.lo_xs = c->g.Wt;
+        f.lo_ps = c->g.V;
+        f.hi = in;
+        f.hi_xs = c->g.Wt;
+        f.hi_ps = c->g.V;
+    } else {
+        f.lo = recv_lo;
+        f.lo_xs = 1;
+        f.lo_ps = c->g.Nx;
+        f.hi = recv_hi;
+        f.hi_xs = 1;
+        f.hi_ps = c->g.Nx;
+    }
+    return f;
+}
+
+double2 *face_buf(sm_ctx *c, int set, int which) {
+    // set 0/1: two independent spinor exchanges; which: 0 send_lo 1 send_hi 2 recv_lo 3 recv_hi
+    return c->faces + (size_t)(set * 4 + which) * 2 * c->g.Nx;
+}
+
+int up_rank(const sm_ctx *c) { return (c->shard + 1) % c->nshard; }
+int down_rank(const sm_ctx *c) { return (c->shard - 1 + c->nshard) % c->nshard; }
+
+// Exchange the t-faces of `field` (both planes) with the t-1 / t+1 shards.
+// My t = Wt-1 column goes up (it is the up-neighbour's t = -1), my t = 0
+// column goes down (the down-neighbour's t = Wt).
+int halo(sm_ctx *c, const double2 *field, int set, TFaces *f) {
+    if (c->nshard == 1) {
+        *f = faces_for(c, field, nullptr, nullptr);
+        return SM_OK;
+    }
+    double2 *slo = face_buf(c, set, 0), *shi = face_buf(c, set, 1);
+    double2 *rlo = face_buf(c, set, 2), *rhi = face_buf(c, set, 3);
+    launch_pack_faces(c->stream, c->g, field, slo, shi);
+    const size_t cnt = (size_t)4 * c->g.Nx;  // doubles: 2 planes x Nx complex
+    NCCL_TRY(ncclGroupStart());
+    NCCL_TRY(ncclSend(shi, cnt, ncclDouble, up_rank(c), c->comm, c->stream));
+    NCCL_TRY(ncclRecv(rlo, cnt, ncclDouble, down_rank(c), c->comm, c->stream));
+    NCCL_TRY(ncclSend(slo, cnt, ncclDouble, down_rank(c), c->comm, c->stream));
+    NCCL_TRY(ncclRecv(rhi, cnt, ncclDouble, up_rank(c), c->comm, c->stream));
+    NCCL_TRY(ncclGroupEnd());
+    *f = faces_for(c, field, rlo, rhi);
+    return SM_OK;
+}
+
+const double2 *loU(sm_ctx *c) { return c->nshard == 1 ? c->U + (c->g.Wt - 1) : c->ghostU; }
+
+int apply(sm_ctx *c, const double2 *in, double2 *out, double mass, int dagger, const double2 *aux,
+          double2 *partials, const CGScalars *skip) {
+    TFaces f;
+    TRY(halo(c, in, 0, &f));
+    launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip);
+    HIP_TRY(hipGetLastError());
+    return SM_OK;
+}
+
+// Global sum of per-block partials into c->sums[slot] (device).
+int global_sum(sm_ctx *c, int nparts, const double2 *part, int slot) {
+    launch_sum_partials(c->stream, nparts, part, c->sums + slot);
+    if (c->nshard > 1)
+        NCCL_TRY(ncclAllReduce(c->sums + slot, c->sums + slot, 2, ncclDouble, ncclSum, c->comm, c->stream));
+    return SM_OK;
+}
+
+int check_ready(sm_ctx *c) {
+    if (!c) return fail(SM_ERR_ARG, "null context");
+    if (!c->have_gauge) return fail(SM_ERR_STATE, "no gauge field uploaded (sm_upload_gauge)");
+    return SM_OK;
+}
+
+int upload_plane_pair(sm_ctx *c, double2 *dst, const double *p0, const double *p1) {
+    const size_t bytes = sizeof(double2) * c->g.V;
+    HIP_TRY(hipMemcpyAsync(dst, p0, bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(dst + c->g.V, p1, bytes, hipMemcpyHostToDevice, c->stream));
+    return SM_OK;
+}
+
+int download_plane_pair(sm_ctx *c, const double2 *src, double *p0, double *p1) {
+    const size_t bytes = sizeof(double2) * c->g.V;
+    HIP_TRY(hipMemcpyAsync(p0, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(p1, src + c->g.V, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SM_OK;
+}
+
+int exchange_ghost_U(sm_ctx *c) {
+    if (c->nshard == 1) return SM_OK;
+    double2 *slo = face_buf(c, 1, 0), *shi = face_buf(c, 1, 1);
+    launch_pack_faces(c->stream, c->g, c->U, slo, shi);
+    // plane 0 of the hi face = U_t(x, Wt-1): the up-neighbour's U_t(x, -1)
+    NCCL_TRY(ncclGroupStart());
+    NCCL_TRY(ncclSend(shi, (size_t)2 * c->g.Nx, ncclDouble, up_rank(c), c->comm, c->stream));
+    NCCL_TRY(ncclRecv(c->ghostU, (size_t)2 * c->g.Nx, ncclDouble, down_rank(c), c->comm, c->stream));
+    NCCL_TRY(ncclGroupEnd());
+    return SM_OK;
+}
+
+}  // namespace
+
+// ============================================================================
+extern "C" {
+
+int sm_abi_version(void) { return 1; }
+const char *sm_last_error(void) { return g_err.c_str(); }
+
+int sm_shard_plan(int Nt, int nshard, int shard, int *t0, int *Wt) {
+    if (Nt <= 0 || nshard <= 0 || shard < 0 || shard >= nshard)
+        return fail(SM_ERR_ARG, "bad shard plan Nt=%d nshard=%d shard=%d", Nt, nshard, shard);
+    // the reference enforces equal blocks (include/mpi_setup.h:14-19)
+    if (Nt % nshard != 0) return fail(SM_ERR_ARG, "Nt=%d not divisible by nshard=%d", Nt, nshard);
+    if (t0) *t0 = shard * (Nt / nshard);
+    if (Wt) *Wt = Nt / nshard;
+    return SM_OK;
+}
+
+void sm_fill_gauge(uint64_t seed, double sigma, int Nt_global, int x0, int nx, int t0, int Wt,
+                   double *U0, double *U1) {
+    sm_fields_fill_gauge(seed, sigma, Nt_global, x0, nx, t0, Wt, U0, U1);
+}
+
+void sm_fill_spinor(uint64_t seed, int Nt_global, int x0, int nx, int t0, int Wt, double *p0,
+                    double *p1) {
+    sm_fields_fill_spinor(seed, Nt_global, x0, nx, t0, Wt, p0, p1);
+}
+
+int sm_conf_write(const char *path, int Nx, int Nt, const double *U0, const double *U1) {
+    FILE *f = fopen(path, "wb");
+    if (!f) return fail(SM_ERR_ARG, "cannot open %s", path);
+    unsigned char rec[28];
+    for (int x = 0; x < Nx; x++)
+        for (int t = 0; t < Nt; t++) {
+            const long n = (long)x * Nt + t;
+            for (int mu = 0; mu < 2; mu++) {
+                const double *U = mu ? U1 : U0;
+                memcpy(rec, &x, 4);
+                memcpy(rec + 4, &t, 4);
+                memcpy(rec + 8, &mu, 4);
+                memcpy(rec + 12, &U[2 * n], 8);
+                memcpy(rec + 20, &U[2 * n + 1], 8);
+                if (fwrite(rec, 1, 28, f) != 28) {
+                    fclose(f);
+                    return fail(SM_ERR_ARG, "short write %s", path);
+                }
+            }
+        }
+    fclose(f);
+    return SM_OK;
+}
+
+int sm_conf_read(const char *path, int Nx, int Nt, double *U0, double *U1) {
+    FILE *f = fopen(path, "rb");
+    if (!f) return fail(SM_ERR_ARG, "cannot open %s", path);
+    unsigned char rec[28];
+    // like readBinary (src/gauge_conf.cpp:515-531) the stored x/t/mu are not
+    // trusted for placement: records are consumed in x, t, mu order.
+    for (int x = 0; x < Nx; x++)
+        for (int t = 0; t < Nt; t++) {
+            const long n = (long)x * Nt + t;
+            for (int mu = 0; mu < 2; mu++) {
+                if (fread(rec, 1, 28, f) != 28) {
+                    fclose(f);
+                    return fail(SM_ERR_ARG, "%s: truncated at site %ld", path, n);
+                }
+                double *U = mu ? U1 : U0;
+                memcpy(&U[2 * n], rec + 12, 8);
+                memcpy(&U[2 * n + 1], rec + 20, 8);
+            }
+        }
+    fclose(f);
+    return SM_OK;
+}
+
+int sm_comm_unique_id(void *id_out, int id_bytes) {
+    if (!id_out || id_bytes < (int)sizeof(ncclUniqueId))
+        return fail(SM_ERR_ARG, "unique id buffer must hold %d bytes", (int)sizeof(ncclUniqueId));
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    memcpy(id_out, &id, sizeof id);
+    return SM_OK;
+}
+
+int sm_create(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device,
+              const void *unique_id) {
+    if (!out) return fail(SM_ERR_ARG, "null out");
+    *out = nullptr;
+    int t0, Wt;
+    if (Nx < 1) return fail(SM_ERR_ARG, "Nx=%d", Nx);
+    TRY(sm_shard_plan(Nt_global, nshard, shard, &t0, &Wt));
+    if (nshard > 1 && !unique_id) return fail(SM_ERR_ARG, "nshard > 1 needs a unique id");
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(SM_ERR_ARG, "device %d of %d", device, ndev);
+    HIP_TRY(hipSetDevice(device));
+    sm_ctx *c = new sm_ctx();
+    c->device = device;
+    c->nshard = nshard;
+    c->shard = shard;
+    c->g.Nx = Nx;
+    c->g.Wt = Wt;
+    c->g.t0 = t0;
+    c->g.Ntg = Nt_global;
+    c->g.V = (long)Nx * Wt;
+    c->cfg = dslash_config(c->g);
+    c->nparts_dslash = dslash_blocks(c->g, c->cfg);
+    c->nparts_red = reduce_blocks(2 * c->g.V);
+    const int np = c->nparts_dslash > c->nparts_red ? c->nparts_dslash : c->nparts_red;
+    const size_t fb = sizeof(double2) * 2 * (size_t)c->g.V;
+    hipError_t e = hipSuccess;
+    auto chk = [&](hipError_t x) { if (e == hipSuccess) e = x; };
+    chk(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+    c->stream = c->own_stream;
+    chk(hipMalloc(&c->U, fb));
+    chk(hipMalloc(&c->ghostU, sizeof(double2) * (size_t)Nx));
+    chk(hipMalloc(&c->fields, fb * NFIELDS));
+    chk(hipMalloc(&c->faces, sizeof(double2) * 2 * (size_t)Nx * 8));
+    chk(hipMalloc(&c->partials, sizeof(double2) * 2 * (size_t)np));
+    chk(hipMalloc(&c->sums, sizeof(double2) * 4));
+    chk(hipMalloc(&c->Fbuf, sizeof(double) * 2 * (size_t)c->g.V));
+    chk(hipMalloc(&c->sc, sizeof(CGScalars)));
+    chk(hipHostMalloc(&c->h_sc, sizeof(CGScalars)));
+    chk(hipHostMalloc(&c->h_sums, sizeof(double2) * 4));
+    if (e == hipSuccess) chk(hipMemset(c->sc, 0, sizeof(CGScalars)));
+    if (e != hipSuccess) {
+        sm_destroy(c);
+        return fail(SM_ERR_HIP, "allocation failed: %s", hipGetErrorString(e));
+    }
+    if (nshard > 1) {
+        ncclUniqueId id;
+        memcpy(&id, unique_id, sizeof id);
+        ncclResult_t r = ncclCommInitRank(&c->comm, nshard, id, shard);
+        if (r != ncclSuccess) {
+            c->comm = nullptr;
+            sm_destroy(c);
+            return fail(SM_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+        }
+    }
+    *out = c;
+    return SM_OK;
+}
+
+int sm_destroy(sm_ctx *c) {
+    if (!c) return SM_OK;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm) ncclCommDestroy(c->comm);
+    void *dev[] = {c->U, c->ghostU, c->fields, c->faces, c->partials, c->sums, c->Fbuf, c->sc};
+    for (void *p : dev)
+        if (p) (void)hipFree(p);
+    if (c->h_sc) (void)hipHostFree(c->h_sc);
+    if (c->h_sums) (void)hipHostFree(c->h_sums);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    return SM_OK;
+}
+
+int sm_set_stream(sm_ctx *c, void *s) {
+    if (!c) return fail(SM_ERR_ARG, "null context");
+    c->stream = s ? (hipStream_t)s : c->own_stream;
+    return SM_OK;
+}
+
+int sm_synchronize(sm_ctx *c) {
+    if (!c) return fail(SM_ERR_ARG, "null context");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SM_OK;
+}
+
+int sm_local_sites(const sm_ctx *c, long *V, int *Nx, int *Wt, int *t0) {
+    if (!c) return fail(SM_ERR_ARG, "null context");
+    if (V) *V = c->g.V;
+    if (Nx) *Nx = c->g.Nx;
+    if (Wt) *Wt = c->g.Wt;
+    if (t0) *t0 = c->g.t0;
+    return SM_OK;
+}
+
+int sm_upload_gauge(sm_ctx *c, const double *U0, const double *U1) {
+    if (!c || !U0 || !U1) return fail(SM_ERR_ARG, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    TRY(upload_plane_pair(c, c->U, U0, U1));
+    TRY(exchange_ghost_U(c));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->have_gauge = true;
+    return SM_OK;
+}
+
+int sm_upload_gauge_dev(sm_ctx *c, const double *U) {
+    if (!c || !U) return fail(SM_ERR_ARG, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpyAsync(c->U, U, sizeof(double2) * 2 * c->g.V, hipMemcpyDeviceToDevice, c->stream));
+    TRY(exchange_ghost_U(c));
+    c->have_gauge = true;
+    return SM_OK;
+}
+
+// ---- device-resident operators -------------------------------------------
+int sm_dirac_dev(sm_ctx *c, const double *in, double *out, double m0, int dagger) {
+    TRY(check_ready(c));
+    return apply(c, (const double2 *)in, (double2 *)out, m0 + 2, dagger ? 1 : 0, nullptr, nullptr, nullptr);
+}
+
+int sm_ddag_dev(sm_ctx *c, const double *in, double *out, double m0) {
+    TRY(check_ready(c));
+    double2 *tmp = c->field(F_TMP);   // the reference's DTEMP
+    TRY(apply(c, (const double2 *)in, tmp, m0 + 2, 1, nullptr, nullptr, nullptr));
+    return apply(c, tmp, (double2 *)out, m0 + 2, 0, nullptr, nullptr, nullptr);
+}
+
+int sm_force_dev(sm_ctx *c, const double *l, const double *r, double *F) {
+    TRY(check_ready(c));
+    TFaces fl, fr;
+    TRY(halo(c, (const double2 *)l, 0, &fl));
+    TRY(halo(c, (const double2 *)r, 1, &fr));
+    launch_force(c->stream, c->g, c->U, (const double2 *)l, (const double2 *)r, fl, fr, F);
+    HIP_TRY(hipGetLastError());
+    return SM_OK;
+}
+
+int sm_dot_dev(sm_ctx *c, const double *a, const double *b, double *out) {
+    if (!c || !out) return fail(SM_ERR_ARG, "null argument");
+    launch_dot_partial(c->stream, 2 * c->g.V, (const double2 *)a, (const double2 *)b, c->partials);
+    TRY(global_sum(c, c->nparts_red, c->partials, 0));
+    HIP_TRY(hipMemcpyAsync(c->h_sums, c->sums, sizeof(double2), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    out[0] = c->h_sums[0].x;
+    out[1] = c->h_sums[0].y;
+    return SM_OK;
+}
+
+// ---- CG on D D^dagger (src/conjugate_gradient.cpp:4-66) ---------------------
+int sm_cg_begin(sm_ctx *c, const double *phi, double *x, double m0, double tol) {
+    TRY(check_ready(c));
+    const long n = 2 * c->g.V;
+    const double2 *ph = (const double2 *)phi;
+    double2 *xx = (double2 *)x;
+    c->cg_mass = m0 + 2;
+    c->cg_phi = ph;
+    c->cg_x = xx;
+    double2 *r = c->field(F_R), *d = c->field(F_D), *Ad = c->field(F_AD), *t = c->field(F_T);
+    if ((const double2 *)xx != ph) launch_copy(c->stream, n, ph, xx);          // x = phi
+    TRY(apply(c, xx, t, c->cg_mass, 1, nullptr, nullptr, nullptr));            // DD^dag x
+    TRY(apply(c, t, Ad, c->cg_mass, 0, nullptr, nullptr, nullptr));
+    double2 *prr = c->partials, *ppp = c->partials + c->nparts_red;
+    launch_cg_init(c->stream, n, ph, Ad, r, d, prr, ppp);                        // r = phi - Ax; d = r
+    if (c->nshard == 1) {
+        launch_cg_finalize_init(c->stream, c->nparts_red, prr, ppp, c->sc, tol);
+    } else {
+        launch_sum_partials(c->stream, c->nparts_red, prr, c->sums);
+        launch_sum_partials(c->stream, c->nparts_red, ppp, c->sums + 1);
+        NCCL_TRY(ncclAllReduce(c->sums, c->sums, 4, ncclDouble, ncclSum, c->comm, c->stream));
+        launch_cg_init_from_sums(c->stream, c->sums, c->sc, tol);
+    }
+    HIP_TRY(hipGetLastError());
+    c->cg_active = 1;
+    return SM_OK;
+}
+
+int sm_cg_iterate(sm_ctx *c, int niter) {
+    TRY(check_ready(c));
+    if (!c->cg_active) return fail(SM_ERR_STATE, "sm_cg_iterate before sm_cg_begin");
+    const long n = 2 * c->g.V;
+    double2 *r = c->field(F_R), *d = c->field(F_D), *Ad = c->field(F_AD), *t = c->field(F_T);
+    double2 *x = c->cg_x;
+    for (int i = 0; i < niter; ++i) {
+        // Ad = D D^dag d, fused partials of <d, Ad>
+        TRY(apply(c, d, t, c->cg_mass, 1, nullptr, nullptr, c->sc));
+        TRY(apply(c, t, Ad, c->cg_mass, 0, d, c->partials, c->sc));
+        if (c->nshard == 1) {
+            launch_cg_alpha(c->stream, c->nparts_dslash, c->partials, c->sc);
+        } else {
+            launch_sum_to_scalar(c->stream, c->nparts_dslash, c->partials, c->sc);
+            NCCL_TRY(ncclAllReduce(&c->sc->sum, &c->sc->sum, 2, ncclDouble, ncclSum, c->comm, c->stream));
+            launch_cg_alpha_from_sum(c->stream, c->sc);
+        }
+        launch_cg_update_xr(c->stream, n, x, r, d, Ad, c->sc, c->partials);
+        if (c->nshard == 1) {
+            launch_cg_beta(c->stream, c->nparts_red, c->partials, c->sc);
+        } else {
+            launch_sum_to_scalar(c->stream, c->nparts_red, c->partials, c->sc);
+            NCCL_TRY(ncclAllReduce(&c->sc->sum, &c->sc->sum, 2, ncclDouble, ncclSum, c->comm, c->stream));
+            launch_cg_beta_from_sum(c->stream, c->sc);
+        }
+        launch_cg_update_d(c->stream, n, d, r, c->sc);
+    }
+    HIP_TRY(hipGetLastError());
+    return SM_OK;
+}
+
+int sm_cg_status(sm_ctx *c, sm_cg_result *res) {
+    if (!c || !res) return fail(SM_ERR_ARG, "null argument");
+    HIP_TRY(hipMemcpyAsync(c->h_sc, c->sc, sizeof(CGScalars), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    res->converged = c->h_sc->converged;
+    res->iterations = c->h_sc->k;
+    res->residual = c->h_sc->err;
+    res->phi_norm = c->h_sc->phi_norm;
+    return SM_OK;
+}
+
+int sm_cg_dev(sm_ctx *c, const double *phi, double *x, double m0, double tol, int max_iter,
+              sm_cg_result *res) {
+    if (!res) return fail(SM_ERR_ARG, "null result");
+    TRY(sm_cg_begin(c, phi, x, m0, tol));
+    // Enqueue iterations in chunks; each CG kernel is a no-op once the device
+    // flag `done` is set, so overshooting a chunk costs only empty launches.
+    int issued = 0, chunk = 4;
+    while (issued < max_iter) {
+        const int nb = (max_iter - issued) < chunk ? (max_iter - issued) : chunk;
+        TRY(sm_cg_iterate(c, nb));
+        issued += nb;
+        TRY(sm_cg_status(c, res));
+        if (res->converged) break;
+        if (chunk < 64) chunk *= 2;
+    }
+    TRY(sm_cg_status(c, res));
+    c->cg_active = 0;
+    return SM_OK;
+}
+
+// ---- host-pointer (drop-in) operators ---------------------------------------
+int sm_dirac(sm_ctx *c, const double *in0, const double *in1, double *out0, double *out1, double m0,
+             int dagger) {
+    TRY(check_ready(c));
+    HIP_TRY(hipSetDevice(c->device));
+    double2 *in = c->field(F_IN), *out = c->field(F_OUT);
+    TRY(upload_plane_pair(c, in, in0, in1));
+    TRY(sm_dirac_dev(c, (const double *)in, (double *)out, m0, dagger));
+    return download_plane_pair(c, out, out0, out1);
+}
+
+int sm_ddag(sm_ctx *c, const double *in0, const double *in1, double *out0, double *out1, double m0) {
+    TRY(check_ready(c));
+    HIP_TRY(hipSetDevice(c->device));
+    double2 *in = c->field(F_IN), *out = c->field(F_OUT);
+    TRY(upload_plane_pair(c, in, in0, in1));
+    TRY(sm_ddag_dev(c, (const double *)in, (double *)out, m0));
+    return download_plane_pair(c, out, out0, out1);
+}
+
+int sm_force(sm_ctx *c, const double *l0, const double *l1, const double *r0, const double *r1,
+             double *F0, double *F1) {
+    TRY(check_ready(c));
+    HIP_TRY(hipSetDevice(c->device));
+    double2 *l = c->field(F_L), *r = c->field(F_RR);
+    TRY(upload_plane_pair(c, l, l0, l1));
+    TRY(upload_plane_pair(c, r, r0, r1));
+    TRY(sm_force_dev(c, (const double *)l, (const double *)r, c->Fbuf));
+    const size_t bytes = sizeof(double) * c->g.V;
+    HIP_TRY(hipMemcpyAsync(F0, c->Fbuf, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(F1, c->Fbuf + c->g.V, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SM_OK;
+}
+
+int sm_dot(sm_ctx *c, const double *a0, const double *a1, const double *b0, const double *b1,
+           double *out) {
+    if (!c) return fail(SM_ERR_ARG, "null context");
+    HIP_TRY(hipSetDevice(c->device));
+    double2 *a = c->field(F_IN), *b = c->field(F_OUT);
+    TRY(upload_plane_pair(c, a, a0, a1));
+    TRY(upload_plane_pair(c, b, b0, b1));
+    return sm_dot_dev(c, (const double *)a, (const double *)b, out);
+}
+
+int sm_cg(sm_ctx *c, const double *phi0, const double *phi1, double *x0, double *x1, double m0,
+          double tol, int max_iter, sm_cg_result *res) {
+    TRY(check_ready(c));
+    HIP_TRY(hipSetDevice(c->device));
+    double2 *phi = c->field(F_PHI), *x = c->field(F_X);
+    TRY(upload_plane_pair(c, phi, phi0, phi1));
+    TRY(sm_cg_dev(c, (const double *)phi, (double *)x, m0, tol, max_iter, res));
+    return download_plane_pair(c, x, x0, x1);
+}
+
+}  // extern "C"

@@ -18,6 +18,9 @@
  */
 #ifndef SM_FIELDS_H
 #define SM_FIELDS_H
+#ifndef _GNU_SOURCE
+#define _GNU_SOURCE 1
+#endif
 #include <math.h>
 #include <stdint.h>
 
@@ -41,8 +44,12 @@ static inline void sm_gauss2(uint64_t seed, uint64_t stream, uint64_t idx,
     double u1 = sm_uniform(seed, 2 * stream, idx);
     double u2 = sm_uniform(seed, 2 * stream + 1, idx);
     double rad = sqrt(-2.0 * log(u1));
-    *g1 = rad * cos(two_pi * u2);
-    *g2 = rad * sin(two_pi * u2);
+    /* glibc sincos explicitly: g++ merges cos+sin into sincos, whose last bit
+     * can differ from separate calls; one entry point for every compiler. */
+    double s, c;
+    sincos(two_pi * u2, &s, &c);
+    *g1 = rad * c;
+    *g2 = rad * s;
 }
 
 static inline void sm_fields_fill_gauge(uint64_t seed, double sigma, int Nt_global, int x0,
@@ -63,8 +70,10 @@ static inline void sm_fields_fill_gauge(uint64_t seed, double sigma, int Nt_glob
                     th = 0.0;
                 }
                 double *U = mu ? U1 : U0;
-                U[2 * n] = cos(th);
-                U[2 * n + 1] = sin(th);
+                double s, c;
+                sincos(th, &s, &c);
+                U[2 * n] = c;
+                U[2 * n + 1] = s;
             }
         }
     }

@@ -1,0 +1,92 @@
+// sm_internal.h -- private interface between the C-ABI host layer (sm_capi.cpp)
+// and the gfx950 kernels (sm_kernels.hip). Not installed; include/sm_hip.h is
+// the public boundary.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sm {
+
+// Device field layout: the reference's SoA spinor, i.e.
+// two planes of complex<double> (double2), plane stride V = Nx*Wt sites,
+// site n = x*Wt + t (t fastest). U: plane 0 = U_t (mu=0), plane 1 = U_x.
+// A face is one t-column for all x, stored [plane][x] (plane stride Nx).
+
+// Neighbour sources of a t-domain. For one GPU (nshard == 1) the "faces" are
+// aliases into the field itself (periodic wrap, xs = Wt); for a t-shard they
+// are the received halo buffers (xs = 1).
+struct TFaces {
+    const double2 *lo;   // psi at local t = -1   : lo[x*lo_xs] (+ lo_ps for plane 1)
+    const double2 *hi;   // psi at local t = Wt   : hi[x*hi_xs] (+ hi_ps for plane 1)
+    long lo_xs, lo_ps, hi_xs, hi_ps;
+};
+
+struct Geometry {
+    int Nx, Wt;          // local block (all x, Wt t-values)
+    int t0, Ntg;         // global t offset of this shard, global Nt
+    long V;              // Nx*Wt
+};
+
+// Scalars of one CG solve, resident on the device (no host round trip per
+// iteration). Mirrors the locals of conjugate_gradient(),
+// src/conjugate_gradient.cpp:6-14.
+struct CGScalars {
+    double2 rn;          // r_norm2 (complex, as the reference keeps it)
+    double2 alpha, beta;
+    double2 sum;         // last globally reduced dot
+    double phi_norm;     // sqrt(Re <phi,phi>)
+    double tol;
+    double err;          // sqrt(Re <r,r>) of the last iteration
+    int k;               // iterations executed
+    int done;            // 1 once converged: every later CG kernel is a no-op
+    int converged;
+    int pad;
+};
+
+enum Epilogue { EPI_NONE = 0, EPI_DOT = 1 };
+
+// ---- launchers (sm_kernels.hip) -------------------------------------------
+struct LaunchCfg {
+    int bt;              // threads per block along t (64/128/256)
+    int xchunk;          // rows marched per block
+};
+LaunchCfg dslash_config(const Geometry &g);
+
+// out = D in (dagger=0) or D^dagger in (dagger=1). EPI_DOT additionally
+// writes per-block partials of sum aux * conj(out) to `partials`.
+void launch_dslash(hipStream_t s, const Geometry &g, const LaunchCfg &c, int dagger,
+                   const double2 *in, double2 *out, const double2 *U, const double2 *loU,
+                   const TFaces &f, double mass, const double2 *aux, double2 *partials,
+                   const CGScalars *skip_if_done);
+int dslash_blocks(const Geometry &g, const LaunchCfg &c);
+
+void launch_force(hipStream_t s, const Geometry &g, const double2 *U, const double2 *l,
+                  const double2 *r, const TFaces &fl, const TFaces &fr, double *F);
+
+int reduce_blocks(long n);   // grid size used by the BLAS-1 reductions of n complex
+void launch_dot_partial(hipStream_t s, long n, const double2 *a, const double2 *b, double2 *partials);
+void launch_sum_partials(hipStream_t s, int nparts, const double2 *partials, double2 *out);
+
+void launch_copy(hipStream_t s, long n, const double2 *src, double2 *dst);
+void launch_cg_init(hipStream_t s, long n, const double2 *phi, const double2 *Ax, double2 *r,
+                    double2 *d, double2 *part_rr, double2 *part_pp);
+void launch_cg_finalize_init(hipStream_t s, int nparts, const double2 *part_rr,
+                             const double2 *part_pp, CGScalars *sc, double tol);
+void launch_cg_alpha(hipStream_t s, int nparts, const double2 *part, CGScalars *sc);
+void launch_cg_update_xr(hipStream_t s, long n, double2 *x, double2 *r, const double2 *d,
+                         const double2 *Ad, CGScalars *sc, double2 *part);
+void launch_cg_beta(hipStream_t s, int nparts, const double2 *part, CGScalars *sc);
+void launch_cg_update_d(hipStream_t s, long n, double2 *d, const double2 *r, const CGScalars *sc);
+
+// Multi-GPU helpers: partial -> local sum (into sc->sum) and global-sum
+// consumers that take the already all-reduced value.
+void launch_sum_to_scalar(hipStream_t s, int nparts, const double2 *part, CGScalars *sc);
+void launch_cg_alpha_from_sum(hipStream_t s, CGScalars *sc);
+void launch_cg_beta_from_sum(hipStream_t s, CGScalars *sc);
+void launch_cg_init_from_sums(hipStream_t s, const double2 *rr_pp, CGScalars *sc, double tol);
+
+// Pack the t = 0 and t = Wt-1 columns (both planes) into contiguous faces.
+void launch_pack_faces(hipStream_t s, const Geometry &g, const double2 *field, double2 *lo_face,
+                       double2 *hi_face);
+
+}  // namespace sm

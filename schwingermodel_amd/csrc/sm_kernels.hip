@@ -1,0 +1,539 @@
+// sm_kernels.hip -- gfx950 (MI355X) kernels for the Wilson-Dirac / CG hot path.
+//
+// Drop-in target: src/dirac_operator.cpp + src/conjugate_gradient.cpp of
+// Fabian2598/SchwingerModel. All arithmetic is IEEE fp64 with NO contraction
+// (-ffp-contract=off + the pragma below) and the reference's evaluation order,
+// so D, D^dagger and the force are bit-identical to the reference (checked in
+// tests/test_gpu_parity.py against tests/golden/).
+//
+// The hot kernel is a marching 5-point stencil: a block owns `bt` consecutive
+// t-columns and marches `xchunk` rows along x, keeping psi(x-1), psi(x),
+// psi(x+1) and U_x(x-1) in registers, so each field row crosses HBM once
+// (plus a 1-row halo per chunk). t-neighbours come from the wave's own
+// coalesced row loads (L1/L2 hits). HBM-bound: 96 B/site algorithmic.
+#include "sm_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace sm {
+
+// ---- complex<double> with std::complex / GCC semantics --------------------
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 cneg(double2 a) { return make_double2(-a.x, -a.y); }
+__device__ __forceinline__ double2 cconj(double2 a) { return make_double2(a.x, -a.y); }
+// GCC expansion of complex multiply: (ac - bd, ad + bc), separately rounded.
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 rmul(double s, double2 a) { return make_double2(s * a.x, s * a.y); }
+
+// libgcc __divdc3 as shipped with GCC 11 (std::complex<double> division).
+__device__ __forceinline__ double2 cdiv(double a, double b, double c, double d) {
+    double denom, ratio, x, y;
+    if (fabs(c) < fabs(d)) {
+        ratio = c / d;
+        denom = (c * ratio) + d;
+        x = ((a * ratio) + b) / denom;
+        y = ((b * ratio) - a) / denom;
+    } else {
+        ratio = d / c;
+        denom = (d * ratio) + c;
+        x = ((b * ratio) + a) / denom;
+        y = (b - (a * ratio)) / denom;
+    }
+    return make_double2(x, y);
+}
+
+#define I_NUM make_double2(0.0, 1.0)      /* I_number, src/dirac_operator.cpp:3 */
+#define MI_NUM make_double2(-0.0, -1.0)   /* -I_number                         */
+
+// One site of D (eq. 34; src/dirac_operator.cpp:31-43) or D^dagger
+// (eqs. 35-36; :255-267). Hop coefficients a,b (forward) c,e (backward)
+// carry the gauge link times the boundary sign, exactly as (U*Sign)*combo.
+template <int DAG>
+__device__ __forceinline__ void dirac_site(double mass, double sr0, double sl0, double2 p0,
+                                           double2 p1, double2 pt0, double2 pt1, double2 px0,
+                                           double2 px1, double2 pm0, double2 pm1, double2 pxm0,
+                                           double2 pxm1, double2 Ut, double2 Ux, double2 Utm,
+                                           double2 Uxm, double2 &s0, double2 &s1) {
+    const double2 one = make_double2(1.0, 0.0);
+    const double2 a = cmul(Ut, make_double2(sr0, 0.0));
+    const double2 b = cmul(Ux, one);
+    const double2 c = cmul(cconj(Utm), make_double2(sl0, 0.0));
+    const double2 e = cmul(cconj(Uxm), one);
+    if (!DAG) {
+        double2 A = cmul(a, csub(pt0, pt1));
+        double2 B = cmul(b, cadd(px0, cmul(I_NUM, px1)));
+        double2 C = cmul(c, cadd(pm0, pm1));
+        double2 E = cmul(e, csub(pxm0, cmul(I_NUM, pxm1)));
+        s0 = csub(rmul(mass, p0), rmul(0.5, cadd(cadd(cadd(A, B), C), E)));
+        A = cmul(a, cadd(cneg(pt0), pt1));
+        B = cmul(b, cadd(cmul(MI_NUM, px0), px1));
+        E = cmul(e, cadd(cmul(I_NUM, pxm0), pxm1));
+        s1 = csub(rmul(mass, p1), rmul(0.5, cadd(cadd(cadd(A, B), C), E)));
+    } else {
+        double2 C = cmul(c, csub(pm0, pm1));
+        double2 E = cmul(e, cadd(pxm0, cmul(I_NUM, pxm1)));
+        double2 A = cmul(a, cadd(pt0, pt1));
+        double2 B = cmul(b, csub(px0, cmul(I_NUM, px1)));
+        s0 = csub(rmul(mass, p0), rmul(0.5, cadd(cadd(cadd(C, E), A), B)));
+        C = cmul(c, cadd(cneg(pm0), pm1));
+        E = cmul(e, cadd(cmul(MI_NUM, pxm0), pxm1));
+        B = cmul(b, cadd(cmul(I_NUM, px0), px1));
+        s1 = csub(rmul(mass, p1), rmul(0.5, cadd(cadd(cadd(C, E), A), B)));
+    }
+}
+
+// Deterministic block sum: wave butterfly, then lane-0 sums waves in order.
+__device__ __forceinline__ double2 block_sum(double2 v, double2 *sh) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        v.x += __shfl_xor(v.x, off);
+        v.y += __shfl_xor(v.y, off);
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) sh[wid] = v;
+    __syncthreads();
+    double2 r = make_double2(0.0, 0.0);
+    if (threadIdx.x == 0) {
+        const int nw = (blockDim.x + 63) >> 6;
+        for (int w = 0; w < nw; ++w) r = cadd(r, sh[w]);
+    }
+    return r;
+}
+
+struct DArgs {
+    const double2 *__restrict__ in;
+    double2 *__restrict__ out;
+    const double2 *__restrict__ U;
+    const double2 *loU;
+    TFaces f;
+    const double2 *aux;
+    double2 *partials;
+    const CGScalars *sc;
+    long V;
+    int Nx, Wt, t0, Ntg, xchunk;
+    double mass;
+};
+
+// Row loads for column t of row x: centre psi, t-neighbours psi(t-1), psi(t+1),
+// links U_t(x,t), U_x(x,t), U_t(x,t-1). Edge lanes read the faces (or the
+// periodic wrap) through a per-lane address select: no divergence.
+struct Row {
+    double2 c0, c1, m0, m1, p0, p1, ut, ux, utm;
+};
+
+__device__ __forceinline__ void load_row(const DArgs &a, int x, int t, Row &r) {
+    const long n = (long)x * a.Wt + t;
+    const double2 *in = a.in;
+    r.c0 = in[n];
+    r.c1 = in[n + a.V];
+    const double2 *pm = (t > 0) ? in + n - 1 : a.f.lo + (long)x * a.f.lo_xs;
+    const long pms = (t > 0) ? a.V : a.f.lo_ps;
+    const double2 *pp = (t + 1 < a.Wt) ? in + n + 1 : a.f.hi + (long)x * a.f.hi_xs;
+    const long pps = (t + 1 < a.Wt) ? a.V : a.f.hi_ps;
+    r.m0 = pm[0];
+    r.m1 = pm[pms];
+    r.p0 = pp[0];
+    r.p1 = pp[pps];
+    r.ut = a.U[n];
+    r.ux = a.U[n + a.V];
+    r.utm = (t > 0) ? a.U[n - 1] : a.loU[(long)x * a.f.lo_xs];
+}
+
+template <int DAG, int EPI>
+__global__ void __launch_bounds__(256) dslash_kernel(DArgs a) {
+    __shared__ double2 sh[4];
+    if (a.sc && a.sc->done) return;  // grid-uniform early exit after CG convergence
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int xbeg = blockIdx.y * a.xchunk;
+    const int xend = min(a.Nx, xbeg + a.xchunk);
+    double2 acc = make_double2(0.0, 0.0);
+    if (t < a.Wt && xbeg < xend) {
+        const int Nx = a.Nx, Wt = a.Wt;
+        const long V = a.V;
+        const double sr0 = (a.t0 + t == a.Ntg - 1) ? -1.0 : 1.0;
+        const double sl0 = (a.t0 + t == 0) ? -1.0 : 1.0;
+        const int xm = (xbeg == 0) ? Nx - 1 : xbeg - 1;
+        const long nm = (long)xm * Wt + t;
+        double2 pxm0 = a.in[nm], pxm1 = a.in[nm + V], uxm = a.U[nm + V];
+        Row cur;
+        load_row(a, xbeg, t, cur);
+        for (int x = xbeg; x < xend; ++x) {
+            const int xp = (x + 1 == Nx) ? 0 : x + 1;
+            const long n = (long)x * Wt + t;
+            Row nxt;
+            if (x + 1 < xend) {
+                load_row(a, xp, t, nxt);
+            } else {
+                const long np = (long)xp * Wt + t;
+                nxt.c0 = a.in[np];
+                nxt.c1 = a.in[np + V];
+            }
+            double2 ax0, ax1;
+            if (EPI == EPI_DOT) {
+                ax0 = a.aux[n];
+                ax1 = a.aux[n + V];
+            }
+            double2 s0, s1;
+            dirac_site<DAG>(a.mass, sr0, sl0, cur.c0, cur.c1, cur.p0, cur.p1, nxt.c0, nxt.c1,
+                            cur.m0, cur.m1, pxm0, pxm1, cur.ut, cur.ux, cur.utm, uxm, s0, s1);
+            a.out[n] = s0;
+            a.out[n + V] = s1;
+            if (EPI == EPI_DOT) {
+                // dot(aux, out) = sum aux * conj(out), include/variables.h:185-188
+                acc = cadd(acc, cmul(ax0, cconj(s0)));
+                acc = cadd(acc, cmul(ax1, cconj(s1)));
+            }
+            pxm0 = cur.c0;
+            pxm1 = cur.c1;
+            uxm = cur.ux;
+            cur = nxt;
+        }
+    }
+    if (EPI == EPI_DOT) {
+        double2 bs = block_sum(acc, sh);
+        if (threadIdx.x == 0) a.partials[(long)blockIdx.y * gridDim.x + blockIdx.x] = bs;
+    }
+}
+
+LaunchCfg dslash_config(const Geometry &g) {
+    LaunchCfg c;
+    c.bt = g.Wt >= 256 ? 256 : (g.Wt >= 128 ? 128 : 64);
+    if (const char *e = getenv("SM_BT")) c.bt = atoi(e);
+    const int tb = (g.Wt + c.bt - 1) / c.bt;
+    int target = 2048;  // blocks: >> 256 CUs, several waves per SIMD
+    if (const char *e = getenv("SM_BLOCKS")) target = atoi(e);
+    int nchunks = (target + tb - 1) / tb;
+    if (nchunks > g.Nx) nchunks = g.Nx;
+    if (nchunks < 1) nchunks = 1;
+    c.xchunk = (g.Nx + nchunks - 1) / nchunks;
+    if (const char *e = getenv("SM_XCHUNK")) c.xchunk = atoi(e);
+    return c;
+}
+
+int dslash_blocks(const Geometry &g, const LaunchCfg &c) {
+    const int tb = (g.Wt + c.bt - 1) / c.bt;
+    const int xb = (g.Nx + c.xchunk - 1) / c.xchunk;
+    return tb * xb;
+}
+
+void launch_dslash(hipStream_t s, const Geometry &g, const LaunchCfg &c, int dagger,
+                   const double2 *in, double2 *out, const double2 *U, const double2 *loU,
+                   const TFaces &f, double mass, const double2 *aux, double2 *partials,
+                   const CGScalars *skip_if_done) {
+    DArgs a;
+    a.in = in;
+    a.out = out;
+    a.U = U;
+    a.loU = loU;
+    a.f = f;
+    a.aux = aux;
+    a.partials = partials;
+    a.sc = skip_if_done;
+    a.V = g.V;
+    a.Nx = g.Nx;
+    a.Wt = g.Wt;
+    a.t0 = g.t0;
+    a.Ntg = g.Ntg;
+    a.xchunk = c.xchunk;
+    a.mass = mass;
+    dim3 grid((g.Wt + c.bt - 1) / c.bt, (g.Nx + c.xchunk - 1) / c.xchunk);
+    dim3 block(c.bt);
+    const bool dot = aux != nullptr;
+    if (!dagger) {
+        if (dot) hipLaunchKernelGGL((dslash_kernel<0, EPI_DOT>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((dslash_kernel<0, EPI_NONE>), grid, block, 0, s, a);
+    } else {
+        if (dot) hipLaunchKernelGGL((dslash_kernel<1, EPI_DOT>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((dslash_kernel<1, EPI_NONE>), grid, block, 0, s, a);
+    }
+}
+
+// ---- fermion force bilinear (eqs. 37-38; src/dirac_operator.cpp:493-506) ----
+struct FArgs {
+    const double2 *U, *l, *r;
+    TFaces fl, fr;   // only .hi is used: forward-only stencil
+    double *F;
+    long V;
+    int Nx, Wt, t0, Ntg;
+};
+
+__global__ void __launch_bounds__(256) force_kernel(FArgs a) {
+    const long V = a.V;
+    for (long n = (long)blockIdx.x * blockDim.x + threadIdx.x; n < V; n += (long)gridDim.x * blockDim.x) {
+        const int x = (int)(n / a.Wt), t = (int)(n - (long)x * a.Wt);
+        const long nx = (long)((x + 1 == a.Nx) ? 0 : x + 1) * a.Wt + t;
+        const double2 SR0 = make_double2((a.t0 + t == a.Ntg - 1) ? -1.0 : 1.0, 0.0);
+        const double2 SR1 = make_double2(1.0, 0.0);
+        const double2 U = a.U[n], W = a.U[n + V];
+        const double2 L0 = a.l[n], L1 = a.l[n + V], R0 = a.r[n], R1 = a.r[n + V];
+        double2 lt0, lt1, rt0, rt1;   // left/right at n + t^
+        if (t + 1 < a.Wt) {
+            lt0 = a.l[n + 1]; lt1 = a.l[n + 1 + V];
+            rt0 = a.r[n + 1]; rt1 = a.r[n + 1 + V];
+        } else {
+            const double2 *pl = a.fl.hi + (long)x * a.fl.hi_xs, *pr = a.fr.hi + (long)x * a.fr.hi_xs;
+            lt0 = pl[0]; lt1 = pl[a.fl.hi_ps];
+            rt0 = pr[0]; rt1 = pr[a.fr.hi_ps];
+        }
+        // mu = 0
+        double2 P = cmul(cmul(cmul(U, SR0), cconj(csub(L0, L1))), csub(rt0, rt1));
+        double2 Q = cmul(cmul(cmul(cconj(U), SR0), cconj(cadd(lt0, lt1))), cadd(R0, R1));
+        a.F[n] = csub(P, Q).y;
+        // mu = 1
+        const double2 lx0 = a.l[nx], lx1 = a.l[nx + V], rx0 = a.r[nx], rx1 = a.r[nx + V];
+        P = cmul(cmul(cmul(W, SR1), csub(cconj(L0), cmul(I_NUM, cconj(L1)))), cadd(rx0, cmul(I_NUM, rx1)));
+        Q = cmul(cmul(cmul(cconj(W), SR1), cadd(cconj(lx0), cmul(I_NUM, cconj(lx1)))),
+                 cadd(cneg(R0), cmul(I_NUM, R1)));
+        a.F[n + V] = cadd(P, Q).y;
+    }
+}
+
+void launch_force(hipStream_t s, const Geometry &g, const double2 *U, const double2 *l,
+                  const double2 *r, const TFaces &fl, const TFaces &fr, double *F) {
+    FArgs a;
+    a.U = U; a.l = l; a.r = r; a.fl = fl; a.fr = fr; a.F = F;
+    a.V = g.V; a.Nx = g.Nx; a.Wt = g.Wt; a.t0 = g.t0; a.Ntg = g.Ntg;
+    long nb = (g.V + 255) / 256;
+    if (nb > 4096) nb = 4096;
+    hipLaunchKernelGGL(force_kernel, dim3((unsigned)nb), dim3(256), 0, s, a);
+}
+
+// ---- BLAS-1 / CG ------------------------------------------------------------
+// All reductions: fixed grid, per-thread grid-stride partial (fixed order),
+// deterministic block sum, then a single-block fixed-order sum of partials.
+// Results are run-to-run reproducible (not the reference's sequential order:
+// CG parity is on the converged solution).
+constexpr int RB = 256;  // threads per reduction block
+
+int reduce_blocks(long n) {
+    long nb = (n + RB * 4 - 1) / (RB * 4);
+    if (nb > 2048) nb = 2048;
+    if (nb < 1) nb = 1;
+    return (int)nb;
+}
+
+__global__ void __launch_bounds__(RB) dot_partial_kernel(long n, const double2 *a, const double2 *b,
+                                                         double2 *part) {
+    __shared__ double2 sh[RB / 64];
+    double2 acc = make_double2(0.0, 0.0);
+    for (long i = (long)blockIdx.x * RB + threadIdx.x; i < n; i += (long)gridDim.x * RB)
+        acc = cadd(acc, cmul(a[i], cconj(b[i])));
+    double2 s = block_sum(acc, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__device__ __forceinline__ double2 sum_partials_block(int nparts, const double2 *part, double2 *sh) {
+    double2 acc = make_double2(0.0, 0.0);
+    for (int i = threadIdx.x; i < nparts; i += RB) acc = cadd(acc, part[i]);
+    return block_sum(acc, sh);
+}
+
+__global__ void __launch_bounds__(RB) sum_partials_kernel(int nparts, const double2 *part, double2 *out) {
+    __shared__ double2 sh[RB / 64];
+    double2 s = sum_partials_block(nparts, part, sh);
+    if (threadIdx.x == 0) *out = s;
+}
+
+void launch_dot_partial(hipStream_t s, long n, const double2 *a, const double2 *b, double2 *partials) {
+    hipLaunchKernelGGL(dot_partial_kernel, dim3(reduce_blocks(n)), dim3(RB), 0, s, n, a, b, partials);
+}
+
+void launch_sum_partials(hipStream_t s, int nparts, const double2 *partials, double2 *out) {
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(RB), 0, s, nparts, partials, out);
+}
+
+__global__ void __launch_bounds__(RB) copy_kernel(long n, const double2 *src, double2 *dst) {
+    for (long i = (long)blockIdx.x * RB + threadIdx.x; i < n; i += (long)gridDim.x * RB) dst[i] = src[i];
+}
+
+void launch_copy(hipStream_t s, long n, const double2 *src, double2 *dst) {
+    hipLaunchKernelGGL(copy_kernel, dim3(reduce_blocks(n)), dim3(RB), 0, s, n, src, dst);
+}
+
+// r = phi - Ax; d = r; partials of <r,r> and <phi,phi>  (src/conjugate_gradient.cpp:19-29)
+__global__ void __launch_bounds__(RB) cg_init_kernel(long n, const double2 *phi, const double2 *Ax,
+                                                     double2 *r, double2 *d, double2 *prr,
+                                                     double2 *ppp) {
+    __shared__ double2 sh[RB / 64];
+    double2 arr = make_double2(0.0, 0.0), app = make_double2(0.0, 0.0);
+    for (long i = (long)blockIdx.x * RB + threadIdx.x; i < n; i += (long)gridDim.x * RB) {
+        const double2 p = phi[i];
+        const double2 ri = csub(p, Ax[i]);
+        r[i] = ri;
+        d[i] = ri;
+        arr = cadd(arr, cmul(ri, cconj(ri)));
+        app = cadd(app, cmul(p, cconj(p)));
+    }
+    double2 s1 = block_sum(arr, sh);
+    __syncthreads();
+    double2 s2 = block_sum(app, sh);
+    if (threadIdx.x == 0) {
+        prr[blockIdx.x] = s1;
+        ppp[blockIdx.x] = s2;
+    }
+}
+
+void launch_cg_init(hipStream_t s, long n, const double2 *phi, const double2 *Ax, double2 *r,
+                    double2 *d, double2 *part_rr, double2 *part_pp) {
+    hipLaunchKernelGGL(cg_init_kernel, dim3(reduce_blocks(n)), dim3(RB), 0, s, n, phi, Ax, r, d,
+                       part_rr, part_pp);
+}
+
+__device__ __forceinline__ void cg_init_scalars(CGScalars *sc, double2 rr, double2 pp, double tol) {
+    sc->rn = rr;
+    sc->phi_norm = sqrt(pp.x);
+    sc->tol = tol;
+    sc->err = 0.0;
+    sc->k = 0;
+    sc->done = 0;
+    sc->converged = 0;
+}
+
+__global__ void __launch_bounds__(RB) cg_finalize_init_kernel(int nparts, const double2 *prr,
+                                                              const double2 *ppp, CGScalars *sc,
+                                                              double tol) {
+    __shared__ double2 sh[RB / 64];
+    double2 rr = sum_partials_block(nparts, prr, sh);
+    __syncthreads();
+    double2 pp = sum_partials_block(nparts, ppp, sh);
+    if (threadIdx.x == 0) cg_init_scalars(sc, rr, pp, tol);
+}
+
+void launch_cg_finalize_init(hipStream_t s, int nparts, const double2 *part_rr,
+                             const double2 *part_pp, CGScalars *sc, double tol) {
+    hipLaunchKernelGGL(cg_finalize_init_kernel, dim3(1), dim3(RB), 0, s, nparts, part_rr, part_pp, sc, tol);
+}
+
+// alpha = r_norm2 / <d, Ad>   (complex division, src/conjugate_gradient.cpp:33)
+__device__ __forceinline__ void cg_alpha_scalar(CGScalars *sc, double2 dAd) {
+    sc->alpha = cdiv(sc->rn.x, sc->rn.y, dAd.x, dAd.y);
+}
+
+__global__ void __launch_bounds__(RB) cg_alpha_kernel(int nparts, const double2 *part, CGScalars *sc) {
+    __shared__ double2 sh[RB / 64];
+    if (sc->done) return;
+    double2 s = sum_partials_block(nparts, part, sh);
+    if (threadIdx.x == 0) cg_alpha_scalar(sc, s);
+}
+
+void launch_cg_alpha(hipStream_t s, int nparts, const double2 *part, CGScalars *sc) {
+    hipLaunchKernelGGL(cg_alpha_kernel, dim3(1), dim3(RB), 0, s, nparts, part, sc);
+}
+
+// x += alpha d; r -= alpha Ad; partial <r,r>   (src/conjugate_gradient.cpp:34-43)
+__global__ void __launch_bounds__(RB) cg_update_xr_kernel(long n, double2 *x, double2 *r,
+                                                          const double2 *d, const double2 *Ad,
+                                                          const CGScalars *sc, double2 *part) {
+    __shared__ double2 sh[RB / 64];
+    if (sc->done) return;
+    const double2 alpha = sc->alpha;
+    double2 acc = make_double2(0.0, 0.0);
+    for (long i = (long)blockIdx.x * RB + threadIdx.x; i < n; i += (long)gridDim.x * RB) {
+        x[i] = cadd(x[i], cmul(alpha, d[i]));
+        const double2 ri = csub(r[i], cmul(alpha, Ad[i]));
+        r[i] = ri;
+        acc = cadd(acc, cmul(ri, cconj(ri)));
+    }
+    double2 s = block_sum(acc, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+void launch_cg_update_xr(hipStream_t s, long n, double2 *x, double2 *r, const double2 *d,
+                         const double2 *Ad, CGScalars *sc, double2 *part) {
+    hipLaunchKernelGGL(cg_update_xr_kernel, dim3(reduce_blocks(n)), dim3(RB), 0, s, n, x, r, d, Ad, sc, part);
+}
+
+// err = sqrt(Re<r,r>); stop test; beta = err^2 / r_norm2   (src/conjugate_gradient.cpp:43-61)
+__device__ __forceinline__ void cg_beta_scalar(CGScalars *sc, double2 rr) {
+    const double err_sqr = rr.x;
+    const double err = sqrt(err_sqr);
+    sc->err = err;
+    sc->k = sc->k + 1;
+    if (err < sc->tol * sc->phi_norm) {
+        sc->done = 1;
+        sc->converged = 1;
+        return;
+    }
+    sc->beta = cdiv(err_sqr, 0.0, sc->rn.x, sc->rn.y);
+    sc->rn = make_double2(err_sqr, 0.0);
+}
+
+__global__ void __launch_bounds__(RB) cg_beta_kernel(int nparts, const double2 *part, CGScalars *sc) {
+    __shared__ double2 sh[RB / 64];
+    if (sc->done) return;
+    double2 s = sum_partials_block(nparts, part, sh);
+    if (threadIdx.x == 0) cg_beta_scalar(sc, s);
+}
+
+void launch_cg_beta(hipStream_t s, int nparts, const double2 *part, CGScalars *sc) {
+    hipLaunchKernelGGL(cg_beta_kernel, dim3(1), dim3(RB), 0, s, nparts, part, sc);
+}
+
+// d = d*beta + r   (src/conjugate_gradient.cpp:54-59)
+__global__ void __launch_bounds__(RB) cg_update_d_kernel(long n, double2 *d, const double2 *r,
+                                                         const CGScalars *sc) {
+    if (sc->done) return;
+    const double2 beta = sc->beta;
+    for (long i = (long)blockIdx.x * RB + threadIdx.x; i < n; i += (long)gridDim.x * RB)
+        d[i] = cadd(cmul(d[i], beta), r[i]);
+}
+
+void launch_cg_update_d(hipStream_t s, long n, double2 *d, const double2 *r, const CGScalars *sc) {
+    hipLaunchKernelGGL(cg_update_d_kernel, dim3(reduce_blocks(n)), dim3(RB), 0, s, n, d, r, sc);
+}
+
+// ---- multi-GPU variants: local partial sum -> (RCCL allreduce) -> scalar ----
+__global__ void __launch_bounds__(RB) sum_to_scalar_kernel(int nparts, const double2 *part, CGScalars *sc) {
+    __shared__ double2 sh[RB / 64];
+    if (sc->done) return;
+    double2 s = sum_partials_block(nparts, part, sh);
+    if (threadIdx.x == 0) sc->sum = s;
+}
+
+void launch_sum_to_scalar(hipStream_t s, int nparts, const double2 *part, CGScalars *sc) {
+    hipLaunchKernelGGL(sum_to_scalar_kernel, dim3(1), dim3(RB), 0, s, nparts, part, sc);
+}
+
+__global__ void cg_alpha_from_sum_kernel(CGScalars *sc) {
+    if (sc->done) return;
+    cg_alpha_scalar(sc, sc->sum);
+}
+__global__ void cg_beta_from_sum_kernel(CGScalars *sc) {
+    if (sc->done) return;
+    cg_beta_scalar(sc, sc->sum);
+}
+__global__ void cg_init_from_sums_kernel(const double2 *rr_pp, CGScalars *sc, double tol) {
+    cg_init_scalars(sc, rr_pp[0], rr_pp[1], tol);
+}
+
+void launch_cg_alpha_from_sum(hipStream_t s, CGScalars *sc) {
+    hipLaunchKernelGGL(cg_alpha_from_sum_kernel, dim3(1), dim3(1), 0, s, sc);
+}
+void launch_cg_beta_from_sum(hipStream_t s, CGScalars *sc) {
+    hipLaunchKernelGGL(cg_beta_from_sum_kernel, dim3(1), dim3(1), 0, s, sc);
+}
+void launch_cg_init_from_sums(hipStream_t s, const double2 *rr_pp, CGScalars *sc, double tol) {
+    hipLaunchKernelGGL(cg_init_from_sums_kernel, dim3(1), dim3(1), 0, s, rr_pp, sc, tol);
+}
+
+// ---- halo faces ---------------------------------------------------------------
+__global__ void pack_faces_kernel(int Nx, int Wt, long V, const double2 *f, double2 *lo, double2 *hi) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= Nx) return;
+    const long a = (long)x * Wt, b = (long)x * Wt + Wt - 1;
+    lo[x] = f[a];
+    lo[x + Nx] = f[a + V];
+    hi[x] = f[b];
+    hi[x + Nx] = f[b + V];
+}
+
+void launch_pack_faces(hipStream_t s, const Geometry &g, const double2 *field, double2 *lo_face,
+                       double2 *hi_face) {
+    hipLaunchKernelGGL(pack_faces_kernel, dim3((g.Nx + 255) / 256), dim3(256), 0, s, g.Nx, g.Wt, g.V,
+                       field, lo_face, hi_face);
+}
+
+}  // namespace sm
