@@ -148,7 +148,10 @@ def main():
     L = sm.Lattice(Nx, Nt, nshard=world, shard=rank, device=local_rank, unique_id=uid)
     V = L.V
     t0 = L.t0
-    stream = torch.cuda.current_stream()
+    # a real (non-null) torch stream: the library launches on it, so the torch
+    # events below bracket exactly the kernels being timed
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     sm.check(sm.lib.sm_set_stream(L.ctx, ctypes.c_void_p(stream.cuda_stream)))
 
     # synthetic inputs of the benchmark shape (counter-based: each shard makes its slice)
