@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--nt-per-gpu", type=int, default=NT_PER_GPU)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("SM_CPU_THREADS", "16")))
+    ap.add_argument("--transport", choices=["rccl", "hosted"], default="rccl",
+                    help="multi-GPU wire: RCCL (production) or the host-staged test transport")
+    ap.add_argument("--device", type=int, default=None, help="override LOCAL_RANK -> GPU mapping")
     return ap.parse_args()
 
 
@@ -125,10 +128,12 @@ def main():
     import torch
     import torch.distributed as dist
     import schwingermodel_amd as sm
+    from schwingermodel_amd import dist as smd
 
     if world > 1:
         dist.init_process_group("gloo")
-    torch.cuda.set_device(local_rank)
+    device = local_rank if args.device is None else args.device
+    torch.cuda.set_device(device)
 
     def barrier():
         torch.cuda.synchronize()
@@ -137,15 +142,14 @@ def main():
 
     Nx, Wt = args.nx, args.nt_per_gpu
     Nt = Wt * world
-    uid = None
-    if world > 1:
-        buf = ctypes.create_string_buffer(128)
-        if rank == 0:
-            sm.check(sm.lib.sm_comm_unique_id(buf, 128))
-        obj = [bytes(buf.raw)]
-        dist.broadcast_object_list(obj, src=0)
-        uid = obj[0]
-    L = sm.Lattice(Nx, Nt, nshard=world, shard=rank, device=local_rank, unique_id=uid)
+    transport = None
+    if world > 1 and args.transport == "hosted":
+        ctx, transport = smd.create_hosted_context(Nx, Nt, device=device)
+        L = sm.Lattice.__new__(sm.Lattice)
+        L.ctx, L.Nx, L.Nt, L.Wt, L.t0, L.V = ctx, Nx, Nt, Wt, rank * Wt, Nx * Wt
+    else:
+        uid = smd.broadcast_unique_id() if world > 1 else None
+        L = sm.Lattice(Nx, Nt, nshard=world, shard=rank, device=device, unique_id=uid)
     V = L.V
     t0 = L.t0
     # a real (non-null) torch stream: the library launches on it, so the torch
@@ -197,9 +201,7 @@ def main():
     t_ev = c0.elapsed_time(c1) / 1e3
     t_local = max(wall, t_ev)
     if world > 1:
-        tt = torch.tensor([t_local, apply_s], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_local, apply_s = float(tt[0]), float(tt[1])
+        t_local, apply_s = smd.max_over_ranks([t_local, apply_s])
         apply_GBps = BYTES_PER_SITE_APPLY * V / apply_s / 1e9
 
     if rank == 0:
@@ -224,6 +226,7 @@ def main():
             "data": "synthetic (counter-based U(1) field theta~N(0,0.2374^2), complex-Gaussian RHS)",
             "config": {"workload": f"CG on D D^dag, {Nx}x{Nt} lattice (beta=5 field, m0={M0}), "
                                    f"t-sharded over {world} GPU(s)",
+                       "transport": args.transport if world > 1 else None,
                        "Nx": Nx, "Nt": Nt, "sites_per_gpu": V, "m0": M0, "sigma": SIGMA_B5,
                        "parallelism": f"t-shard x{world}" + (" (RCCL halos)" if world > 1 else "")},
             "dirac_apply_GBps": round(apply_GBps, 1),

@@ -77,6 +77,9 @@ void sm_fill_spinor(uint64_t seed, int Nt_global, int x0, int nx, int t0, int Wt
 int sm_conf_write(const char *path, int Nx, int Nt, const double *U0, const double *U1);
 int sm_conf_read(const char *path, int Nx, int Nt, double *U0, double *U1);
 
+/* Number of visible GPUs (0 and an error code when there is none). */
+int sm_device_count(int *n);
+
 /* RCCL unique id for nshard > 1 (rank 0 creates, all ranks receive it). */
 int sm_comm_unique_id(void *id_out, int id_bytes);  /* id_bytes >= 128 */
 
@@ -84,6 +87,22 @@ int sm_comm_unique_id(void *id_out, int id_bytes);  /* id_bytes >= 128 */
 /* One context = one t-shard on one GPU. unique_id is ignored for nshard == 1. */
 int sm_create(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device,
               const void *unique_id);
+
+/* Host-staged transport (instead of RCCL) for nshard > 1: halos and scalar
+ * all-reduces go through caller callbacks on host buffers. Used to run several
+ * shards on ONE GPU (tests: torch.distributed gloo) or over a caller's own
+ * MPI; slower than RCCL, same kernels and the same results.
+ *   exchange: send_up -> shard+1 (arrives there as recv_lo),
+ *             send_down -> shard-1 (arrives there as recv_hi); n doubles each.
+ *   allreduce_sum: in-place global sum of n doubles, identical on all shards. */
+typedef struct {
+    void *user;
+    int (*exchange)(void *user, const double *send_down, const double *send_up, double *recv_lo,
+                    double *recv_hi, long n);
+    int (*allreduce_sum)(void *user, double *buf, long n);
+} sm_host_transport;
+int sm_create_hosted(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device,
+                     const sm_host_transport *transport);
 int sm_destroy(sm_ctx *ctx);
 /* Launch on a caller stream (a hipStream_t, e.g. torch's current stream);
  * NULL restores the context's own stream. */

@@ -36,7 +36,9 @@ def _load():
         "sm_conf_write": ([ctypes.c_char_p, ci, ci, vp, vp], ci),
         "sm_conf_read": ([ctypes.c_char_p, ci, ci, vp, vp], ci),
         "sm_comm_unique_id": ([vp, ci], ci),
+        "sm_device_count": ([ctypes.POINTER(ci)], ci),
         "sm_create": ([ctypes.POINTER(vp), ci, ci, ci, ci, ci, vp], ci),
+        "sm_create_hosted": ([ctypes.POINTER(vp), ci, ci, ci, ci, ci, vp], ci),
         "sm_destroy": ([vp], ci),
         "sm_set_stream": ([vp, vp], ci),
         "sm_synchronize": ([vp], ci),

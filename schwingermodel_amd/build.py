@@ -58,6 +58,8 @@ def build_oracle(with_reference=None):
         with_reference = os.path.isdir("/root/reference/src")
     if with_reference and shutil.which("g++"):
         subprocess.run(["make", "-s", "-C", oracle_dir, "ref"], check=True)
+        # the reference's own driver code linked against our drop-in shim
+        subprocess.run(["make", "-s", "-C", oracle_dir, "dropin"], check=True)
 
 
 if __name__ == "__main__":

@@ -67,6 +67,10 @@ struct sm_ctx {
     LaunchCfg cfg{};
     hipStream_t own_stream = nullptr, stream = nullptr;
     ncclComm_t comm = nullptr;
+    bool hosted = false;            // host-callback transport instead of RCCL
+    sm_host_transport tr{};
+    double *h_face = nullptr;       // pinned: send_lo, send_hi, recv_lo, recv_hi (4 x 4Nx doubles)
+    double *h_red = nullptr;        // pinned: all-reduce staging (8 doubles)
     bool have_gauge = false;
     double2 *U = nullptr;          // 2V
     double2 *ghostU = nullptr;     // Nx: U_t at local t = -1 (lower neighbour's last column)
@@ -121,7 +125,47 @@ int down_rank(const sm_ctx *c) { return (c->shard - 1 + c->nshard) % c->nshard; 
 
 // Exchange the t-faces of `field` (both planes) with the t-1 / t+1 shards.
 // My t = Wt-1 column goes up (it is the up-neighbour's t = -1), my t = 0
-// column goes down (the down-neighbour's t = Wt).
+// column goes down (the down-neighbour's t = Wt). The face buffers are
+// [plane][x], 4*Nx doubles.
+int exchange_faces(sm_ctx *c, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi) {
+    const size_t cnt = (size_t)4 * c->g.Nx;
+    if (c->hosted) {
+        double *h = c->h_face;
+        HIP_TRY(hipMemcpyAsync(h, slo, cnt * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(h + cnt, shi, cnt * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (c->tr.exchange(c->tr.user, h, h + cnt, h + 2 * cnt, h + 3 * cnt, (long)cnt) != 0)
+            return fail(SM_ERR_ARG, "host transport exchange failed");
+        HIP_TRY(hipMemcpyAsync(rlo, h + 2 * cnt, cnt * 8, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(rhi, h + 3 * cnt, cnt * 8, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));  // staging buffers are reused
+        return SM_OK;
+    }
+    NCCL_TRY(ncclGroupStart());
+    NCCL_TRY(ncclSend(shi, cnt, ncclDouble, up_rank(c), c->comm, c->stream));
+    NCCL_TRY(ncclRecv(rlo, cnt, ncclDouble, down_rank(c), c->comm, c->stream));
+    NCCL_TRY(ncclSend(slo, cnt, ncclDouble, down_rank(c), c->comm, c->stream));
+    NCCL_TRY(ncclRecv(rhi, cnt, ncclDouble, up_rank(c), c->comm, c->stream));
+    NCCL_TRY(ncclGroupEnd());
+    return SM_OK;
+}
+
+// In-place global sum of n doubles resident on the device.
+int allreduce_dev(sm_ctx *c, double *dev, int n) {
+    if (c->nshard == 1) return SM_OK;
+    if (c->hosted) {
+        HIP_TRY(hipMemcpyAsync(c->h_red, dev, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (c->tr.allreduce_sum(c->tr.user, c->h_red, n) != 0)
+            return fail(SM_ERR_ARG, "host transport allreduce failed");
+        HIP_TRY(hipMemcpyAsync(dev, c->h_red, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return SM_OK;
+    }
+    NCCL_TRY(ncclAllReduce(dev, dev, n, ncclDouble, ncclSum, c->comm, c->stream));
+    return SM_OK;
+}
+
 int halo(sm_ctx *c, const double2 *field, int set, TFaces *f) {
     if (c->nshard == 1) {
         *f = faces_for(c, field, nullptr, nullptr);
@@ -130,13 +174,7 @@ int halo(sm_ctx *c, const double2 *field, int set, TFaces *f) {
     double2 *slo = face_buf(c, set, 0), *shi = face_buf(c, set, 1);
     double2 *rlo = face_buf(c, set, 2), *rhi = face_buf(c, set, 3);
     launch_pack_faces(c->stream, c->g, field, slo, shi);
-    const size_t cnt = (size_t)4 * c->g.Nx;  // doubles: 2 planes x Nx complex
-    NCCL_TRY(ncclGroupStart());
-    NCCL_TRY(ncclSend(shi, cnt, ncclDouble, up_rank(c), c->comm, c->stream));
-    NCCL_TRY(ncclRecv(rlo, cnt, ncclDouble, down_rank(c), c->comm, c->stream));
-    NCCL_TRY(ncclSend(slo, cnt, ncclDouble, down_rank(c), c->comm, c->stream));
-    NCCL_TRY(ncclRecv(rhi, cnt, ncclDouble, up_rank(c), c->comm, c->stream));
-    NCCL_TRY(ncclGroupEnd());
+    TRY(exchange_faces(c, slo, shi, rlo, rhi));
     *f = faces_for(c, field, rlo, rhi);
     return SM_OK;
 }
@@ -155,9 +193,7 @@ int apply(sm_ctx *c, const double2 *in, double2 *out, double mass, int dagger, c
 // Global sum of per-block partials into c->sums[slot] (device).
 int global_sum(sm_ctx *c, int nparts, const double2 *part, int slot) {
     launch_sum_partials(c->stream, nparts, part, c->sums + slot);
-    if (c->nshard > 1)
-        NCCL_TRY(ncclAllReduce(c->sums + slot, c->sums + slot, 2, ncclDouble, ncclSum, c->comm, c->stream));
-    return SM_OK;
+    return allreduce_dev(c, (double *)(c->sums + slot), 2);
 }
 
 int check_ready(sm_ctx *c) {
@@ -183,13 +219,12 @@ int download_plane_pair(sm_ctx *c, const double2 *src, double *p0, double *p1) {
 
 int exchange_ghost_U(sm_ctx *c) {
     if (c->nshard == 1) return SM_OK;
+    // U_t(x, Wt-1) (plane 0 of my hi face) is the up-neighbour's U_t(x, -1)
     double2 *slo = face_buf(c, 1, 0), *shi = face_buf(c, 1, 1);
+    double2 *rlo = face_buf(c, 1, 2), *rhi = face_buf(c, 1, 3);
     launch_pack_faces(c->stream, c->g, c->U, slo, shi);
-    // plane 0 of the hi face = U_t(x, Wt-1): the up-neighbour's U_t(x, -1)
-    NCCL_TRY(ncclGroupStart());
-    NCCL_TRY(ncclSend(shi, (size_t)2 * c->g.Nx, ncclDouble, up_rank(c), c->comm, c->stream));
-    NCCL_TRY(ncclRecv(c->ghostU, (size_t)2 * c->g.Nx, ncclDouble, down_rank(c), c->comm, c->stream));
-    NCCL_TRY(ncclGroupEnd());
+    TRY(exchange_faces(c, slo, shi, rlo, rhi));
+    HIP_TRY(hipMemcpyAsync(c->ghostU, rlo, sizeof(double2) * c->g.Nx, hipMemcpyDeviceToDevice, c->stream));
     return SM_OK;
 }
 
@@ -268,6 +303,13 @@ int sm_conf_read(const char *path, int Nx, int Nt, double *U0, double *U1) {
     return SM_OK;
 }
 
+int sm_device_count(int *n) {
+    if (!n) return fail(SM_ERR_ARG, "null argument");
+    *n = 0;
+    HIP_TRY(hipGetDeviceCount(n));
+    return SM_OK;
+}
+
 int sm_comm_unique_id(void *id_out, int id_bytes) {
     if (!id_out || id_bytes < (int)sizeof(ncclUniqueId))
         return fail(SM_ERR_ARG, "unique id buffer must hold %d bytes", (int)sizeof(ncclUniqueId));
@@ -277,14 +319,15 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
     return SM_OK;
 }
 
-int sm_create(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device,
-              const void *unique_id) {
+static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device,
+                         const void *unique_id, const sm_host_transport *tr) {
     if (!out) return fail(SM_ERR_ARG, "null out");
     *out = nullptr;
     int t0, Wt;
     if (Nx < 1) return fail(SM_ERR_ARG, "Nx=%d", Nx);
     TRY(sm_shard_plan(Nt_global, nshard, shard, &t0, &Wt));
-    if (nshard > 1 && !unique_id) return fail(SM_ERR_ARG, "nshard > 1 needs a unique id");
+    if (nshard > 1 && !unique_id && !tr) return fail(SM_ERR_ARG, "nshard > 1 needs a unique id or a transport");
+    if (tr && (!tr->exchange || !tr->allreduce_sum)) return fail(SM_ERR_ARG, "incomplete host transport");
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return fail(SM_ERR_ARG, "device %d of %d", device, ndev);
@@ -317,12 +360,17 @@ int sm_create(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int de
     chk(hipMalloc(&c->sc, sizeof(CGScalars)));
     chk(hipHostMalloc(&c->h_sc, sizeof(CGScalars)));
     chk(hipHostMalloc(&c->h_sums, sizeof(double2) * 4));
+    chk(hipHostMalloc(&c->h_face, sizeof(double) * 16 * (size_t)Nx));
+    chk(hipHostMalloc(&c->h_red, sizeof(double) * 8));
     if (e == hipSuccess) chk(hipMemset(c->sc, 0, sizeof(CGScalars)));
     if (e != hipSuccess) {
         sm_destroy(c);
         return fail(SM_ERR_HIP, "allocation failed: %s", hipGetErrorString(e));
     }
-    if (nshard > 1) {
+    if (nshard > 1 && tr) {
+        c->hosted = true;
+        c->tr = *tr;
+    } else if (nshard > 1) {
         ncclUniqueId id;
         memcpy(&id, unique_id, sizeof id);
         ncclResult_t r = ncclCommInitRank(&c->comm, nshard, id, shard);
@@ -336,6 +384,17 @@ int sm_create(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int de
     return SM_OK;
 }
 
+int sm_create(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device,
+              const void *unique_id) {
+    return create_common(out, Nx, Nt_global, nshard, shard, device, unique_id, nullptr);
+}
+
+int sm_create_hosted(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device,
+                     const sm_host_transport *transport) {
+    if (!transport) return fail(SM_ERR_ARG, "null transport");
+    return create_common(out, Nx, Nt_global, nshard, shard, device, nullptr, transport);
+}
+
 int sm_destroy(sm_ctx *c) {
     if (!c) return SM_OK;
     (void)hipSetDevice(c->device);
@@ -346,6 +405,8 @@ int sm_destroy(sm_ctx *c) {
         if (p) (void)hipFree(p);
     if (c->h_sc) (void)hipHostFree(c->h_sc);
     if (c->h_sums) (void)hipHostFree(c->h_sums);
+    if (c->h_face) (void)hipHostFree(c->h_face);
+    if (c->h_red) (void)hipHostFree(c->h_red);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
     return SM_OK;
@@ -445,7 +506,7 @@ int sm_cg_begin(sm_ctx *c, const double *phi, double *x, double m0, double tol) 
     } else {
         launch_sum_partials(c->stream, c->nparts_red, prr, c->sums);
         launch_sum_partials(c->stream, c->nparts_red, ppp, c->sums + 1);
-        NCCL_TRY(ncclAllReduce(c->sums, c->sums, 4, ncclDouble, ncclSum, c->comm, c->stream));
+        TRY(allreduce_dev(c, (double *)c->sums, 4));
         launch_cg_init_from_sums(c->stream, c->sums, c->sc, tol);
     }
     HIP_TRY(hipGetLastError());
@@ -467,7 +528,7 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
             launch_cg_alpha(c->stream, c->nparts_dslash, c->partials, c->sc);
         } else {
             launch_sum_to_scalar(c->stream, c->nparts_dslash, c->partials, c->sc);
-            NCCL_TRY(ncclAllReduce(&c->sc->sum, &c->sc->sum, 2, ncclDouble, ncclSum, c->comm, c->stream));
+            TRY(allreduce_dev(c, (double *)&c->sc->sum, 2));
             launch_cg_alpha_from_sum(c->stream, c->sc);
         }
         launch_cg_update_xr(c->stream, n, x, r, d, Ad, c->sc, c->partials);
@@ -475,7 +536,7 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
             launch_cg_beta(c->stream, c->nparts_red, c->partials, c->sc);
         } else {
             launch_sum_to_scalar(c->stream, c->nparts_red, c->partials, c->sc);
-            NCCL_TRY(ncclAllReduce(&c->sc->sum, &c->sc->sum, 2, ncclDouble, ncclSum, c->comm, c->stream));
+            TRY(allreduce_dev(c, (double *)&c->sc->sum, 2));
             launch_cg_beta_from_sum(c->stream, c->sc);
         }
         launch_cg_update_d(c->stream, n, d, r, c->sc);

@@ -1,0 +1,141 @@
+#!/usr/bin/env python3
+"""One rank of a t-sharded multi-process check (launched by tests/test_dist_*.py).
+
+    RANK=r WORLD_SIZE=P MASTER_ADDR=127.0.0.1 MASTER_PORT=... \
+        python tests/dist_worker.py <mode> <fixture> <result.json>
+
+mode "oracle" (CPU, gloo): every rank applies the ORACLE's local operator to its
+    t-shard with faces exchanged by schwingermodel_amd.dist.exchange_faces (the
+    protocol of the GPU path) and the geometry of sm_shard_plan; rank 0 checks
+    the gathered result bit-for-bit against the reference's golden vectors.
+mode "gpu" (one GPU shared by all ranks, gloo host transport): every rank runs
+    the HIP kernels on its shard through sm_create_hosted (same kernels, face
+    packing, ghost links, sign ownership and scalar reductions as the RCCL
+    path); rank 0 checks D / D^dag / D D^dag / force bitwise and CG to 1e-12.
+"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, REPO)
+sys.path.insert(0, HERE)
+
+
+def shard_field(flat, Nx, Nt, t0, Wt):
+    """Global two-plane interleaved field -> this shard's block (same layout)."""
+    S = Nx * Nt
+    out = []
+    for p in range(2):
+        plane = flat[2 * S * p: 2 * S * (p + 1)].view(np.complex128).reshape(Nx, Nt)
+        out.append(np.ascontiguousarray(plane[:, t0:t0 + Wt]).reshape(-1))
+    return out  # [mu0, mu1] complex arrays of Nx*Wt
+
+
+def unshard(blocks, Nx, Nt, Wt, dtype):
+    planes = []
+    for p in range(2):
+        g = np.concatenate([b[p].reshape(Nx, Wt) for b in blocks], axis=1)
+        planes.append(g.reshape(-1).view(np.float64) if dtype == complex else g.reshape(-1))
+    return np.concatenate(planes)
+
+
+def faces(mu0, mu1, Nx, Wt):
+    """[plane][x] faces of columns t = 0 (lo) and t = Wt-1 (hi), 4*Nx doubles each."""
+    a0, a1 = mu0.reshape(Nx, Wt), mu1.reshape(Nx, Wt)
+    lo = np.concatenate([a0[:, 0], a1[:, 0]]).view(np.float64).copy()
+    hi = np.concatenate([a0[:, Wt - 1], a1[:, Wt - 1]]).view(np.float64).copy()
+    return lo, hi
+
+
+def main():
+    mode, name, result_path = sys.argv[1], sys.argv[2], sys.argv[3]
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    from conftest import bits_equal, load_fixture
+    import schwingermodel_amd as sm
+    from schwingermodel_amd import dist as smd
+
+    meta, a = load_fixture(name)
+    Nx, Nt, m0 = meta["Nx"], meta["Nt"], meta["m0"]
+    t0, Wt = ctypes.c_int(), ctypes.c_int()
+    sm.check(sm.lib.sm_shard_plan(Nt, world, rank, ctypes.byref(t0), ctypes.byref(Wt)))
+    t0, Wt = t0.value, Wt.value
+    V = Nx * Wt
+    U = shard_field(a["U"], Nx, Nt, t0, Wt)
+    psi = shard_field(a["psi"], Nx, Nt, t0, Wt)
+    chi = shard_field(a["chi"], Nx, Nt, t0, Wt)
+    P = lambda x: ctypes.c_void_p(x.ctypes.data)  # noqa: E731
+    local = {}
+
+    if mode == "oracle":
+        o = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
+        vp, ci, cd = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+        o.oracle_dirac_local.argtypes = [ci, ci, ci, ci] + [vp] * 11 + [cd, ci]
+        # ghost link U_t(x, -1): the down-neighbour's U_t(x, Wt-1)
+        ulo, uhi = faces(U[0], U[1], Nx, Wt)
+        g_lo, g_hi = np.empty(4 * Nx), np.empty(4 * Nx)
+        smd.exchange_faces(ulo, uhi, g_lo, g_hi)
+        for key, src, dag in (("ref_Dpsi", psi, 0), ("ref_Ddagchi", chi, 1)):
+            lo, hi = faces(src[0], src[1], Nx, Wt)
+            r_lo, r_hi = np.empty(4 * Nx), np.empty(4 * Nx)
+            smd.exchange_faces(lo, hi, r_lo, r_hi)
+            out0, out1 = np.empty(V, complex), np.empty(V, complex)
+            o.oracle_dirac_local(Nx, Wt, t0, Nt, P(U[0]), P(U[1]), P(src[0]), P(src[1]),
+                                 P(r_lo[:2 * Nx]), P(r_lo[2 * Nx:]), P(g_lo[:2 * Nx]),
+                                 P(r_hi[:2 * Nx]), P(r_hi[2 * Nx:]), P(out0), P(out1), m0, dag)
+            local[key] = (out0, out1)
+    else:
+        ctx, tr = smd.create_hosted_context(Nx, Nt, device=int(os.environ.get("SM_DEVICE", "0")))
+        sm.check(sm.lib.sm_upload_gauge(ctx, P(U[0]), P(U[1])))
+        for key, src, fn in (("ref_Dpsi", psi, 0), ("ref_Ddagchi", chi, 1), ("ref_DDdagpsi", psi, 2)):
+            out0, out1 = np.empty(V, complex), np.empty(V, complex)
+            if fn < 2:
+                sm.check(sm.lib.sm_dirac(ctx, P(src[0]), P(src[1]), P(out0), P(out1), m0, fn))
+            else:
+                sm.check(sm.lib.sm_ddag(ctx, P(src[0]), P(src[1]), P(out0), P(out1), m0))
+            local[key] = (out0, out1)
+        F0, F1 = np.empty(V), np.empty(V)
+        sm.check(sm.lib.sm_force(ctx, P(psi[0]), P(psi[1]), P(chi[0]), P(chi[1]), P(F0), P(F1)))
+        local["ref_force"] = (F0, F1)
+        x0, x1 = np.empty(V, complex), np.empty(V, complex)
+        res = sm.CGResult()
+        sm.check(sm.lib.sm_cg(ctx, P(psi[0]), P(psi[1]), P(x0), P(x1), m0, 1e-10, 10000, ctypes.byref(res)))
+        local["ref_cgx"] = (x0, x1)
+        local["cg"] = (res.converged, res.iterations)
+        z = np.empty(2)
+        sm.check(sm.lib.sm_dot(ctx, P(chi[0]), P(chi[1]), P(psi[0]), P(psi[1]), P(z)))
+        local["dot"] = tuple(z)
+        sm.lib.sm_destroy(ctx)
+
+    gathered = [None] * world
+    dist.all_gather_object(gathered, local)
+    if rank == 0:
+        report = {"world": world, "mode": mode, "fixture": name, "checks": {}}
+        for key in ("ref_Dpsi", "ref_Ddagchi", "ref_DDdagpsi", "ref_force", "ref_cgx"):
+            if key not in local:
+                continue
+            dtype = float if key == "ref_force" else complex
+            g = unshard([d[key] for d in gathered], Nx, Nt, Wt, dtype)
+            if key == "ref_cgx":
+                report["checks"][key] = float(np.linalg.norm(g - a[key]) / np.linalg.norm(a[key]))
+            else:
+                report["checks"][key] = bool(bits_equal(g, a[key]))
+        if "cg" in local:
+            report["cg_iters"] = [d["cg"][1] for d in gathered]
+            report["cg_converged"] = [d["cg"][0] for d in gathered]
+            report["ref_cg_iters"] = meta["cg_iters"]
+            report["dots"] = [list(d["dot"]) for d in gathered]
+        with open(result_path, "w") as f:
+            json.dump(report, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
