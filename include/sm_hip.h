@@ -108,6 +108,17 @@ int sm_destroy(sm_ctx *ctx);
  * NULL restores the context's own stream. */
 int sm_set_stream(sm_ctx *ctx, void *hip_stream);
 int sm_synchronize(sm_ctx *ctx);
+/* Launch-geometry knobs of the stencil kernels (tuning / A-B benchmarks):
+ * bt = t-columns per block (64, 128, 256), xchunk = rows marched per block,
+ * xcd_remap = 1 maps the tiles one XCD receives to x-adjacent tiles,
+ * variant selects the stencil code variant. Values <= 0 (< 0 for xcd_remap
+ * and variant) keep the current setting. */
+int sm_tune(sm_ctx *ctx, int bt, int xchunk, int xcd_remap, int variant);
+/* Streaming-bandwidth ceiling on the ctx stream (measured roofline reference):
+ * out = a + b (two_reads = 1: the stencil's 2-read/1-write byte mix) or
+ * out = a, over n complex<double> device elements. */
+int sm_bench_stream(sm_ctx *ctx, int two_reads, long n, const double *a, const double *b, double *out,
+                    int blocks);
 int sm_local_sites(const sm_ctx *ctx, long *V, int *Nx, int *Wt, int *t0);
 
 /* Gauge field (host / device). Must precede every operator call; re-upload

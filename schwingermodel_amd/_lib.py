@@ -42,6 +42,8 @@ def _load():
         "sm_destroy": ([vp], ci),
         "sm_set_stream": ([vp, vp], ci),
         "sm_synchronize": ([vp], ci),
+        "sm_tune": ([vp, ci, ci, ci, ci], ci),
+        "sm_bench_stream": ([vp, ci, cl, vp, vp, vp, ci], ci),
         "sm_local_sites": ([vp, ctypes.POINTER(cl), ctypes.POINTER(ci), ctypes.POINTER(ci),
                             ctypes.POINTER(ci)], ci),
         "sm_upload_gauge": ([vp, vp, vp], ci),

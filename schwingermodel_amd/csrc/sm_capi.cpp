@@ -344,7 +344,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     c->cfg = dslash_config(c->g);
     c->nparts_dslash = dslash_blocks(c->g, c->cfg);
     c->nparts_red = reduce_blocks(2 * c->g.V);
-    const int np = c->nparts_dslash > c->nparts_red ? c->nparts_dslash : c->nparts_red;
+    const int np = kMaxPartials;
     const size_t fb = sizeof(double2) * 2 * (size_t)c->g.V;
     hipError_t e = hipSuccess;
     auto chk = [&](hipError_t x) { if (e == hipSuccess) e = x; };
@@ -409,6 +409,29 @@ int sm_destroy(sm_ctx *c) {
     if (c->h_red) (void)hipHostFree(c->h_red);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
+    return SM_OK;
+}
+
+int sm_tune(sm_ctx *c, int bt, int xchunk, int xcd_remap, int variant) {
+    if (!c) return fail(SM_ERR_ARG, "null context");
+    LaunchCfg cfg = c->cfg;
+    if (bt > 0) cfg.bt = bt;
+    if (xchunk > 0) cfg.xchunk = xchunk;
+    if (xcd_remap >= 0) cfg.xcd_remap = xcd_remap;
+    if (variant >= 0) cfg.variant = variant;
+    if (cfg.bt % 64 || cfg.bt > 256 || cfg.xchunk < 1)
+        return fail(SM_ERR_ARG, "bad launch config bt=%d xchunk=%d", cfg.bt, cfg.xchunk);
+    if (dslash_blocks(c->g, cfg) > kMaxPartials) return fail(SM_ERR_ARG, "too many blocks");
+    c->cfg = cfg;
+    c->nparts_dslash = dslash_blocks(c->g, cfg);
+    return SM_OK;
+}
+
+int sm_bench_stream(sm_ctx *c, int two_reads, long n, const double *a, const double *b, double *out,
+                    int blocks) {
+    if (!c || !a || !out || (two_reads && !b)) return fail(SM_ERR_ARG, "null argument");
+    launch_stream(c->stream, two_reads, n, (const double2 *)a, (const double2 *)b, (double2 *)out, blocks);
+    HIP_TRY(hipGetLastError());
     return SM_OK;
 }
 

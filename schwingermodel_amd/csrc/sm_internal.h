@@ -49,7 +49,10 @@ enum Epilogue { EPI_NONE = 0, EPI_DOT = 1 };
 struct LaunchCfg {
     int bt;              // threads per block along t (64/128/256)
     int xchunk;          // rows marched per block
+    int xcd_remap;       // 1: consecutive tiles of one XCD are x-adjacent (L2 reuse of halo rows)
+    int variant;         // dslash code variant (sm_kernels.hip)
 };
+constexpr int kMaxPartials = 1 << 16;
 LaunchCfg dslash_config(const Geometry &g);
 
 // out = D in (dagger=0) or D^dagger in (dagger=1). EPI_DOT additionally
@@ -84,6 +87,9 @@ void launch_sum_to_scalar(hipStream_t s, int nparts, const double2 *part, CGScal
 void launch_cg_alpha_from_sum(hipStream_t s, CGScalars *sc);
 void launch_cg_beta_from_sum(hipStream_t s, CGScalars *sc);
 void launch_cg_init_from_sums(hipStream_t s, const double2 *rr_pp, CGScalars *sc, double tol);
+
+void launch_stream(hipStream_t s, int two, long n, const double2 *a, const double2 *b, double2 *out,
+                   int blocks);
 
 // Pack the t = 0 and t = Wt-1 columns (both planes) into contiguous faces.
 void launch_pack_faces(hipStream_t s, const Geometry &g, const double2 *field, double2 *lo_face,

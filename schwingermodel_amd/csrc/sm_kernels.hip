@@ -114,40 +114,84 @@ struct DArgs {
     const CGScalars *sc;
     long V;
     int Nx, Wt, t0, Ntg, xchunk;
+    int TB, XB, xcd_remap;   // tile grid (t-blocks x x-chunks), 1-D launch
     double mass;
 };
 
+// Linear block id -> (t-block, x-chunk). With xcd_remap the ids that the
+// dispatcher deals to one XCD (L, L+8, L+16, ...: round-robin, speed only,
+// MI355X_MICROARCH.md) get a contiguous range of tiles, so the x-halo rows and
+// t-edge lines shared by neighbouring tiles are L2 hits on that XCD.
+__device__ __forceinline__ void block_tile(int L, int TB, int XB, int remap, int &tb, int &xc) {
+    int w = L;
+    if (remap) {
+        const int n = TB * XB, q = n >> 3, r = n & 7, xcd = L & 7;
+        w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
+    }
+    tb = w % TB;
+    xc = w / TB;
+}
+
 // Row loads for column t of row x: centre psi, t-neighbours psi(t-1), psi(t+1),
 // links U_t(x,t), U_x(x,t), U_t(x,t-1). Edge lanes read the faces (or the
-// periodic wrap) through a per-lane address select: no divergence.
+// periodic wrap) through a per-lane POINTER select followed by one
+// unconditional load: no branch, so the compiler can keep the next row's
+// loads in flight across the loop back-edge (a divergent `c ? load : load`
+// becomes a branch and a vmcnt(0) drain per row).
 struct Row {
     double2 c0, c1, m0, m1, p0, p1, ut, ux, utm;
 };
 
-__device__ __forceinline__ void load_row(const DArgs &a, int x, int t, Row &r) {
-    const long n = (long)x * a.Wt + t;
-    const double2 *in = a.in;
-    r.c0 = in[n];
-    r.c1 = in[n + a.V];
-    const double2 *pm = (t > 0) ? in + n - 1 : a.f.lo + (long)x * a.f.lo_xs;
-    const long pms = (t > 0) ? a.V : a.f.lo_ps;
-    const double2 *pp = (t + 1 < a.Wt) ? in + n + 1 : a.f.hi + (long)x * a.f.hi_xs;
-    const long pps = (t + 1 < a.Wt) ? a.V : a.f.hi_ps;
-    r.m0 = pm[0];
-    r.m1 = pm[pms];
-    r.p0 = pp[0];
-    r.p1 = pp[pps];
-    r.ut = a.U[n];
-    r.ux = a.U[n + a.V];
-    r.utm = (t > 0) ? a.U[n - 1] : a.loU[(long)x * a.f.lo_xs];
+struct LaneSrc {             // per-lane neighbour addressing, fixed for the whole march
+    const double2 *pm, *pp, *um;   // base of the t-1 / t+1 column and of U_t(t-1)
+    long pms, pps;                 // plane stride for pm / pp
+    long xs_m, xs_p;               // row stride for pm(+um) / pp
+};
+
+__device__ __forceinline__ LaneSrc lane_src(const DArgs &a, int t) {
+    LaneSrc s;
+    const bool lo = t == 0, hi = t + 1 == a.Wt;
+    s.pm = lo ? a.f.lo : a.in + (t - 1);
+    s.um = lo ? a.loU : a.U + (t - 1);
+    s.pms = lo ? a.f.lo_ps : a.V;
+    s.xs_m = lo ? a.f.lo_xs : (long)a.Wt;
+    s.pp = hi ? a.f.hi : a.in + (t + 1);
+    s.pps = hi ? a.f.hi_ps : a.V;
+    s.xs_p = hi ? a.f.hi_xs : (long)a.Wt;
+    return s;
 }
 
-template <int DAG, int EPI>
-__global__ void __launch_bounds__(256) dslash_kernel(DArgs a) {
+// xn: row of the centre psi; xs: row of everything else (== xn except at the
+// chunk's last step, where it re-reads the current row: cache hits, no HBM).
+__device__ __forceinline__ void load_row(const DArgs &a, const LaneSrc &L, int xn, int xs, int t,
+                                         Row &r) {
+    const long n = (long)xn * a.Wt + t;
+    r.c0 = a.in[n];
+    r.c1 = a.in[n + a.V];
+    const long ns = (long)xs * a.Wt + t;
+    const double2 *pm = L.pm + (long)xs * L.xs_m;
+    const double2 *pp = L.pp + (long)xs * L.xs_p;
+    r.m0 = pm[0];
+    r.m1 = pm[L.pms];
+    r.p0 = pp[0];
+    r.p1 = pp[L.pps];
+    r.ut = a.U[ns];
+    r.ux = a.U[ns + a.V];
+    r.utm = L.um[(long)xs * L.xs_m];
+}
+
+// Marching loop with a two-row prefetch: at step x the loads of row x+2 are
+// issued while row x is computed from rows x-1 (centre), x and x+1, which
+// were loaded one and two steps earlier. xn/xs clamp at the chunk end so no
+// load is ever conditional (re-reads there are cache hits).
+template <int DAG, int EPI, int PREF>
+__device__ __forceinline__ void dslash_body(const DArgs &a) {
     __shared__ double2 sh[4];
     if (a.sc && a.sc->done) return;  // grid-uniform early exit after CG convergence
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    const int xbeg = blockIdx.y * a.xchunk;
+    int tb, xc;
+    block_tile(blockIdx.x, a.TB, a.XB, a.xcd_remap, tb, xc);
+    const int t = tb * blockDim.x + threadIdx.x;
+    const int xbeg = xc * a.xchunk;
     const int xend = min(a.Nx, xbeg + a.xchunk);
     double2 acc = make_double2(0.0, 0.0);
     if (t < a.Wt && xbeg < xend) {
@@ -155,29 +199,57 @@ __global__ void __launch_bounds__(256) dslash_kernel(DArgs a) {
         const long V = a.V;
         const double sr0 = (a.t0 + t == a.Ntg - 1) ? -1.0 : 1.0;
         const double sl0 = (a.t0 + t == 0) ? -1.0 : 1.0;
+        const LaneSrc L = lane_src(a, t);
+        auto wrap = [Nx](int x) { return x >= Nx ? x - Nx : x; };
         const int xm = (xbeg == 0) ? Nx - 1 : xbeg - 1;
         const long nm = (long)xm * Wt + t;
         double2 pxm0 = a.in[nm], pxm1 = a.in[nm + V], uxm = a.U[nm + V];
-        Row cur;
-        load_row(a, xbeg, t, cur);
-        for (int x = xbeg; x < xend; ++x) {
-            const int xp = (x + 1 == Nx) ? 0 : x + 1;
-            const long n = (long)x * Wt + t;
-            Row nxt;
-            if (x + 1 < xend) {
-                load_row(a, xp, t, nxt);
-            } else {
-                const long np = (long)xp * Wt + t;
-                nxt.c0 = a.in[np];
-                nxt.c1 = a.in[np + V];
+        if (PREF == 1) {
+            // one-row lookahead (fewer registers, more waves per SIMD)
+            Row cur;
+            load_row(a, L, xbeg, xbeg, t, cur);
+            for (int x = xbeg; x < xend; ++x) {
+                const int xp = (x + 1 == Nx) ? 0 : x + 1;
+                const int xs = (x + 1 < xend) ? xp : x;
+                const long n = (long)x * Wt + t;
+                Row nxt;
+                load_row(a, L, xp, xs, t, nxt);
+                double2 ax0, ax1;
+                if (EPI == EPI_DOT) {
+                    ax0 = a.aux[n];
+                    ax1 = a.aux[n + V];
+                }
+                double2 s0, s1;
+                dirac_site<DAG>(a.mass, sr0, sl0, cur.c0, cur.c1, cur.p0, cur.p1, nxt.c0, nxt.c1,
+                                cur.m0, cur.m1, pxm0, pxm1, cur.ut, cur.ux, cur.utm, uxm, s0, s1);
+                a.out[n] = s0;
+                a.out[n + V] = s1;
+                if (EPI == EPI_DOT) {
+                    acc = cadd(acc, cmul(ax0, cconj(s0)));
+                    acc = cadd(acc, cmul(ax1, cconj(s1)));
+                }
+                pxm0 = cur.c0;
+                pxm1 = cur.c1;
+                uxm = cur.ux;
+                cur = nxt;
             }
+        } else {
+        // Three row registers used round-robin (manual 3-way unroll): the
+        // rotation is a renaming, so no register copy waits on an in-flight load.
+        Row R0, R1, R2;
+        load_row(a, L, xbeg, xbeg, t, R0);
+        load_row(a, L, wrap(xbeg + 1), min(xbeg + 1, xend - 1), t, R1);
+        int x = xbeg;
+        auto step = [&](Row &cur, const Row &nx1, Row &nx2) {
+            const long n = (long)x * Wt + t;
+            load_row(a, L, wrap(min(x + 2, xend)), min(x + 2, xend - 1), t, nx2);
             double2 ax0, ax1;
             if (EPI == EPI_DOT) {
                 ax0 = a.aux[n];
                 ax1 = a.aux[n + V];
             }
             double2 s0, s1;
-            dirac_site<DAG>(a.mass, sr0, sl0, cur.c0, cur.c1, cur.p0, cur.p1, nxt.c0, nxt.c1,
+            dirac_site<DAG>(a.mass, sr0, sl0, cur.c0, cur.c1, cur.p0, cur.p1, nx1.c0, nx1.c1,
                             cur.m0, cur.m1, pxm0, pxm1, cur.ut, cur.ux, cur.utm, uxm, s0, s1);
             a.out[n] = s0;
             a.out[n + V] = s1;
@@ -189,14 +261,32 @@ __global__ void __launch_bounds__(256) dslash_kernel(DArgs a) {
             pxm0 = cur.c0;
             pxm1 = cur.c1;
             uxm = cur.ux;
-            cur = nxt;
+        };
+        for (;;) {
+            step(R0, R1, R2);
+            if (++x >= xend) break;
+            step(R1, R2, R0);
+            if (++x >= xend) break;
+            step(R2, R0, R1);
+            if (++x >= xend) break;
+        }
         }
     }
     if (EPI == EPI_DOT) {
         double2 bs = block_sum(acc, sh);
-        if (threadIdx.x == 0) a.partials[(long)blockIdx.y * gridDim.x + blockIdx.x] = bs;
+        if (threadIdx.x == 0) a.partials[blockIdx.x] = bs;
     }
 }
+
+// Variants (LaunchCfg::variant): 0 = one-row lookahead; 1 = two-row
+// lookahead, registers unconstrained (2 waves/SIMD); 2 = two-row lookahead
+// capped at 168 VGPRs (3 waves/SIMD).
+template <int DAG, int EPI>
+__global__ void __launch_bounds__(256) dslash_kernel_v0(DArgs a) { dslash_body<DAG, EPI, 1>(a); }
+template <int DAG, int EPI>
+__global__ void __launch_bounds__(256) dslash_kernel_v1(DArgs a) { dslash_body<DAG, EPI, 2>(a); }
+template <int DAG, int EPI>
+__global__ void __launch_bounds__(256, 3) dslash_kernel_v2(DArgs a) { dslash_body<DAG, EPI, 2>(a); }
 
 LaunchCfg dslash_config(const Geometry &g) {
     LaunchCfg c;
@@ -210,6 +300,10 @@ LaunchCfg dslash_config(const Geometry &g) {
     if (nchunks < 1) nchunks = 1;
     c.xchunk = (g.Nx + nchunks - 1) / nchunks;
     if (const char *e = getenv("SM_XCHUNK")) c.xchunk = atoi(e);
+    c.xcd_remap = 1;
+    if (const char *e = getenv("SM_XCD_REMAP")) c.xcd_remap = atoi(e);
+    c.variant = 0;
+    if (const char *e = getenv("SM_DSLASH_VARIANT")) c.variant = atoi(e);
     return c;
 }
 
@@ -238,17 +332,27 @@ void launch_dslash(hipStream_t s, const Geometry &g, const LaunchCfg &c, int dag
     a.t0 = g.t0;
     a.Ntg = g.Ntg;
     a.xchunk = c.xchunk;
+    a.TB = (g.Wt + c.bt - 1) / c.bt;
+    a.XB = (g.Nx + c.xchunk - 1) / c.xchunk;
+    a.xcd_remap = c.xcd_remap;
     a.mass = mass;
-    dim3 grid((g.Wt + c.bt - 1) / c.bt, (g.Nx + c.xchunk - 1) / c.xchunk);
+    dim3 grid(a.TB * a.XB);
     dim3 block(c.bt);
     const bool dot = aux != nullptr;
-    if (!dagger) {
-        if (dot) hipLaunchKernelGGL((dslash_kernel<0, EPI_DOT>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((dslash_kernel<0, EPI_NONE>), grid, block, 0, s, a);
-    } else {
-        if (dot) hipLaunchKernelGGL((dslash_kernel<1, EPI_DOT>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((dslash_kernel<1, EPI_NONE>), grid, block, 0, s, a);
-    }
+#define SM_LAUNCH(K)                                                                    \
+    do {                                                                                \
+        if (!dagger) {                                                                  \
+            if (dot) hipLaunchKernelGGL((K<0, EPI_DOT>), grid, block, 0, s, a);         \
+            else hipLaunchKernelGGL((K<0, EPI_NONE>), grid, block, 0, s, a);            \
+        } else {                                                                        \
+            if (dot) hipLaunchKernelGGL((K<1, EPI_DOT>), grid, block, 0, s, a);         \
+            else hipLaunchKernelGGL((K<1, EPI_NONE>), grid, block, 0, s, a);            \
+        }                                                                               \
+    } while (0)
+    if (c.variant == 1) SM_LAUNCH(dslash_kernel_v1);
+    else if (c.variant == 2) SM_LAUNCH(dslash_kernel_v2);
+    else SM_LAUNCH(dslash_kernel_v0);
+#undef SM_LAUNCH
 }
 
 // ---- fermion force bilinear (eqs. 37-38; src/dirac_operator.cpp:493-506) ----
@@ -517,6 +621,33 @@ void launch_cg_beta_from_sum(hipStream_t s, CGScalars *sc) {
 }
 void launch_cg_init_from_sums(hipStream_t s, const double2 *rr_pp, CGScalars *sc, double tol) {
     hipLaunchKernelGGL(cg_init_from_sums_kernel, dim3(1), dim3(1), 0, s, rr_pp, sc, tol);
+}
+
+// ---- bandwidth ceilings (measured roofline reference) --------------------------
+// out = a + b over n complex (2 reads + 1 write, the dslash byte mix) or
+// out = a (1 read + 1 write); 4 independent 16-B loads per lane in flight.
+template <int TWO>
+__global__ void __launch_bounds__(256) stream_kernel(long n, const double2 *__restrict__ a,
+                                                     const double2 *__restrict__ b,
+                                                     double2 *__restrict__ out) {
+    const long stride = (long)gridDim.x * 256;
+    long i = (long)blockIdx.x * 256 + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        double2 x0 = a[i], x1 = a[i + stride], x2 = a[i + 2 * stride], x3 = a[i + 3 * stride];
+        if (TWO) {
+            const double2 y0 = b[i], y1 = b[i + stride], y2 = b[i + 2 * stride], y3 = b[i + 3 * stride];
+            x0 = cadd(x0, y0); x1 = cadd(x1, y1); x2 = cadd(x2, y2); x3 = cadd(x3, y3);
+        }
+        out[i] = x0; out[i + stride] = x1; out[i + 2 * stride] = x2; out[i + 3 * stride] = x3;
+    }
+    for (; i < n; i += stride) out[i] = TWO ? cadd(a[i], b[i]) : a[i];
+}
+
+void launch_stream(hipStream_t s, int two, long n, const double2 *a, const double2 *b, double2 *out,
+                   int blocks) {
+    if (blocks <= 0) blocks = 4096;
+    if (two) hipLaunchKernelGGL(stream_kernel<1>, dim3(blocks), dim3(256), 0, s, n, a, b, out);
+    else hipLaunchKernelGGL(stream_kernel<0>, dim3(blocks), dim3(256), 0, s, n, a, b, out);
 }
 
 // ---- halo faces ---------------------------------------------------------------

@@ -56,8 +56,11 @@ def test_reference_hmc_program_on_gpu(tmp_path):
     exe = os.path.join(REF, "SM_64x64_hip")
     if not os.path.exists(exe):
         pytest.skip("drop-in HMC binary not built")
-    # ranks_x ranks_t m0 MD_steps tau beta Ntherm Nmeas Nsteps save (src/main.cpp:33-57)
-    params = "1\n1\n0\n10\n1\n2\n5\n20\n0\n0\n"
+    # ranks_x ranks_t m0 MD_steps tau beta Ntherm Nmeas Nsteps save (src/main.cpp:33-57).
+    # The unmodified CPU reference with these inputs (dev container, 64x64):
+    #   Ep = 0.717813 +- 0.00133, acceptance 0.875 (57.6 s). Hot start, so
+    #   short thermalisation; the band below is statistical, not bitwise.
+    params = "1\n1\n0\n10\n0.3\n2\n30\n20\n1\n0\n"
     r = subprocess.run([exe], input=params, capture_output=True, text=True, env=env(),
                        cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -66,6 +69,6 @@ def test_reference_hmc_program_on_gpu(tmp_path):
     lines = open(tmp_path / sim[0]).read().split("\n")
     ep = float(lines[lines.index("#Ep                           #dEp") + 1].split()[0])
     acc = float(lines[lines.index("#Acceptance rate") + 1].split()[0])
-    assert 0.5 < ep < 0.95, ep     # beta = 2: pure-gauge <plaq> = I1(2)/I0(2) = 0.698
-    assert 0.3 < acc <= 1.0, acc
+    assert 0.69 < ep < 0.75, (ep, acc)
+    assert 0.5 < acc <= 1.0, acc
     assert "did not converge" not in r.stdout
