@@ -114,6 +114,9 @@ int sm_synchronize(sm_ctx *ctx);
  * variant selects the stencil code variant. Values <= 0 (< 0 for xcd_remap
  * and variant) keep the current setting. */
 int sm_tune(sm_ctx *ctx, int bt, int xchunk, int xcd_remap, int variant);
+/* CG path: fused = 1 runs an iteration in two HBM passes (sm_cgfused.hip),
+ * 0 the six-kernel sequence; xchunk = rows per block of the fused kernel. */
+int sm_tune_cg(sm_ctx *ctx, int fused, int xchunk);
 /* Streaming-bandwidth ceiling on the ctx stream (measured roofline reference):
  * out = a + b (two_reads = 1: the stencil's 2-read/1-write byte mix) or
  * out = a, over n complex<double> device elements. */
@@ -157,6 +160,10 @@ int sm_cg_dev(sm_ctx *ctx, const double *phi, double *x, double m0, double tol, 
 int sm_cg_begin(sm_ctx *ctx, const double *phi, double *x, double m0, double tol);
 int sm_cg_iterate(sm_ctx *ctx, int n);
 int sm_cg_status(sm_ctx *ctx, sm_cg_result *res);
+/* End a stepwise solve: apply the x update the fused iteration defers to the
+ * next pass (x += alpha_{k-1} d_{k-1}), then report like sm_cg_status. Until
+ * then x lags one update behind the reference's x. */
+int sm_cg_finish(sm_ctx *ctx, sm_cg_result *res);
 
 #ifdef __cplusplus
 }

@@ -61,6 +61,8 @@ def _load():
         "sm_cg_begin": ([vp, vp, vp, cd, cd], ci),
         "sm_cg_iterate": ([vp, ci], ci),
         "sm_cg_status": ([vp, ctypes.POINTER(CGResult)], ci),
+        "sm_cg_finish": ([vp, ctypes.POINTER(CGResult)], ci),
+        "sm_tune_cg": ([vp, ci, ci], ci),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

@@ -58,13 +58,15 @@ int fail(int code, const char *fmt, ...) {
 }  // namespace
 
 // Work fields, each 2*V complex (plane mu0 then mu1).
-enum { F_IN, F_OUT, F_TMP, F_X, F_R, F_D, F_T, F_AD, F_PHI, F_L, F_RR, NFIELDS };
+enum { F_IN, F_OUT, F_TMP, F_X, F_R, F_D, F_D2, F_T, F_AD, F_PHI, F_L, F_RR, NFIELDS };
 
 struct sm_ctx {
     int device = 0;
     int nshard = 1, shard = 0;
     Geometry g{};
     LaunchCfg cfg{};
+    CGFusedCfg fcfg{};
+    int cg_fused = 1;               // 1: two-pass fused CG iteration (sm_cgfused.hip)
     hipStream_t own_stream = nullptr, stream = nullptr;
     ncclComm_t comm = nullptr;
     bool hosted = false;            // host-callback transport instead of RCCL
@@ -76,6 +78,7 @@ struct sm_ctx {
     double2 *ghostU = nullptr;     // Nx: U_t at local t = -1 (lower neighbour's last column)
     double2 *fields = nullptr;     // NFIELDS * 2V
     double2 *faces = nullptr;      // 4 * 2Nx per spinor being exchanged (x2 for force)
+    double2 *faces2 = nullptr;     // 2-deep faces: send lo/hi (4Nx each), recv d, r, U (8Nx each)
     double2 *partials = nullptr;   // 2 * max(nparts)
     double2 *sums = nullptr;       // 4 complex scratch (allreduce)
     double *Fbuf = nullptr;        // 2V doubles (force)
@@ -88,6 +91,8 @@ struct sm_ctx {
     const double2 *cg_phi = nullptr;
     double2 *cg_x = nullptr;
     int cg_active = 0;
+    long cg_issued = 0;             // iterations enqueued since sm_cg_begin
+    int cg_pending_x = 0;           // fused path: last x update deferred to sm_cg_finish
 
     double2 *field(int i) { return fields + (size_t)i * 2 * g.V; }
 };
@@ -127,8 +132,7 @@ int down_rank(const sm_ctx *c) { return (c->shard - 1 + c->nshard) % c->nshard; 
 // My t = Wt-1 column goes up (it is the up-neighbour's t = -1), my t = 0
 // column goes down (the down-neighbour's t = Wt). The face buffers are
 // [plane][x], 4*Nx doubles.
-int exchange_faces(sm_ctx *c, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi) {
-    const size_t cnt = (size_t)4 * c->g.Nx;
+int exchange_faces(sm_ctx *c, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi, size_t cnt) {
     if (c->hosted) {
         double *h = c->h_face;
         HIP_TRY(hipMemcpyAsync(h, slo, cnt * 8, hipMemcpyDeviceToHost, c->stream));
@@ -174,7 +178,7 @@ int halo(sm_ctx *c, const double2 *field, int set, TFaces *f) {
     double2 *slo = face_buf(c, set, 0), *shi = face_buf(c, set, 1);
     double2 *rlo = face_buf(c, set, 2), *rhi = face_buf(c, set, 3);
     launch_pack_faces(c->stream, c->g, field, slo, shi);
-    TRY(exchange_faces(c, slo, shi, rlo, rhi));
+    TRY(exchange_faces(c, slo, shi, rlo, rhi, (size_t)4 * c->g.Nx));
     *f = faces_for(c, field, rlo, rhi);
     return SM_OK;
 }
@@ -217,14 +221,29 @@ int download_plane_pair(sm_ctx *c, const double2 *src, double *p0, double *p1) {
     return SM_OK;
 }
 
+// 2-deep faces of the fused CG kernel: 4 columns [-2,-1,Wt,Wt+1][plane][x].
+double2 *face2_recv(sm_ctx *c, int which) {  // 0: d, 1: r, 2: U
+    return c->faces2 + (size_t)(8 + 8 * which) * c->g.Nx;
+}
+
+int halo2(sm_ctx *c, const double2 *field, double2 *face) {
+    if (c->nshard == 1) return SM_OK;
+    double2 *slo = c->faces2, *shi = c->faces2 + (size_t)4 * c->g.Nx;
+    launch_pack_faces2(c->stream, c->g, field, slo, shi);
+    const size_t cnt = (size_t)8 * c->g.Nx;  // doubles: 2 columns x 2 planes x Nx complex
+    return exchange_faces(c, slo, shi, face, face + (size_t)4 * c->g.Nx, cnt);
+}
+
 int exchange_ghost_U(sm_ctx *c) {
     if (c->nshard == 1) return SM_OK;
     // U_t(x, Wt-1) (plane 0 of my hi face) is the up-neighbour's U_t(x, -1)
     double2 *slo = face_buf(c, 1, 0), *shi = face_buf(c, 1, 1);
     double2 *rlo = face_buf(c, 1, 2), *rhi = face_buf(c, 1, 3);
     launch_pack_faces(c->stream, c->g, c->U, slo, shi);
-    TRY(exchange_faces(c, slo, shi, rlo, rhi));
+    TRY(exchange_faces(c, slo, shi, rlo, rhi, (size_t)4 * c->g.Nx));
     HIP_TRY(hipMemcpyAsync(c->ghostU, rlo, sizeof(double2) * c->g.Nx, hipMemcpyDeviceToDevice, c->stream));
+    // 2-deep ghost links for the fused CG kernel
+    TRY(halo2(c, c->U, face2_recv(c, 2)));
     return SM_OK;
 }
 
@@ -344,6 +363,8 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     c->cfg = dslash_config(c->g);
     c->nparts_dslash = dslash_blocks(c->g, c->cfg);
     c->nparts_red = reduce_blocks(2 * c->g.V);
+    c->fcfg = cg_fused_config(c->g);
+    if (const char *e = getenv("SM_CG_FUSED")) c->cg_fused = atoi(e);
     const int np = kMaxPartials;
     const size_t fb = sizeof(double2) * 2 * (size_t)c->g.V;
     hipError_t e = hipSuccess;
@@ -354,6 +375,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     chk(hipMalloc(&c->ghostU, sizeof(double2) * (size_t)Nx));
     chk(hipMalloc(&c->fields, fb * NFIELDS));
     chk(hipMalloc(&c->faces, sizeof(double2) * 2 * (size_t)Nx * 8));
+    chk(hipMalloc(&c->faces2, sizeof(double2) * 32 * (size_t)Nx));
     chk(hipMalloc(&c->partials, sizeof(double2) * 2 * (size_t)np));
     chk(hipMalloc(&c->sums, sizeof(double2) * 4));
     chk(hipMalloc(&c->Fbuf, sizeof(double) * 2 * (size_t)c->g.V));
@@ -400,7 +422,7 @@ int sm_destroy(sm_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
-    void *dev[] = {c->U, c->ghostU, c->fields, c->faces, c->partials, c->sums, c->Fbuf, c->sc};
+    void *dev[] = {c->U, c->ghostU, c->fields, c->faces, c->faces2, c->partials, c->sums, c->Fbuf, c->sc};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_sc) (void)hipHostFree(c->h_sc);
@@ -409,6 +431,19 @@ int sm_destroy(sm_ctx *c) {
     if (c->h_red) (void)hipHostFree(c->h_red);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
+    return SM_OK;
+}
+
+int sm_tune_cg(sm_ctx *c, int fused, int xchunk) {
+    if (!c) return fail(SM_ERR_ARG, "null context");
+    if (fused >= 0) c->cg_fused = fused;
+    if (xchunk > 0) {
+        CGFusedCfg f = c->fcfg;
+        f.xchunk = xchunk;
+        f.XB = (c->g.Nx + xchunk - 1) / xchunk;
+        if (cg_fused_blocks(f) > kMaxPartials) return fail(SM_ERR_ARG, "too many blocks");
+        c->fcfg = f;
+    }
     return SM_OK;
 }
 
@@ -534,6 +569,22 @@ int sm_cg_begin(sm_ctx *c, const double *phi, double *x, double m0, double tol) 
     }
     HIP_TRY(hipGetLastError());
     c->cg_active = 1;
+    c->cg_issued = 0;
+    c->cg_pending_x = 0;
+    return SM_OK;
+}
+
+// alpha / beta from per-block partials (local sum, all-reduce over shards, scalar)
+static int cg_scalar(sm_ctx *c, int nparts, int which) {
+    if (c->nshard == 1) {
+        if (which == 0) launch_cg_alpha(c->stream, nparts, c->partials, c->sc);
+        else launch_cg_beta(c->stream, nparts, c->partials, c->sc);
+        return SM_OK;
+    }
+    launch_sum_to_scalar(c->stream, nparts, c->partials, c->sc);
+    TRY(allreduce_dev(c, (double *)&c->sc->sum, 2));
+    if (which == 0) launch_cg_alpha_from_sum(c->stream, c->sc);
+    else launch_cg_beta_from_sum(c->stream, c->sc);
     return SM_OK;
 }
 
@@ -541,31 +592,48 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
     TRY(check_ready(c));
     if (!c->cg_active) return fail(SM_ERR_STATE, "sm_cg_iterate before sm_cg_begin");
     const long n = 2 * c->g.V;
-    double2 *r = c->field(F_R), *d = c->field(F_D), *Ad = c->field(F_AD), *t = c->field(F_T);
+    double2 *r = c->field(F_R), *Ad = c->field(F_AD), *t = c->field(F_T);
     double2 *x = c->cg_x;
     for (int i = 0; i < niter; ++i) {
-        // Ad = D D^dag d, fused partials of <d, Ad>
-        TRY(apply(c, d, t, c->cg_mass, 1, nullptr, nullptr, c->sc));
-        TRY(apply(c, t, Ad, c->cg_mass, 0, d, c->partials, c->sc));
-        if (c->nshard == 1) {
-            launch_cg_alpha(c->stream, c->nparts_dslash, c->partials, c->sc);
+        if (c->cg_fused) {
+            // pass 1: d_k, deferred x update, Ad = D D^dag d_k, <d_k, Ad>
+            double2 *dold = c->field((c->cg_issued & 1) ? F_D2 : F_D);
+            double2 *dnew = c->field((c->cg_issued & 1) ? F_D : F_D2);
+            TRY(halo2(c, dold, face2_recv(c, 0)));
+            TRY(halo2(c, r, face2_recv(c, 1)));
+            launch_cg_fused(c->stream, c->g, c->fcfg, c->nshard, dold, dnew, r, x, Ad, c->U,
+                            face2_recv(c, 0), face2_recv(c, 1), face2_recv(c, 2), c->cg_mass,
+                            c->cg_issued == 0, c->sc, c->partials);
+            TRY(cg_scalar(c, cg_fused_blocks(c->fcfg), 0));
+            // pass 2: r -= alpha Ad, <r, r>; stop test and beta
+            launch_cg_update_r(c->stream, n, r, Ad, c->sc, c->partials);
+            TRY(cg_scalar(c, c->nparts_red, 1));
+            c->cg_pending_x = 1;
         } else {
-            launch_sum_to_scalar(c->stream, c->nparts_dslash, c->partials, c->sc);
-            TRY(allreduce_dev(c, (double *)&c->sc->sum, 2));
-            launch_cg_alpha_from_sum(c->stream, c->sc);
+            double2 *d = c->field(F_D);
+            // Ad = D D^dag d, fused partials of <d, Ad>
+            TRY(apply(c, d, t, c->cg_mass, 1, nullptr, nullptr, c->sc));
+            TRY(apply(c, t, Ad, c->cg_mass, 0, d, c->partials, c->sc));
+            TRY(cg_scalar(c, c->nparts_dslash, 0));
+            launch_cg_update_xr(c->stream, n, x, r, d, Ad, c->sc, c->partials);
+            TRY(cg_scalar(c, c->nparts_red, 1));
+            launch_cg_update_d(c->stream, n, d, r, c->sc);
         }
-        launch_cg_update_xr(c->stream, n, x, r, d, Ad, c->sc, c->partials);
-        if (c->nshard == 1) {
-            launch_cg_beta(c->stream, c->nparts_red, c->partials, c->sc);
-        } else {
-            launch_sum_to_scalar(c->stream, c->nparts_red, c->partials, c->sc);
-            TRY(allreduce_dev(c, (double *)&c->sc->sum, 2));
-            launch_cg_beta_from_sum(c->stream, c->sc);
-        }
-        launch_cg_update_d(c->stream, n, d, r, c->sc);
+        c->cg_issued++;
     }
     HIP_TRY(hipGetLastError());
     return SM_OK;
+}
+
+int sm_cg_finish(sm_ctx *c, sm_cg_result *res) {
+    if (!c || !res) return fail(SM_ERR_ARG, "null argument");
+    if (c->cg_active && c->cg_pending_x) {
+        launch_cg_finish_x(c->stream, 2 * c->g.V, c->cg_x, c->field(F_D), c->field(F_D2), c->sc);
+        HIP_TRY(hipGetLastError());
+        c->cg_pending_x = 0;
+    }
+    c->cg_active = 0;
+    return sm_cg_status(c, res);
 }
 
 int sm_cg_status(sm_ctx *c, sm_cg_result *res) {
@@ -594,9 +662,7 @@ int sm_cg_dev(sm_ctx *c, const double *phi, double *x, double m0, double tol, in
         if (res->converged) break;
         if (chunk < 64) chunk *= 2;
     }
-    TRY(sm_cg_status(c, res));
-    c->cg_active = 0;
-    return SM_OK;
+    return sm_cg_finish(c, res);
 }
 
 // ---- host-pointer (drop-in) operators ---------------------------------------

@@ -1,0 +1,314 @@
+// sm_cgfused.hip -- one CG iteration on D D^dagger in two HBM passes (gfx950).
+//
+// Reference loop body (src/conjugate_gradient.cpp:31-63), iteration k:
+//     Ad = D D^dag d_k ; alpha_k = rn / <d_k, Ad> ; x += alpha_k d_k ;
+//     r -= alpha_k Ad ; err = |r| ; stop? ; beta_k = err^2 / rn ; d_{k+1} = d_k beta_k + r
+// Pass 1 (cg_fused_kernel), iteration k:
+//     d_k = d_{k-1} beta_{k-1} + r_k          (on the fly, stored once)
+//     x  += alpha_{k-1} d_{k-1}               (deferred x update of iteration k-1)
+//     T   = D^dag d_k   (registers only)      Ad = D T ; partials of <d_k, Ad>
+// Pass 2 (cg_update_r_kernel): r -= alpha_k Ad ; partials of <r, r>.
+// Every per-element operation is the reference's (same complex arithmetic,
+// same order), only the dot-product reduction order differs.
+//
+// HBM bytes per site: pass 1 reads d_{k-1}, r, x, U (128) and writes d_k, x, Ad
+// (96); pass 2 reads r, Ad and writes r (96): 320 B/site against 576 for the
+// reference's sequence.
+//
+// Geometry: a wave owns 60 consecutive t-columns; its 64 lanes cover columns
+// T0-2 .. T0+61 (2 halo lanes per side) and march along x. The t-neighbours of
+// the intermediates (d_k, T, U_t) come from adjacent lanes through DPP
+// wave-shifts; the x-neighbours are register rows. Halo lanes compute and are
+// discarded, so waves are independent (no LDS, no barrier in the loop).
+#include "sm_device.h"
+#include "sm_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace sm {
+
+constexpr int FW = 60;  // output t-columns per wave
+
+struct CGFArgs {
+    const double2 *dold;
+    double2 *dnew;
+    const double2 *r;
+    double2 *x;
+    double2 *Ad;
+    const double2 *U;
+    const double2 *fd, *fr, *fU;  // nshard > 1: 4-column faces [-2,-1,Wt,Wt+1][plane][x]
+    CGScalars *sc;
+    double2 *partials;
+    long V;
+    int Nx, Wt, t0, Ntg, nshard;
+    int xchunk, NWT, TBk, XB, remap, first;
+    double mass;
+};
+
+struct CSrc {
+    const double2 *p;
+    long xs, ps;
+};
+
+// Where column c of a field lives: in-domain, periodic wrap (one shard), or
+// the received face (t-shard). Clamped so every lane's address is valid.
+__device__ __forceinline__ CSrc csrc(const double2 *base, const double2 *face, int c, const CGFArgs &a) {
+    CSrc s;
+    if (c >= 0 && c < a.Wt) {
+        s.p = base + c;
+        s.xs = a.Wt;
+        s.ps = a.V;
+    } else if (a.nshard == 1) {
+        int cw = c % a.Wt;
+        if (cw < 0) cw += a.Wt;
+        s.p = base + cw;
+        s.xs = a.Wt;
+        s.ps = a.V;
+    } else {
+        int fc = c < 0 ? c + 2 : c - a.Wt + 2;
+        fc = fc < 0 ? 0 : (fc > 3 ? 3 : fc);
+        s.p = face + (long)fc * 2 * a.Nx;
+        s.xs = 1;
+        s.ps = a.Nx;
+    }
+    return s;
+}
+
+struct Raw {
+    double2 d0, d1, r0, r1, ut, ux, x0, x1;
+};
+
+struct Sp {   // a 2-spinor at one site
+    double2 a, b;
+};
+
+__device__ __forceinline__ Sp shr(Sp v) { return Sp{dpp_shr1(v.a), dpp_shr1(v.b)}; }
+__device__ __forceinline__ Sp shl(Sp v) { return Sp{dpp_shl1(v.a), dpp_shl1(v.b)}; }
+
+__global__ void __launch_bounds__(256) cg_fused_kernel(CGFArgs a) {
+    __shared__ double2 sh[4];
+    CGScalars *sc = a.sc;
+    if (sc->done) return;  // grid-uniform: converged in an earlier iteration
+    const double2 alpha = sc->alpha, beta = sc->beta;  // alpha_{k-1}, beta_{k-1}
+    int tb, xc;
+    {
+        int w = blockIdx.x;
+        if (a.remap) {
+            const int n = a.TBk * a.XB, q = n >> 3, rr = n & 7, xcd = w & 7;
+            w = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (w >> 3);
+        }
+        tb = w % a.TBk;
+        xc = w / a.TBk;
+    }
+    const int lane = threadIdx.x & 63;
+    const int g = tb * 4 + (threadIdx.x >> 6);  // wave tile along t
+    const int x0 = xc * a.xchunk;
+    const int xe = min(a.Nx, x0 + a.xchunk);
+    double2 acc = make_double2(0.0, 0.0);
+    if (g < a.NWT && x0 < xe) {
+        const int Nx = a.Nx, Wt = a.Wt;
+        const int c = g * FW - 2 + lane;                 // this lane's t-column
+        const bool own = lane >= 2 && lane < FW + 2 && c < Wt;
+        int tg = (a.t0 + c) % a.Ntg;
+        if (tg < 0) tg += a.Ntg;
+        const double sr0 = tg == a.Ntg - 1 ? -1.0 : 1.0;  // SignR[2n], include/dirac_operator.h:53-55
+        const double sl0 = tg == 0 ? -1.0 : 1.0;          // SignL[2n], :56-58
+        const CSrc Sd = csrc(a.dold, a.fd, c, a), Sr = csrc(a.r, a.fr, c, a), Su = csrc(a.U, a.fU, c, a);
+        const int cx = c < 0 ? 0 : (c >= Wt ? Wt - 1 : c);  // in-domain column for x / stores
+        const bool first = a.first != 0;
+        auto wrap = [Nx](int x) { int w = x % Nx; return w < 0 ? w + Nx : w; };
+        // raw loads of logical row xr: d_{k-1}, r (rows x0-2 .. xe+1), U (clamped
+        // to x0-2 .. xe), x (clamped to owned rows; re-reads are cache hits)
+        auto load = [&](int xr, Raw &R) {
+            const long pr = (long)wrap(xr);
+            const double2 *pd = Sd.p + pr * Sd.xs, *pq = Sr.p + pr * Sr.xs;
+            R.d0 = pd[0];
+            R.d1 = pd[Sd.ps];
+            R.r0 = pq[0];
+            R.r1 = pq[Sr.ps];
+            const double2 *pu = Su.p + (long)wrap(min(xr, xe)) * Su.xs;
+            R.ut = pu[0];
+            R.ux = pu[Su.ps];
+            const long nx = (long)wrap(min(max(xr, x0), xe - 1)) * Wt + cx;
+            R.x0 = a.x[nx];
+            R.x1 = a.x[nx + a.V];
+        };
+        // d_k = d_{k-1} * beta + r (src/conjugate_gradient.cpp:55-58); on owned
+        // rows also store it and apply the deferred x += alpha d_{k-1} (:36-37)
+        auto dnew = [&](int xr, const Raw &R) {
+            Sp d;
+            d.a = first ? R.d0 : cadd(cmul(R.d0, beta), R.r0);
+            d.b = first ? R.d1 : cadd(cmul(R.d1, beta), R.r1);
+            if (xr >= x0 && xr < xe && own) {
+                const long n = (long)xr * Wt + c;
+                a.dnew[n] = d.a;
+                a.dnew[n + a.V] = d.b;
+                if (!first) {
+                    a.x[n] = cadd(R.x0, cmul(alpha, R.d0));
+                    a.x[n + a.V] = cadd(R.x1, cmul(alpha, R.d1));
+                }
+            }
+            return d;
+        };
+        // D^dag at this lane's column of row xr (centre p, x-neighbours pxm/pxp)
+        auto ddag = [&](const Sp &p, const Sp &pxm, const Sp &pxp, double2 ut, double2 ux,
+                        double2 uxm, double2 &utm_out) {
+            const Sp pm = shr(p), pp = shl(p);
+            utm_out = dpp_shr1(ut);
+            Sp o;
+            dirac_site<1>(a.mass, sr0, sl0, p.a, p.b, pp.a, pp.b, pxp.a, pxp.b, pm.a, pm.b, pxm.a,
+                          pxm.b, ut, ux, utm_out, uxm, o.a, o.b);
+            return o;
+        };
+        // prologue: rows x0-2 .. x0+1
+        Raw R;
+        load(x0 - 2, R);
+        Sp dm2 = dnew(x0 - 2, R);
+        double2 uxm2 = R.ux;
+        load(x0 - 1, R);
+        Sp dm1 = dnew(x0 - 1, R);
+        double2 utm1 = R.ut, uxm1 = R.ux;
+        load(x0, R);
+        Sp dc = dnew(x0, R);
+        double2 utc = R.ut, uxc = R.ux;
+        load(x0 + 1, R);
+        Sp dn = dnew(x0 + 1, R);
+        double2 utn = R.ut, uxn = R.ux;
+        load(x0 + 2, R);
+        double2 dummy;
+        Sp Tp = ddag(dm1, dm2, dc, utm1, uxm1, uxm2, dummy);  // T(x0-1)
+        double2 utmc;
+        Sp Tc = ddag(dc, dm1, dn, utc, uxc, uxm1, utmc);      // T(x0), U_t(x0, t-1)
+        double2 uxp = uxm1;                                   // U_x(x-1)
+        for (int x = x0; x < xe; ++x) {
+            // A: row x+2 -> d_{k}(x+2); then immediately reuse R for row x+3
+            const Sp d2 = dnew(x + 2, R);
+            const double2 ut2 = R.ut, ux2 = R.ux;
+            load(min(x + 3, xe + 1), R);
+            __builtin_amdgcn_sched_barrier(0);  // keep the next row's loads issued here
+            // B: T(x+1) = D^dag d at row x+1
+            double2 utmn;
+            const Sp Tn = ddag(dn, dc, d2, utn, uxn, uxc, utmn);
+            // C: Ad(x) = D T at row x; dot <d_k, Ad> on owned sites
+            const Sp Tm = shr(Tc), Tq = shl(Tc);
+            Sp o;
+            dirac_site<0>(a.mass, sr0, sl0, Tc.a, Tc.b, Tq.a, Tq.b, Tn.a, Tn.b, Tm.a, Tm.b, Tp.a, Tp.b,
+                          utc, uxc, utmc, uxp, o.a, o.b);
+            if (own) {
+                const long n = (long)x * Wt + c;
+                a.Ad[n] = o.a;
+                a.Ad[n + a.V] = o.b;
+                acc = cadd(acc, cmul(dc.a, cconj(o.a)));  // dot(d, Ad), include/variables.h:185-188
+                acc = cadd(acc, cmul(dc.b, cconj(o.b)));
+            }
+            // rotate (all ready values: no load is waited on here)
+            Tp = Tc;
+            Tc = Tn;
+            dc = dn;
+            dn = d2;
+            uxp = uxc;
+            utc = utn;
+            uxc = uxn;
+            utmc = utmn;
+            utn = ut2;
+            uxn = ux2;
+        }
+    }
+    const double2 bs = block_sum(acc, sh);
+    if (threadIdx.x == 0) a.partials[blockIdx.x] = bs;
+}
+
+CGFusedCfg cg_fused_config(const Geometry &g) {
+    CGFusedCfg c;
+    c.NWT = (g.Wt + FW - 1) / FW;
+    c.TBk = (c.NWT + 3) / 4;
+    int target = 1024;
+    if (const char *e = getenv("SM_CGF_BLOCKS")) target = atoi(e);
+    int nchunks = (target + c.TBk - 1) / c.TBk;
+    if (nchunks > g.Nx) nchunks = g.Nx;
+    if (nchunks < 1) nchunks = 1;
+    c.xchunk = (g.Nx + nchunks - 1) / nchunks;
+    if (const char *e = getenv("SM_CGF_XCHUNK")) c.xchunk = atoi(e);
+    c.XB = (g.Nx + c.xchunk - 1) / c.xchunk;
+    c.remap = 1;
+    return c;
+}
+
+int cg_fused_blocks(const CGFusedCfg &c) { return c.TBk * c.XB; }
+
+void launch_cg_fused(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard,
+                     const double2 *dold, double2 *dnew, const double2 *r, double2 *x, double2 *Ad,
+                     const double2 *U, const double2 *fd, const double2 *fr, const double2 *fU,
+                     double mass, int first, CGScalars *sc, double2 *partials) {
+    CGFArgs a;
+    a.dold = dold; a.dnew = dnew; a.r = r; a.x = x; a.Ad = Ad; a.U = U;
+    a.fd = fd; a.fr = fr; a.fU = fU;
+    a.sc = sc; a.partials = partials;
+    a.V = g.V; a.Nx = g.Nx; a.Wt = g.Wt; a.t0 = g.t0; a.Ntg = g.Ntg; a.nshard = nshard;
+    a.xchunk = c.xchunk; a.NWT = c.NWT; a.TBk = c.TBk; a.XB = c.XB; a.remap = c.remap;
+    a.first = first;
+    a.mass = mass;
+    hipLaunchKernelGGL(cg_fused_kernel, dim3(c.TBk * c.XB), dim3(256), 0, s, a);
+}
+
+// ---- pass 2: r -= alpha Ad ; partials <r, r>  (src/conjugate_gradient.cpp:39-43)
+constexpr int RB2 = 256;
+__global__ void __launch_bounds__(RB2) cg_update_r_kernel(long n, double2 *r, const double2 *Ad,
+                                                          const CGScalars *sc, double2 *part) {
+    __shared__ double2 sh[RB2 / 64];
+    if (sc->done) return;
+    const double2 alpha = sc->alpha;
+    double2 acc = make_double2(0.0, 0.0);
+    for (long i = (long)blockIdx.x * RB2 + threadIdx.x; i < n; i += (long)gridDim.x * RB2) {
+        const double2 ri = csub(r[i], cmul(alpha, Ad[i]));
+        r[i] = ri;
+        acc = cadd(acc, cmul(ri, cconj(ri)));
+    }
+    const double2 s = block_sum(acc, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+void launch_cg_update_r(hipStream_t s, long n, double2 *r, const double2 *Ad, const CGScalars *sc,
+                        double2 *part) {
+    hipLaunchKernelGGL(cg_update_r_kernel, dim3(reduce_blocks(n)), dim3(RB2), 0, s, n, r, Ad, sc, part);
+}
+
+// ---- the deferred x update of the last executed iteration --------------------
+// x += alpha_{k-1} d_{k-1}, d_{k-1} in dbuf[k & 1] (k = iterations executed).
+__global__ void __launch_bounds__(RB2) cg_finish_x_kernel(long n, double2 *x, const double2 *d0,
+                                                          const double2 *d1, const CGScalars *sc) {
+    const int k = sc->k;
+    if (k < 1) return;
+    const double2 alpha = sc->alpha;
+    const double2 *d = (k & 1) ? d1 : d0;
+    for (long i = (long)blockIdx.x * RB2 + threadIdx.x; i < n; i += (long)gridDim.x * RB2)
+        x[i] = cadd(x[i], cmul(alpha, d[i]));
+}
+
+void launch_cg_finish_x(hipStream_t s, long n, double2 *x, const double2 *d0, const double2 *d1,
+                        const CGScalars *sc) {
+    hipLaunchKernelGGL(cg_finish_x_kernel, dim3(reduce_blocks(n)), dim3(RB2), 0, s, n, x, d0, d1, sc);
+}
+
+// ---- 2-deep t-faces: columns {Wt-2, Wt-1} go up (arrive as -2, -1), {0, 1} go
+// down (arrive as Wt, Wt+1). Buffers [col][plane][x], 4*Nx complex each.
+__global__ void pack_faces2_kernel(int Nx, int Wt, long V, const double2 *f, double2 *lo, double2 *hi) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= Nx) return;
+    const long row = (long)x * Wt;
+    for (int col = 0; col < 2; ++col)
+        for (int p = 0; p < 2; ++p) {
+            const int c_lo = col < Wt ? col : Wt - 1;           // t = 0, 1
+            const int c_hi = Wt - 2 + col >= 0 ? Wt - 2 + col : 0;  // t = Wt-2, Wt-1
+            lo[(long)(col * 2 + p) * Nx + x] = f[row + c_lo + p * V];
+            hi[(long)(col * 2 + p) * Nx + x] = f[row + c_hi + p * V];
+        }
+}
+
+void launch_pack_faces2(hipStream_t s, const Geometry &g, const double2 *field, double2 *lo,
+                        double2 *hi) {
+    hipLaunchKernelGGL(pack_faces2_kernel, dim3((g.Nx + 255) / 256), dim3(256), 0, s, g.Nx, g.Wt, g.V,
+                       field, lo, hi);
+}
+
+}  // namespace sm

@@ -11,97 +11,12 @@
 // psi(x+1) and U_x(x-1) in registers, so each field row crosses HBM once
 // (plus a 1-row halo per chunk). t-neighbours come from the wave's own
 // coalesced row loads (L1/L2 hits). HBM-bound: 96 B/site algorithmic.
+#include "sm_device.h"
 #include "sm_internal.h"
 
 #pragma clang fp contract(off)
 
 namespace sm {
-
-// ---- complex<double> with std::complex / GCC semantics --------------------
-__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ double2 cneg(double2 a) { return make_double2(-a.x, -a.y); }
-__device__ __forceinline__ double2 cconj(double2 a) { return make_double2(a.x, -a.y); }
-// GCC expansion of complex multiply: (ac - bd, ad + bc), separately rounded.
-__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
-    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-__device__ __forceinline__ double2 rmul(double s, double2 a) { return make_double2(s * a.x, s * a.y); }
-
-// libgcc __divdc3 as shipped with GCC 11 (std::complex<double> division).
-__device__ __forceinline__ double2 cdiv(double a, double b, double c, double d) {
-    double denom, ratio, x, y;
-    if (fabs(c) < fabs(d)) {
-        ratio = c / d;
-        denom = (c * ratio) + d;
-        x = ((a * ratio) + b) / denom;
-        y = ((b * ratio) - a) / denom;
-    } else {
-        ratio = d / c;
-        denom = (d * ratio) + c;
-        x = ((b * ratio) + a) / denom;
-        y = (b - (a * ratio)) / denom;
-    }
-    return make_double2(x, y);
-}
-
-#define I_NUM make_double2(0.0, 1.0)      /* I_number, src/dirac_operator.cpp:3 */
-#define MI_NUM make_double2(-0.0, -1.0)   /* -I_number                         */
-
-// One site of D (eq. 34; src/dirac_operator.cpp:31-43) or D^dagger
-// (eqs. 35-36; :255-267). Hop coefficients a,b (forward) c,e (backward)
-// carry the gauge link times the boundary sign, exactly as (U*Sign)*combo.
-template <int DAG>
-__device__ __forceinline__ void dirac_site(double mass, double sr0, double sl0, double2 p0,
-                                           double2 p1, double2 pt0, double2 pt1, double2 px0,
-                                           double2 px1, double2 pm0, double2 pm1, double2 pxm0,
-                                           double2 pxm1, double2 Ut, double2 Ux, double2 Utm,
-                                           double2 Uxm, double2 &s0, double2 &s1) {
-    const double2 one = make_double2(1.0, 0.0);
-    const double2 a = cmul(Ut, make_double2(sr0, 0.0));
-    const double2 b = cmul(Ux, one);
-    const double2 c = cmul(cconj(Utm), make_double2(sl0, 0.0));
-    const double2 e = cmul(cconj(Uxm), one);
-    if (!DAG) {
-        double2 A = cmul(a, csub(pt0, pt1));
-        double2 B = cmul(b, cadd(px0, cmul(I_NUM, px1)));
-        double2 C = cmul(c, cadd(pm0, pm1));
-        double2 E = cmul(e, csub(pxm0, cmul(I_NUM, pxm1)));
-        s0 = csub(rmul(mass, p0), rmul(0.5, cadd(cadd(cadd(A, B), C), E)));
-        A = cmul(a, cadd(cneg(pt0), pt1));
-        B = cmul(b, cadd(cmul(MI_NUM, px0), px1));
-        E = cmul(e, cadd(cmul(I_NUM, pxm0), pxm1));
-        s1 = csub(rmul(mass, p1), rmul(0.5, cadd(cadd(cadd(A, B), C), E)));
-    } else {
-        double2 C = cmul(c, csub(pm0, pm1));
-        double2 E = cmul(e, cadd(pxm0, cmul(I_NUM, pxm1)));
-        double2 A = cmul(a, cadd(pt0, pt1));
-        double2 B = cmul(b, csub(px0, cmul(I_NUM, px1)));
-        s0 = csub(rmul(mass, p0), rmul(0.5, cadd(cadd(cadd(C, E), A), B)));
-        C = cmul(c, cadd(cneg(pm0), pm1));
-        E = cmul(e, cadd(cmul(MI_NUM, pxm0), pxm1));
-        B = cmul(b, cadd(cmul(I_NUM, px0), px1));
-        s1 = csub(rmul(mass, p1), rmul(0.5, cadd(cadd(cadd(C, E), A), B)));
-    }
-}
-
-// Deterministic block sum: wave butterfly, then lane-0 sums waves in order.
-__device__ __forceinline__ double2 block_sum(double2 v, double2 *sh) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        v.x += __shfl_xor(v.x, off);
-        v.y += __shfl_xor(v.y, off);
-    }
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (lane == 0) sh[wid] = v;
-    __syncthreads();
-    double2 r = make_double2(0.0, 0.0);
-    if (threadIdx.x == 0) {
-        const int nw = (blockDim.x + 63) >> 6;
-        for (int w = 0; w < nw; ++w) r = cadd(r, sh[w]);
-    }
-    return r;
-}
 
 struct DArgs {
     const double2 *__restrict__ in;

@@ -51,12 +51,15 @@ def test_operators_bitwise_vs_reference(sm, name):
     assert bits_equal(np.concatenate([F.mu0, F.mu1]), a["ref_force"])
 
 
+@pytest.mark.parametrize("fused", [1, 0], ids=["fused", "sixkernel"])
 @pytest.mark.parametrize("name", NAMES)
-def test_cg_vs_reference(sm, name):
+def test_cg_vs_reference(sm, name, fused):
+    """Both CG paths: the two-pass fused iteration (default) and the six-kernel sequence."""
     meta, a = load_fixture(name)
     Nx, Nt, m0 = meta["Nx"], meta["Nt"], meta["m0"]
     S = Nx * Nt
     L = sm.init(Nx, Nt)
+    sm.check(sm.lib.sm_tune_cg(L.ctx, fused, 0))
     U, psi = as_spinor(sm, a["U"], S), as_spinor(sm, a["psi"], S)
     x = sm.spinor(S)
     assert sm.conjugate_gradient(U, psi, x, m0) == 1
