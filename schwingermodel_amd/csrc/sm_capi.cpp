@@ -71,7 +71,7 @@ struct sm_ctx {
     ncclComm_t comm = nullptr;
     bool hosted = false;            // host-callback transport instead of RCCL
     sm_host_transport tr{};
-    double *h_face = nullptr;       // pinned: send_lo, send_hi, recv_lo, recv_hi (4 x 4Nx doubles)
+    double *h_face = nullptr;       // pinned: send_lo, send_hi, recv_lo, recv_hi (4 x up to 8Nx doubles)
     double *h_red = nullptr;        // pinned: all-reduce staging (8 doubles)
     bool have_gauge = false;
     double2 *U = nullptr;          // 2V
@@ -132,7 +132,11 @@ int down_rank(const sm_ctx *c) { return (c->shard - 1 + c->nshard) % c->nshard; 
 // My t = Wt-1 column goes up (it is the up-neighbour's t = -1), my t = 0
 // column goes down (the down-neighbour's t = Wt). The face buffers are
 // [plane][x], 4*Nx doubles.
+// Largest face exchanged, in doubles per x: 2 columns x 2 planes x complex.
+constexpr size_t kMaxFaceDoubles = 8;
+
 int exchange_faces(sm_ctx *c, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi, size_t cnt) {
+    if (cnt > kMaxFaceDoubles * (size_t)c->g.Nx) return fail(SM_ERR_ARG, "face too large (%zu)", cnt);
     if (c->hosted) {
         double *h = c->h_face;
         HIP_TRY(hipMemcpyAsync(h, slo, cnt * 8, hipMemcpyDeviceToHost, c->stream));
@@ -382,7 +386,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     chk(hipMalloc(&c->sc, sizeof(CGScalars)));
     chk(hipHostMalloc(&c->h_sc, sizeof(CGScalars)));
     chk(hipHostMalloc(&c->h_sums, sizeof(double2) * 4));
-    chk(hipHostMalloc(&c->h_face, sizeof(double) * 16 * (size_t)Nx));
+    chk(hipHostMalloc(&c->h_face, sizeof(double) * 4 * kMaxFaceDoubles * (size_t)Nx));
     chk(hipHostMalloc(&c->h_red, sizeof(double) * 8));
     if (e == hipSuccess) chk(hipMemset(c->sc, 0, sizeof(CGScalars)));
     if (e != hipSuccess) {

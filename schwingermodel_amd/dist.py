@@ -84,7 +84,7 @@ class GlooTransport:
             exchange_faces(_arr(sd, n), _arr(su, n), _arr(rl, n), _arr(rh, n))
             return 0
         except Exception as e:  # noqa: BLE001 -- no exceptions across the C boundary
-            self.error = e
+            self._report(e)
             return 1
 
     def _allreduce(self, user, buf, n):
@@ -92,8 +92,14 @@ class GlooTransport:
             allreduce_sum(_arr(buf, n))
             return 0
         except Exception as e:  # noqa: BLE001
-            self.error = e
+            self._report(e)
             return 1
+
+    def _report(self, e):
+        import sys
+        import traceback
+        self.error = e
+        traceback.print_exception(type(e), e, e.__traceback__, file=sys.stderr)
 
 
 def create_hosted_context(Nx, Nt, device=0):
