@@ -141,11 +141,11 @@ __global__ void __launch_bounds__(256) cg_fused_kernel(CGFArgs a) {
             d.b = first ? R.d1 : cadd(cmul(R.d1, beta), R.r1);
             if (xr >= x0 && xr < xe && own) {
                 const long n = (long)xr * Wt + c;
-                a.dnew[n] = d.a;
-                a.dnew[n + a.V] = d.b;
+                st_nt(a.dnew + n, d.a);
+                st_nt(a.dnew + n + a.V, d.b);
                 if (!first) {
-                    a.x[n] = cadd(R.x0, cmul(alpha, R.d0));
-                    a.x[n + a.V] = cadd(R.x1, cmul(alpha, R.d1));
+                    st_nt(a.x + n, cadd(R.x0, cmul(alpha, R.d0)));
+                    st_nt(a.x + n + a.V, cadd(R.x1, cmul(alpha, R.d1)));
                 }
             }
             return d;
@@ -196,8 +196,8 @@ __global__ void __launch_bounds__(256) cg_fused_kernel(CGFArgs a) {
                           utc, uxc, utmc, uxp, o.a, o.b);
             if (own) {
                 const long n = (long)x * Wt + c;
-                a.Ad[n] = o.a;
-                a.Ad[n + a.V] = o.b;
+                st_nt(a.Ad + n, o.a);
+                st_nt(a.Ad + n + a.V, o.b);
                 acc = cadd(acc, cmul(dc.a, cconj(o.a)));  // dot(d, Ad), include/variables.h:185-188
                 acc = cadd(acc, cmul(dc.b, cconj(o.b)));
             }
@@ -222,7 +222,7 @@ CGFusedCfg cg_fused_config(const Geometry &g) {
     CGFusedCfg c;
     c.NWT = (g.Wt + FW - 1) / FW;
     c.TBk = (c.NWT + 3) / 4;
-    int target = 1024;
+    int target = 4096;  // 4096^2: xchunk 18 (tools/tune_cg.py: 16-32 best, 128 -12 %)
     if (const char *e = getenv("SM_CGF_BLOCKS")) target = atoi(e);
     int nchunks = (target + c.TBk - 1) / c.TBk;
     if (nchunks > g.Nx) nchunks = g.Nx;
@@ -259,11 +259,20 @@ __global__ void __launch_bounds__(RB2) cg_update_r_kernel(long n, double2 *r, co
     if (sc->done) return;
     const double2 alpha = sc->alpha;
     double2 acc = make_double2(0.0, 0.0);
-    for (long i = (long)blockIdx.x * RB2 + threadIdx.x; i < n; i += (long)gridDim.x * RB2) {
-        const double2 ri = csub(r[i], cmul(alpha, Ad[i]));
-        r[i] = ri;
+    const Chunk ch = block_chunk(n);
+    auto f = [&](long i) {
+        const double2 ri = csub(ld_nt(r + i), cmul(alpha, ld_nt(Ad + i)));
+        st_nt(r + i, ri);
         acc = cadd(acc, cmul(ri, cconj(ri)));
+    };
+    long i = ch.beg + threadIdx.x;
+    for (; i + 3 * RB2 < ch.end; i += 4 * RB2) {
+        f(i);
+        f(i + RB2);
+        f(i + 2 * RB2);
+        f(i + 3 * RB2);
     }
+    for (; i < ch.end; i += RB2) f(i);
     const double2 s = block_sum(acc, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
@@ -281,8 +290,8 @@ __global__ void __launch_bounds__(RB2) cg_finish_x_kernel(long n, double2 *x, co
     if (k < 1) return;
     const double2 alpha = sc->alpha;
     const double2 *d = (k & 1) ? d1 : d0;
-    for (long i = (long)blockIdx.x * RB2 + threadIdx.x; i < n; i += (long)gridDim.x * RB2)
-        x[i] = cadd(x[i], cmul(alpha, d[i]));
+    const Chunk ch = block_chunk(n);
+    for (long i = ch.beg + threadIdx.x; i < ch.end; i += RB2) x[i] = cadd(x[i], cmul(alpha, d[i]));
 }
 
 void launch_cg_finish_x(hipStream_t s, long n, double2 *x, const double2 *d0, const double2 *d1,

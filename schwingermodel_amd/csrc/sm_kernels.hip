@@ -137,8 +137,8 @@ __device__ __forceinline__ void dslash_body(const DArgs &a) {
                 double2 s0, s1;
                 dirac_site<DAG>(a.mass, sr0, sl0, cur.c0, cur.c1, cur.p0, cur.p1, nxt.c0, nxt.c1,
                                 cur.m0, cur.m1, pxm0, pxm1, cur.ut, cur.ux, cur.utm, uxm, s0, s1);
-                a.out[n] = s0;
-                a.out[n + V] = s1;
+                st_nt(a.out + n, s0);
+                st_nt(a.out + n + V, s1);
                 if (EPI == EPI_DOT) {
                     acc = cadd(acc, cmul(ax0, cconj(s0)));
                     acc = cadd(acc, cmul(ax1, cconj(s1)));
@@ -166,8 +166,8 @@ __device__ __forceinline__ void dslash_body(const DArgs &a) {
             double2 s0, s1;
             dirac_site<DAG>(a.mass, sr0, sl0, cur.c0, cur.c1, cur.p0, cur.p1, nx1.c0, nx1.c1,
                             cur.m0, cur.m1, pxm0, pxm1, cur.ut, cur.ux, cur.utm, uxm, s0, s1);
-            a.out[n] = s0;
-            a.out[n + V] = s1;
+            st_nt(a.out + n, s0);
+            st_nt(a.out + n + V, s1);
             if (EPI == EPI_DOT) {
                 // dot(aux, out) = sum aux * conj(out), include/variables.h:185-188
                 acc = cadd(acc, cmul(ax0, cconj(s0)));
@@ -208,7 +208,7 @@ LaunchCfg dslash_config(const Geometry &g) {
     c.bt = g.Wt >= 256 ? 256 : (g.Wt >= 128 ? 128 : 64);
     if (const char *e = getenv("SM_BT")) c.bt = atoi(e);
     const int tb = (g.Wt + c.bt - 1) / c.bt;
-    int target = 2048;  // blocks: >> 256 CUs, several waves per SIMD
+    int target = 2048;  // blocks: >> 256 CUs; 4096^2: xchunk 32 (tools/tune_dslash.py)
     if (const char *e = getenv("SM_BLOCKS")) target = atoi(e);
     int nchunks = (target + tb - 1) / tb;
     if (nchunks > g.Nx) nchunks = g.Nx;
@@ -217,7 +217,7 @@ LaunchCfg dslash_config(const Geometry &g) {
     if (const char *e = getenv("SM_XCHUNK")) c.xchunk = atoi(e);
     c.xcd_remap = 1;
     if (const char *e = getenv("SM_XCD_REMAP")) c.xcd_remap = atoi(e);
-    c.variant = 0;
+    c.variant = 1;  // two-row lookahead: 296 vs 315 us at 4096^2 (profiles/r01)
     if (const char *e = getenv("SM_DSLASH_VARIANT")) c.variant = atoi(e);
     return c;
 }
@@ -334,12 +334,26 @@ int reduce_blocks(long n) {
     return (int)nb;
 }
 
+// Streaming loop over this block's chunk: f(i) for every i, 4 lane-tiles per
+// step so 4 independent 16-B accesses per operand are in flight.
+template <typename F>
+__device__ __forceinline__ void chunk_loop(long n, F f) {
+    const Chunk c = block_chunk(n);
+    long i = c.beg + threadIdx.x;
+    for (; i + 3 * RB < c.end; i += 4 * RB) {
+        f(i);
+        f(i + RB);
+        f(i + 2 * RB);
+        f(i + 3 * RB);
+    }
+    for (; i < c.end; i += RB) f(i);
+}
+
 __global__ void __launch_bounds__(RB) dot_partial_kernel(long n, const double2 *a, const double2 *b,
                                                          double2 *part) {
     __shared__ double2 sh[RB / 64];
     double2 acc = make_double2(0.0, 0.0);
-    for (long i = (long)blockIdx.x * RB + threadIdx.x; i < n; i += (long)gridDim.x * RB)
-        acc = cadd(acc, cmul(a[i], cconj(b[i])));
+    chunk_loop(n, [&](long i) { acc = cadd(acc, cmul(ld_nt(a + i), cconj(ld_nt(b + i)))); });
     double2 s = block_sum(acc, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
@@ -365,7 +379,7 @@ void launch_sum_partials(hipStream_t s, int nparts, const double2 *partials, dou
 }
 
 __global__ void __launch_bounds__(RB) copy_kernel(long n, const double2 *src, double2 *dst) {
-    for (long i = (long)blockIdx.x * RB + threadIdx.x; i < n; i += (long)gridDim.x * RB) dst[i] = src[i];
+    chunk_loop(n, [&](long i) { st_nt(dst + i, ld_nt(src + i)); });
 }
 
 void launch_copy(hipStream_t s, long n, const double2 *src, double2 *dst) {
@@ -378,14 +392,14 @@ __global__ void __launch_bounds__(RB) cg_init_kernel(long n, const double2 *phi,
                                                      double2 *ppp) {
     __shared__ double2 sh[RB / 64];
     double2 arr = make_double2(0.0, 0.0), app = make_double2(0.0, 0.0);
-    for (long i = (long)blockIdx.x * RB + threadIdx.x; i < n; i += (long)gridDim.x * RB) {
-        const double2 p = phi[i];
-        const double2 ri = csub(p, Ax[i]);
-        r[i] = ri;
-        d[i] = ri;
+    chunk_loop(n, [&](long i) {
+        const double2 p = ld_nt(phi + i);
+        const double2 ri = csub(p, ld_nt(Ax + i));
+        st_nt(r + i, ri);
+        st_nt(d + i, ri);
         arr = cadd(arr, cmul(ri, cconj(ri)));
         app = cadd(app, cmul(p, cconj(p)));
-    }
+    });
     double2 s1 = block_sum(arr, sh);
     __syncthreads();
     double2 s2 = block_sum(app, sh);
@@ -450,12 +464,12 @@ __global__ void __launch_bounds__(RB) cg_update_xr_kernel(long n, double2 *x, do
     if (sc->done) return;
     const double2 alpha = sc->alpha;
     double2 acc = make_double2(0.0, 0.0);
-    for (long i = (long)blockIdx.x * RB + threadIdx.x; i < n; i += (long)gridDim.x * RB) {
-        x[i] = cadd(x[i], cmul(alpha, d[i]));
-        const double2 ri = csub(r[i], cmul(alpha, Ad[i]));
-        r[i] = ri;
+    chunk_loop(n, [&](long i) {
+        st_nt(x + i, cadd(ld_nt(x + i), cmul(alpha, ld_nt(d + i))));
+        const double2 ri = csub(ld_nt(r + i), cmul(alpha, ld_nt(Ad + i)));
+        st_nt(r + i, ri);
         acc = cadd(acc, cmul(ri, cconj(ri)));
-    }
+    });
     double2 s = block_sum(acc, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
@@ -496,8 +510,7 @@ __global__ void __launch_bounds__(RB) cg_update_d_kernel(long n, double2 *d, con
                                                          const CGScalars *sc) {
     if (sc->done) return;
     const double2 beta = sc->beta;
-    for (long i = (long)blockIdx.x * RB + threadIdx.x; i < n; i += (long)gridDim.x * RB)
-        d[i] = cadd(cmul(d[i], beta), r[i]);
+    chunk_loop(n, [&](long i) { st_nt(d + i, cadd(cmul(ld_nt(d + i), beta), ld_nt(r + i))); });
 }
 
 void launch_cg_update_d(hipStream_t s, long n, double2 *d, const double2 *r, const CGScalars *sc) {
@@ -545,22 +558,18 @@ template <int TWO>
 __global__ void __launch_bounds__(256) stream_kernel(long n, const double2 *__restrict__ a,
                                                      const double2 *__restrict__ b,
                                                      double2 *__restrict__ out) {
-    const long stride = (long)gridDim.x * 256;
-    long i = (long)blockIdx.x * 256 + threadIdx.x;
-    for (; i + 3 * stride < n; i += 4 * stride) {
-        double2 x0 = a[i], x1 = a[i + stride], x2 = a[i + 2 * stride], x3 = a[i + 3 * stride];
-        if (TWO) {
-            const double2 y0 = b[i], y1 = b[i + stride], y2 = b[i + 2 * stride], y3 = b[i + 3 * stride];
-            x0 = cadd(x0, y0); x1 = cadd(x1, y1); x2 = cadd(x2, y2); x3 = cadd(x3, y3);
-        }
-        out[i] = x0; out[i + stride] = x1; out[i + 2 * stride] = x2; out[i + 3 * stride] = x3;
-    }
-    for (; i < n; i += stride) out[i] = TWO ? cadd(a[i], b[i]) : a[i];
+    // the measured-best streaming form (tools/membench.hip): block-contiguous
+    // chunks, 4 tiles in flight, non-temporal loads and stores
+    chunk_loop(n, [&](long i) {
+        double2 v = ld_nt(a + i);
+        if (TWO) v = cadd(v, ld_nt(b + i));
+        st_nt(out + i, v);
+    });
 }
 
 void launch_stream(hipStream_t s, int two, long n, const double2 *a, const double2 *b, double2 *out,
                    int blocks) {
-    if (blocks <= 0) blocks = 4096;
+    if (blocks <= 0) blocks = 2048;
     if (two) hipLaunchKernelGGL(stream_kernel<1>, dim3(blocks), dim3(256), 0, s, n, a, b, out);
     else hipLaunchKernelGGL(stream_kernel<0>, dim3(blocks), dim3(256), 0, s, n, a, b, out);
 }
