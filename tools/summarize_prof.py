@@ -67,10 +67,11 @@ def main():
             e["avg_ns"] = avg_ns[k]
             e["hbm_GBps"] = (rd + wr) / avg_ns[k]
         kernels[k] = e
-    dslash = [k for k in kernels if k.startswith("void sm::dslash_kernel<0, 0>")]
+    dslash = [k for k in kernels if "dslash_kernel" in k and "<0, 0>" in k]
     out = {"Nx": a.nx, "Nt": a.nt, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes",
            "correction": "reads = 2 x FETCH_SIZE KiB (gfx950), writes = WRITE_SIZE KiB",
            "algorithmic_bytes_per_launch": 96 * sites,
+           "dslash_kernel": dslash[0] if dslash else None,
            "hbm_bytes_per_launch": kernels[dslash[0]]["hbm_bytes"] if dslash else None,
            "kernels": kernels}
     with open(os.path.join(pdir, f"{tag}_dslash_pmc.json"), "w") as f:
