@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -68,6 +69,8 @@ struct sm_ctx {
     CGFusedCfg fcfg{};
     int cg_fused = 1;               // 1: two-pass fused CG iteration (sm_cgfused.hip)
     hipStream_t own_stream = nullptr, stream = nullptr;
+    hipStream_t comm_stream = nullptr;  // halo exchange overlapped with interior compute
+    hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
     ncclComm_t comm = nullptr;
     bool hosted = false;            // host-callback transport instead of RCCL
     sm_host_transport tr{};
@@ -78,7 +81,7 @@ struct sm_ctx {
     double2 *ghostU = nullptr;     // Nx: U_t at local t = -1 (lower neighbour's last column)
     double2 *fields = nullptr;     // NFIELDS * 2V
     double2 *faces = nullptr;      // 4 * 2Nx per spinor being exchanged (x2 for force)
-    double2 *faces2 = nullptr;     // 2-deep faces: send lo/hi (4Nx each), recv d, r, U (8Nx each)
+    double2 *faces2 = nullptr;     // 2-deep faces: send lo/hi of 2 fields (4Nx each), recv d, r, U (8Nx each)
     double2 *partials = nullptr;   // 2 * max(nparts)
     double2 *sums = nullptr;       // 4 complex scratch (allreduce)
     double *Fbuf = nullptr;        // 2V doubles (force)
@@ -137,6 +140,7 @@ constexpr size_t kMaxFaceDoubles = 8;
 
 int exchange_faces(sm_ctx *c, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi, size_t cnt) {
     if (cnt > kMaxFaceDoubles * (size_t)c->g.Nx) return fail(SM_ERR_ARG, "face too large (%zu)", cnt);
+    // (RCCL: on the compute stream; the fused CG uses exchange_faces2 on comm_stream)
     if (c->hosted) {
         double *h = c->h_face;
         HIP_TRY(hipMemcpyAsync(h, slo, cnt * 8, hipMemcpyDeviceToHost, c->stream));
@@ -227,15 +231,39 @@ int download_plane_pair(sm_ctx *c, const double2 *src, double *p0, double *p1) {
 
 // 2-deep faces of the fused CG kernel: 4 columns [-2,-1,Wt,Wt+1][plane][x].
 double2 *face2_recv(sm_ctx *c, int which) {  // 0: d, 1: r, 2: U
-    return c->faces2 + (size_t)(8 + 8 * which) * c->g.Nx;
+    return c->faces2 + (size_t)(16 + 8 * which) * c->g.Nx;
+}
+double2 *face2_send(sm_ctx *c, int f, int hi) {  // send buffers of field slot f
+    return c->faces2 + (size_t)(8 * f + 4 * hi) * c->g.Nx;
+}
+
+// Pack and exchange the 2-deep faces of nf (<= 2) fields in ONE transport
+// round on stream s (RCCL: a single group of 4*nf p2p ops).
+int halo2_multi(sm_ctx *c, hipStream_t s, const double2 *const *fields, double2 *const *faces, int nf) {
+    if (c->nshard == 1) return SM_OK;
+    const size_t cnt = (size_t)8 * c->g.Nx;  // doubles: 2 columns x 2 planes x Nx complex
+    for (int f = 0; f < nf; ++f) launch_pack_faces2(s, c->g, fields[f], face2_send(c, f, 0), face2_send(c, f, 1));
+    if (c->hosted) {
+        if (s != c->stream) HIP_TRY(hipStreamSynchronize(s));
+        for (int f = 0; f < nf; ++f)
+            TRY(exchange_faces(c, face2_send(c, f, 0), face2_send(c, f, 1), faces[f], faces[f] + (size_t)4 * c->g.Nx, cnt));
+        return SM_OK;
+    }
+    NCCL_TRY(ncclGroupStart());
+    for (int f = 0; f < nf; ++f) {
+        NCCL_TRY(ncclSend(face2_send(c, f, 1), cnt, ncclDouble, up_rank(c), c->comm, s));
+        NCCL_TRY(ncclRecv(faces[f], cnt, ncclDouble, down_rank(c), c->comm, s));
+        NCCL_TRY(ncclSend(face2_send(c, f, 0), cnt, ncclDouble, down_rank(c), c->comm, s));
+        NCCL_TRY(ncclRecv(faces[f] + (size_t)4 * c->g.Nx, cnt, ncclDouble, up_rank(c), c->comm, s));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    return SM_OK;
 }
 
 int halo2(sm_ctx *c, const double2 *field, double2 *face) {
-    if (c->nshard == 1) return SM_OK;
-    double2 *slo = c->faces2, *shi = c->faces2 + (size_t)4 * c->g.Nx;
-    launch_pack_faces2(c->stream, c->g, field, slo, shi);
-    const size_t cnt = (size_t)8 * c->g.Nx;  // doubles: 2 columns x 2 planes x Nx complex
-    return exchange_faces(c, slo, shi, face, face + (size_t)4 * c->g.Nx, cnt);
+    const double2 *f[1] = {field};
+    double2 *r[1] = {face};
+    return halo2_multi(c, c->stream, f, r, 1);
 }
 
 int exchange_ghost_U(sm_ctx *c) {
@@ -379,7 +407,10 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     chk(hipMalloc(&c->ghostU, sizeof(double2) * (size_t)Nx));
     chk(hipMalloc(&c->fields, fb * NFIELDS));
     chk(hipMalloc(&c->faces, sizeof(double2) * 2 * (size_t)Nx * 8));
-    chk(hipMalloc(&c->faces2, sizeof(double2) * 32 * (size_t)Nx));
+    chk(hipMalloc(&c->faces2, sizeof(double2) * 40 * (size_t)Nx));
+    chk(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+    chk(hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming));
+    chk(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
     chk(hipMalloc(&c->partials, sizeof(double2) * 2 * (size_t)np));
     chk(hipMalloc(&c->sums, sizeof(double2) * 4));
     chk(hipMalloc(&c->Fbuf, sizeof(double) * 2 * (size_t)c->g.V));
@@ -433,6 +464,10 @@ int sm_destroy(sm_ctx *c) {
     if (c->h_sums) (void)hipHostFree(c->h_sums);
     if (c->h_face) (void)hipHostFree(c->h_face);
     if (c->h_red) (void)hipHostFree(c->h_red);
+    if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
+    if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
+    if (c->ev_halo) (void)hipEventDestroy(c->ev_halo);
+    if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
     return SM_OK;
@@ -603,11 +638,51 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
             // pass 1: d_k, deferred x update, Ad = D D^dag d_k, <d_k, Ad>
             double2 *dold = c->field((c->cg_issued & 1) ? F_D2 : F_D);
             double2 *dnew = c->field((c->cg_issued & 1) ? F_D : F_D2);
-            TRY(halo2(c, dold, face2_recv(c, 0)));
-            TRY(halo2(c, r, face2_recv(c, 1)));
-            launch_cg_fused(c->stream, c->g, c->fcfg, c->nshard, dold, dnew, r, x, Ad, c->U,
-                            face2_recv(c, 0), face2_recv(c, 1), face2_recv(c, 2), c->cg_mass,
-                            c->cg_issued == 0, c->sc, c->partials);
+            const CGFusedCfg &fc = c->fcfg;
+            auto pass1 = [&](int tb0, int tbn) {
+                launch_cg_fused(c->stream, c->g, fc, c->nshard, dold, dnew, r, x, Ad, c->U,
+                                face2_recv(c, 0), face2_recv(c, 1), face2_recv(c, 2), c->cg_mass,
+                                c->cg_issued == 0, c->sc, c->partials, tb0, tbn);
+            };
+            if (c->nshard == 1) {
+                pass1(0, fc.TBk);
+            } else {
+                // Only the first and last t-blocks read the faces: exchange them
+                // (d_{k-1} and r in one round) on the comm stream while the
+                // interior blocks run, then finish the two edge block-columns.
+                const double2 *flds[2] = {dold, r};
+                double2 *fcs[2] = {face2_recv(c, 0), face2_recv(c, 1)};
+                // interior t-blocks: every valid tile's lanes (columns 60g-2 .. 60g+61)
+                // stay inside [0, Wt): they never read a face
+                auto interior = [&](int tb) {
+                    const int g_lo = 4 * tb, g_hi = std::min(4 * tb + 3, fc.NWT - 1);
+                    return kFusedWaveCols * g_lo - 2 >= 0 &&
+                           kFusedWaveCols * g_hi + kFusedWaveCols + 1 <= c->g.Wt - 1;
+                };
+                int tb_lo = 0, tb_hi = -1;
+                for (int tb = 0; tb < fc.TBk; ++tb)
+                    if (interior(tb)) {
+                        if (tb_hi < 0) tb_lo = tb;
+                        tb_hi = tb;
+                    }
+                const bool split = tb_hi >= tb_lo && tb_hi >= 0;
+                if (c->hosted) {
+                    TRY(halo2_multi(c, c->stream, flds, fcs, 2));
+                } else {
+                    HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
+                    HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
+                    TRY(halo2_multi(c, c->comm_stream, flds, fcs, 2));
+                    HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
+                }
+                if (split) pass1(tb_lo, tb_hi - tb_lo + 1);
+                if (!c->hosted) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+                if (split) {
+                    pass1(0, tb_lo);
+                    pass1(tb_hi + 1, fc.TBk - tb_hi - 1);
+                } else {
+                    pass1(0, fc.TBk);
+                }
+            }
             TRY(cg_scalar(c, cg_fused_blocks(c->fcfg), 0));
             // pass 2: r -= alpha Ad, <r, r>; stop test and beta
             launch_cg_update_r(c->stream, n, r, Ad, c->sc, c->partials);

@@ -27,7 +27,7 @@
 
 namespace sm {
 
-constexpr int FW = 60;  // output t-columns per wave
+constexpr int FW = kFusedWaveCols;  // output t-columns per wave
 
 struct CGFArgs {
     const double2 *dold;
@@ -42,6 +42,7 @@ struct CGFArgs {
     long V;
     int Nx, Wt, t0, Ntg, nshard;
     int xchunk, NWT, TBk, XB, remap, first;
+    int tb0, tbn, part0;  // launch covers t-blocks [tb0, tb0+tbn); partials at part0 + blockIdx
     double mass;
 };
 
@@ -94,11 +95,11 @@ __global__ void __launch_bounds__(256) cg_fused_kernel(CGFArgs a) {
     {
         int w = blockIdx.x;
         if (a.remap) {
-            const int n = a.TBk * a.XB, q = n >> 3, rr = n & 7, xcd = w & 7;
+            const int n = a.tbn * a.XB, q = n >> 3, rr = n & 7, xcd = w & 7;
             w = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (w >> 3);
         }
-        tb = w % a.TBk;
-        xc = w / a.TBk;
+        tb = a.tb0 + w % a.tbn;
+        xc = w / a.tbn;
     }
     const int lane = threadIdx.x & 63;
     const int g = tb * 4 + (threadIdx.x >> 6);  // wave tile along t
@@ -215,7 +216,7 @@ __global__ void __launch_bounds__(256) cg_fused_kernel(CGFArgs a) {
         }
     }
     const double2 bs = block_sum(acc, sh);
-    if (threadIdx.x == 0) a.partials[blockIdx.x] = bs;
+    if (threadIdx.x == 0) a.partials[a.part0 + blockIdx.x] = bs;
 }
 
 CGFusedCfg cg_fused_config(const Geometry &g) {
@@ -239,7 +240,8 @@ int cg_fused_blocks(const CGFusedCfg &c) { return c.TBk * c.XB; }
 void launch_cg_fused(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard,
                      const double2 *dold, double2 *dnew, const double2 *r, double2 *x, double2 *Ad,
                      const double2 *U, const double2 *fd, const double2 *fr, const double2 *fU,
-                     double mass, int first, CGScalars *sc, double2 *partials) {
+                     double mass, int first, CGScalars *sc, double2 *partials, int tb0, int tbn) {
+    if (tbn <= 0) return;
     CGFArgs a;
     a.dold = dold; a.dnew = dnew; a.r = r; a.x = x; a.Ad = Ad; a.U = U;
     a.fd = fd; a.fr = fr; a.fU = fU;
@@ -248,7 +250,10 @@ void launch_cg_fused(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int 
     a.xchunk = c.xchunk; a.NWT = c.NWT; a.TBk = c.TBk; a.XB = c.XB; a.remap = c.remap;
     a.first = first;
     a.mass = mass;
-    hipLaunchKernelGGL(cg_fused_kernel, dim3(c.TBk * c.XB), dim3(256), 0, s, a);
+    a.tb0 = tb0;
+    a.tbn = tbn;
+    a.part0 = tb0 * c.XB;  // disjoint partial slots per t-block range
+    hipLaunchKernelGGL(cg_fused_kernel, dim3(tbn * c.XB), dim3(256), 0, s, a);
 }
 
 // ---- pass 2: r -= alpha Ad ; partials <r, r>  (src/conjugate_gradient.cpp:39-43)

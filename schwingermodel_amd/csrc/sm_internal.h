@@ -89,6 +89,7 @@ void launch_cg_beta_from_sum(hipStream_t s, CGScalars *sc);
 void launch_cg_init_from_sums(hipStream_t s, const double2 *rr_pp, CGScalars *sc, double tol);
 
 // ---- fused CG iteration (sm_cgfused.hip) ----
+constexpr int kFusedWaveCols = 60;  // output t-columns per wave (64 lanes - 2x2 halo)
 struct CGFusedCfg {
     int NWT, TBk;        // wave tiles along t (60 columns each), blocks along t (4 waves)
     int xchunk, XB;      // rows per block, blocks along x
@@ -99,7 +100,7 @@ int cg_fused_blocks(const CGFusedCfg &c);
 void launch_cg_fused(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard,
                      const double2 *dold, double2 *dnew, const double2 *r, double2 *x, double2 *Ad,
                      const double2 *U, const double2 *fd, const double2 *fr, const double2 *fU,
-                     double mass, int first, CGScalars *sc, double2 *partials);
+                     double mass, int first, CGScalars *sc, double2 *partials, int tb0, int tbn);
 void launch_cg_update_r(hipStream_t s, long n, double2 *r, const double2 *Ad, const CGScalars *sc,
                         double2 *part);
 void launch_cg_finish_x(hipStream_t s, long n, double2 *x, const double2 *d0, const double2 *d1,

@@ -52,6 +52,34 @@ def faces(mu0, mu1, Nx, Wt):
     return lo, hi
 
 
+def single_reference(sm, a, meta):
+    """One shard (nshard = 1) on this GPU: the reference for a sharded run."""
+    Nx, Nt, m0 = meta["Nx"], meta["Nt"], meta["m0"]
+    S = Nx * Nt
+    P = lambda x: ctypes.c_void_p(x.ctypes.data)  # noqa: E731
+    L = sm.Lattice(Nx, Nt, device=int(os.environ.get("SM_DEVICE", "0")))
+    sm.check(sm.lib.sm_upload_gauge(L.ctx, P(a["U"]), P(a["U"][2 * S:])))
+    for key, src, fn in (("ref_Dpsi", "psi", 0), ("ref_Ddagchi", "chi", 1), ("ref_DDdagpsi", "psi", 2)):
+        out = np.empty(4 * S)
+        i0, i1 = a[src][:2 * S], a[src][2 * S:]
+        if fn < 2:
+            sm.check(sm.lib.sm_dirac(L.ctx, P(i0), P(i1), P(out), P(out[2 * S:]), m0, fn))
+        else:
+            sm.check(sm.lib.sm_ddag(L.ctx, P(i0), P(i1), P(out), P(out[2 * S:]), m0))
+        a[key] = out
+    F = np.empty(2 * S)
+    sm.check(sm.lib.sm_force(L.ctx, P(a["psi"]), P(a["psi"][2 * S:]), P(a["chi"]), P(a["chi"][2 * S:]),
+                             P(F), P(F[S:])))
+    a["ref_force"] = F
+    x = np.empty(4 * S)
+    res = sm.CGResult()
+    sm.check(sm.lib.sm_cg(L.ctx, P(a["psi"]), P(a["psi"][2 * S:]), P(x), P(x[2 * S:]), m0, 1e-10, 10000,
+                          ctypes.byref(res)))
+    a["ref_cgx"] = x
+    meta["cg_iters"] = res.iterations
+    L.close()
+
+
 def main():
     mode, name, result_path = sys.argv[1], sys.argv[2], sys.argv[3]
     import torch.distributed as dist
@@ -61,8 +89,22 @@ def main():
     import schwingermodel_amd as sm
     from schwingermodel_amd import dist as smd
 
-    meta, a = load_fixture(name)
-    Nx, Nt, m0 = meta["Nx"], meta["Nt"], meta["m0"]
+    if name.startswith("gen:"):
+        # gen:<Nx>x<Nt>:<sigma>:<m0> -- synthetic fields; reference = one shard on this GPU
+        _, dims, sigma, m0s = name.split(":")
+        Nx, Nt = (int(v) for v in dims.split("x"))
+        sigma, m0 = float(sigma), float(m0s)
+        S = Nx * Nt
+        a = {k: np.empty(4 * S) for k in ("U", "psi", "chi")}
+        sm.lib.sm_fill_gauge(4321, sigma, Nt, 0, Nx, 0, Nt, a["U"].ctypes.data, a["U"][2 * S:].ctypes.data)
+        sm.lib.sm_fill_spinor(5678, Nt, 0, Nx, 0, Nt, a["psi"].ctypes.data, a["psi"][2 * S:].ctypes.data)
+        sm.lib.sm_fill_spinor(91011, Nt, 0, Nx, 0, Nt, a["chi"].ctypes.data, a["chi"][2 * S:].ctypes.data)
+        meta = {"Nx": Nx, "Nt": Nt, "m0": m0}
+        if rank == 0:
+            single_reference(sm, a, meta)
+    else:
+        meta, a = load_fixture(name)
+        Nx, Nt, m0 = meta["Nx"], meta["Nt"], meta["m0"]
     t0, Wt = ctypes.c_int(), ctypes.c_int()
     sm.check(sm.lib.sm_shard_plan(Nt, world, rank, ctypes.byref(t0), ctypes.byref(Wt)))
     t0, Wt = t0.value, Wt.value
@@ -116,7 +158,7 @@ def main():
     gathered = [None] * world
     dist.all_gather_object(gathered, local)
     if rank == 0:
-        report = {"world": world, "mode": mode, "fixture": name, "checks": {}}
+        report = {"world": world, "mode": mode, "fixture": name, "checks": {}, "Wt": Wt}
         for key in ("ref_Dpsi", "ref_Ddagchi", "ref_DDdagpsi", "ref_force", "ref_cgx"):
             if key not in local:
                 continue

@@ -14,7 +14,11 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("fixture,world", [("l64x64_b2_m0", 2), ("l32x48_b3_m-0p10", 4),
-                                           ("l64x64_b5_m-0p06", 4)])
+                                           ("l64x64_b5_m-0p06", 4),
+                                           # Wt = 512 / 240: the fused CG runs interior and edge
+                                           # t-blocks as separate launches (halo overlap path);
+                                           # reference = one shard on the same GPU
+                                           ("gen:48x1024:0.3:-0.05", 2), ("gen:32x960:0.4242:0.0", 4)])
 def test_sharded_gpu_path_matches_reference(tmp_path, fixture, world):
     rep = run_world("gpu", fixture, world, tmp_path, timeout=600)
     c = rep["checks"]
