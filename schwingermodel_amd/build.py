@@ -59,7 +59,7 @@ def build_oracle(with_reference=None):
     if with_reference and shutil.which("g++"):
         subprocess.run(["make", "-s", "-C", oracle_dir, "ref"], check=True)
         # the reference's own driver code linked against our drop-in shim
-        subprocess.run(["make", "-s", "-C", oracle_dir, "dropin"], check=True)
+        subprocess.run(["make", "-s", "-C", oracle_dir, "dropin", "refapp"], check=True)
 
 
 if __name__ == "__main__":

@@ -59,9 +59,48 @@ def run(cmd, **kw):
     return r.stdout
 
 
+# Large-lattice summary fixtures (BASELINE config 2): full outputs are too big
+# to commit, so keep the reference's outputs at SAMPLE_SITES seeded random
+# sites plus global norms; the GPU test regenerates the inputs with the same
+# counter-based generator (bit-exact, tests/test_capi_host.py) and compares.
+LARGE = [("l1024x1024_b3_m-0p10", 1024, 1024, 0.3246, -0.10)]
+SAMPLE_SITES = 4096
+
+
+def make_large(name, nx, nt, sigma, m0, workdir=None):
+    exe = os.path.join(REF_DIR, f"sm_ref_{nx}x{nt}")
+    with tempfile.TemporaryDirectory() as tmp:
+        d = workdir or tmp
+        if not os.path.exists(os.path.join(d, "meta.json")) or os.path.getsize(os.path.join(d, "meta.json")) == 0:
+            run([exe, "gen", d, str(SEED_U), repr(sigma), str(SEED_PSI), str(SEED_CHI)])
+            meta = json.loads(run([exe, "fixture", d, "1", "1", repr(m0), "1e-10", "10000"]))
+        else:
+            with open(os.path.join(d, "meta.json")) as f:
+                meta = json.load(f)
+        S = nx * nt
+        rng = np.random.default_rng(20261015)
+        sites = np.sort(rng.choice(S, SAMPLE_SITES, replace=False))
+        out = {"sites": sites}
+        for k in OUTS:
+            a = np.fromfile(os.path.join(d, k + ".bin"), dtype=np.float64)
+            if k == "ref_force":
+                out[k] = np.concatenate([a[:S][sites], a[S:][sites]])
+                out[k + "_sumsq"] = np.array([np.dot(a, a)])
+            else:
+                c0 = a[:2 * S].view(np.complex128)
+                c1 = a[2 * S:].view(np.complex128)
+                out[k] = np.concatenate([c0[sites], c1[sites]]).view(np.float64)
+                out[k + "_sumsq"] = np.array([np.dot(a, a)])
+    meta.update({"sigma": sigma, "file": name + ".npz", "summary": True, "sample_sites": SAMPLE_SITES})
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    return meta
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mpi", action="store_true", help="also run 2x2 ranks (mpirun)")
+    ap.add_argument("--large", action="store_true", help="also the 1024^2 summary fixture (~4 min CPU)")
+    ap.add_argument("--large-workdir", default=None, help="reuse an existing reference run directory")
     ap.add_argument("--mpirun", default="/opt/conda/bin/mpirun")
     args = ap.parse_args()
     sizes = sorted({f"{nx}x{nt}" for _, nx, nt, _, _ in FIXTURES})
@@ -97,6 +136,16 @@ def main():
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
         manifest["fixtures"][name] = meta
         print(name, json.dumps(meta), file=sys.stderr)
+    if args.large:
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref", "REF_SIZES=1024x1024"], check=True)
+        manifest["large"] = {}
+        for name, nx, nt, sigma, m0 in LARGE:
+            manifest["large"][name] = make_large(name, nx, nt, sigma, m0, args.large_workdir)
+    else:
+        old = os.path.join(HERE, "manifest.json")
+        if os.path.exists(old):
+            with open(old) as f:
+                manifest["large"] = json.load(f).get("large", {})
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
 

@@ -1,0 +1,84 @@
+"""BASELINE config 2 at full size: 1024^2, beta=3 field, m0 = -0.10, CG to 1e-10.
+
+The reference's outputs for this lattice (unmodified reference, single rank,
+2485 CG iterations, 240 s on one core) are kept as a summary fixture
+(tests/golden/make_golden.py --large): values at 4096 seeded random sites plus
+the sum of squares of every full output field. The inputs are regenerated on
+the fly with the same counter-based generator (bit-exact, test_capi_host.py).
+
+* D, D^dag, D D^dag, force: bitwise at the sampled sites AND the full-field
+  sum of squares equals the reference's bit for bit (a checksum of the whole
+  field, computed by the same numpy call on both sides).
+* CG: same iteration count (+-1 %), sampled x within 1e-12 relative, true
+  residual < 1e-10.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, bits_equal, ptr
+
+pytestmark = pytest.mark.gpu
+NAME = "l1024x1024_b3_m-0p10"
+
+
+@pytest.fixture(scope="module")
+def case():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        meta = json.load(f)["large"][NAME]
+    with np.load(os.path.join(GOLDEN, meta["file"]), allow_pickle=False) as z:
+        ref = {k: z[k].copy() for k in z.files}
+    import schwingermodel_amd as sm
+    N = meta["Nx"]
+    S = N * N
+    L = sm.init(N, N)
+    U, psi, chi = sm.spinor(S), sm.spinor(S), sm.spinor(S)
+    sm.lib.sm_fill_gauge(4321, meta["sigma"], N, 0, N, 0, N, ptr(U.mu0), ptr(U.mu1))
+    sm.lib.sm_fill_spinor(5678, N, 0, N, 0, N, ptr(psi.mu0), ptr(psi.mu1))
+    sm.lib.sm_fill_spinor(91011, N, 0, N, 0, N, ptr(chi.mu0), ptr(chi.mu1))
+    yield sm, L, meta, ref, U, psi, chi
+    L.close()
+
+
+def sample(s, sites):
+    return np.concatenate([s.mu0[sites], s.mu1[sites]]).view(np.float64)
+
+
+def flat(s):
+    return np.concatenate([s.mu0.view(np.float64), s.mu1.view(np.float64)])
+
+
+def test_operators_bitwise_1024(case):
+    sm, L, meta, ref, U, psi, chi = case
+    sites = ref["sites"]
+    S = meta["Nx"] * meta["Nt"]
+    out = sm.spinor(S)
+    for key, fn, src in (("ref_Dpsi", sm.D_phi, psi), ("ref_Ddagchi", sm.D_dagger_phi, chi),
+                         ("ref_DDdagpsi", sm.D_D_dagger_phi, psi)):
+        fn(U, src, out, meta["m0"])
+        assert bits_equal(sample(out, sites), ref[key]), key
+        f = flat(out)
+        assert bits_equal(np.array([np.dot(f, f)]), ref[key + "_sumsq"]), key
+    F = sm.phi_dag_partialD_phi(U, psi, chi)
+    assert bits_equal(np.concatenate([F.mu0[sites], F.mu1[sites]]), ref["ref_force"])
+    f = np.concatenate([F.mu0, F.mu1])
+    assert bits_equal(np.array([np.dot(f, f)]), ref["ref_force_sumsq"])
+
+
+def test_cg_1024_matches_reference(case):
+    sm, L, meta, ref, U, psi, chi = case
+    S = meta["Nx"] * meta["Nt"]
+    x = sm.spinor(S)
+    assert sm.conjugate_gradient(U, psi, x, meta["m0"]) == 1
+    it, ref_it = L.last_cg.iterations, meta["cg_iters"]
+    assert abs(it - ref_it) <= max(1, ref_it // 100), (it, ref_it)
+    xs, xr = sample(x, ref["sites"]), ref["ref_cgx"]
+    assert np.linalg.norm(xs - xr) / np.linalg.norm(xr) <= 1e-12
+    f = flat(x)
+    assert abs(np.dot(f, f) - ref["ref_cgx_sumsq"][0]) <= 2e-12 * ref["ref_cgx_sumsq"][0]
+    Ax = sm.spinor(S)
+    sm.D_D_dagger_phi(U, x, Ax, meta["m0"])
+    r = np.concatenate([psi.mu0 - Ax.mu0, psi.mu1 - Ax.mu1])
+    assert np.linalg.norm(r) / np.linalg.norm(np.concatenate([psi.mu0, psi.mu1])) < 1e-10

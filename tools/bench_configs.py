@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Time-to-solution for the BASELINE.json configs on one GPU (JSON lines).
+
+    python tools/bench_configs.py [--configs 2,3,5] [--hmc]
+
+config 2: 1024^2, beta=3 field (sigma 0.3246), m0=-0.10, CG to 1e-10
+config 3: 4096^2, beta=5 field (sigma 0.2374), m0=-0.06, CG to 1e-10
+config 5: 8192^2, beta=2 field (sigma 0.4242), m0=-0.19 (near m_crit), CG to 1e-10,
+          here on ONE GPU (8 GiB per field fits the 288 GB HBM)
+--hmc:    config 1, the reference HMC program (64^2, beta=2, m0=0, 10 MD steps)
+          on the GPU through the drop-in shim vs the unmodified CPU reference,
+          same stdin parameters (oracle/_ref/SM_64x64_hip vs SM_64x64_ref).
+Inputs are resident in HBM before timing; the solve includes sm_cg_begin
+(x0 = phi, r0, norms) and the final x update, like conjugate_gradient().
+"""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+CONFIGS = {
+    2: dict(N=1024, sigma=0.3246, m0=-0.10),
+    3: dict(N=4096, sigma=0.2374, m0=-0.06),
+    5: dict(N=8192, sigma=0.4242, m0=-0.19),
+}
+
+
+def fill_parallel(sm, N, sigma, U, p, nthreads=16):
+    """Counter-based generator is row-separable: fill row blocks in threads."""
+    from concurrent.futures import ThreadPoolExecutor
+    V = N * N
+    rows = max(1, N // nthreads)
+
+    def job(x0):
+        nx = min(rows, N - x0)
+        off = 2 * x0 * N
+        sm.lib.sm_fill_gauge(4321, sigma, N, x0, nx, 0, N, U[off:].ctypes.data, U[2 * V + off:].ctypes.data)
+        sm.lib.sm_fill_spinor(91011, N, x0, nx, 0, N, p[off:].ctypes.data, p[2 * V + off:].ctypes.data)
+    with ThreadPoolExecutor(nthreads) as ex:
+        list(ex.map(job, range(0, N, rows)))
+
+
+def run_config(cid, tol=1e-10):
+    import torch
+    import schwingermodel_amd as sm
+    c = CONFIGS[cid]
+    N = c["N"]
+    V = N * N
+    L = sm.Lattice(N, N)
+    s = torch.cuda.Stream()
+    torch.cuda.set_stream(s)
+    vp = ctypes.c_void_p
+    sm.check(sm.lib.sm_set_stream(L.ctx, vp(s.cuda_stream)))
+    U = torch.empty(4 * V, dtype=torch.float64)
+    p = torch.empty(4 * V, dtype=torch.float64)
+    t = time.perf_counter()
+    fill_parallel(sm, N, c["sigma"], U.numpy(), p.numpy())
+    gen_s = time.perf_counter() - t
+    dU, dp = U.cuda(), p.cuda()
+    del U, p
+    x = torch.empty_like(dp)
+    sm.check(sm.lib.sm_upload_gauge_dev(L.ctx, vp(dU.data_ptr())))
+    torch.cuda.synchronize()
+    res = sm.CGResult()
+    t = time.perf_counter()
+    sm.check(sm.lib.sm_cg_dev(L.ctx, vp(dp.data_ptr()), vp(x.data_ptr()), c["m0"], tol, 100000, ctypes.byref(res)))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t
+    # independent true residual |phi - D D^dag x| / |phi|
+    Ax = torch.empty_like(dp)
+    sm.check(sm.lib.sm_ddag_dev(L.ctx, vp(x.data_ptr()), vp(Ax.data_ptr()), c["m0"]))
+    torch.cuda.synchronize()
+    relres = float(torch.linalg.vector_norm(dp - Ax) / torch.linalg.vector_norm(dp))
+    out = {"config": cid, "lattice": f"{N}x{N}", "sigma": c["sigma"], "m0": c["m0"], "tol": tol,
+           "converged": res.converged, "iterations": res.iterations, "seconds": round(dt, 4),
+           "it_per_s": round(res.iterations / dt, 1), "ms_per_it": round(1e3 * dt / max(1, res.iterations), 4),
+           "true_relres": relres, "host_gen_s": round(gen_s, 2)}
+    L.close()
+    return out
+
+
+def run_hmc():
+    params = "1\n1\n0\n10\n1\n2\n10\n20\n0\n0\n"  # rx rt m0 MD tau beta Ntherm Nmeas Nsteps save
+    out = {"config": 1, "lattice": "64x64", "params": "m0=0 MD=10 tau=1 beta=2 Ntherm=10 Nmeas=20 Nsteps=0"}
+    for tag in ("hip", "ref"):
+        exe = os.path.join(REPO, "oracle", "_ref", f"SM_64x64_{tag}")
+        if not os.path.exists(exe):
+            out[tag] = None
+            continue
+        env = dict(os.environ, HOSTNAME=os.environ.get("HOSTNAME", "box"))
+        with __import__("tempfile").TemporaryDirectory() as d:
+            t = time.perf_counter()
+            r = subprocess.run([exe], input=params, capture_output=True, text=True, env=env, cwd=d, timeout=900)
+            dt = time.perf_counter() - t
+        line = [ln for ln in r.stdout.splitlines() if "Execution time" in ln]
+        out[tag] = {"wall_s": round(dt, 2), "reported": line[-1] if line else r.stderr[-300:]}
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="2,3,5")
+    ap.add_argument("--hmc", action="store_true")
+    a = ap.parse_args()
+    for cid in [int(v) for v in a.configs.split(",") if v]:
+        print(json.dumps(run_config(cid)), flush=True)
+    if a.hmc:
+        print(json.dumps(run_hmc()), flush=True)
+
+
+if __name__ == "__main__":
+    main()
