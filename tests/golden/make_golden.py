@@ -21,7 +21,9 @@ global layout: two planes of interleaved complex, n = x*Nt + t) and
 tests/golden/manifest.json. The fixtures are data, not reference source.
 """
 import argparse
+import hashlib
 import json
+import math
 import os
 import subprocess
 import sys
@@ -78,6 +80,7 @@ def make_large(name, nx, nt, sigma, m0, workdir=None):
             with open(os.path.join(d, "meta.json")) as f:
                 meta = json.load(f)
         S = nx * nt
+        meta_sha, meta_sumsq = {}, {}
         rng = np.random.default_rng(20261015)
         sites = np.sort(rng.choice(S, SAMPLE_SITES, replace=False))
         out = {"sites": sites}
@@ -85,13 +88,16 @@ def make_large(name, nx, nt, sigma, m0, workdir=None):
             a = np.fromfile(os.path.join(d, k + ".bin"), dtype=np.float64)
             if k == "ref_force":
                 out[k] = np.concatenate([a[:S][sites], a[S:][sites]])
-                out[k + "_sumsq"] = np.array([np.dot(a, a)])
             else:
                 c0 = a[:2 * S].view(np.complex128)
                 c1 = a[2 * S:].view(np.complex128)
                 out[k] = np.concatenate([c0[sites], c1[sites]]).view(np.float64)
-                out[k + "_sumsq"] = np.array([np.dot(a, a)])
-    meta.update({"sigma": sigma, "file": name + ".npz", "summary": True, "sample_sites": SAMPLE_SITES})
+            # machine-independent whole-field checks: SHA-256 of the bytes (the
+            # bitwise outputs) and the exactly rounded sum of squares (CG x)
+            meta_sha[k] = hashlib.sha256(a.tobytes()).hexdigest()
+            meta_sumsq[k] = math.fsum((a * a).tolist())
+    meta.update({"sigma": sigma, "file": name + ".npz", "summary": True, "sample_sites": SAMPLE_SITES,
+                 "sha256": meta_sha, "fsum_sq": meta_sumsq})
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
     return meta
 
