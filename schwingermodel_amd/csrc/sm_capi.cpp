@@ -138,28 +138,32 @@ int down_rank(const sm_ctx *c) { return (c->shard - 1 + c->nshard) % c->nshard; 
 // Largest face exchanged, in doubles per x: 2 columns x 2 planes x complex.
 constexpr size_t kMaxFaceDoubles = 8;
 
-int exchange_faces(sm_ctx *c, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi, size_t cnt) {
+int exchange_faces_on(sm_ctx *c, hipStream_t s, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi,
+                      size_t cnt) {
     if (cnt > kMaxFaceDoubles * (size_t)c->g.Nx) return fail(SM_ERR_ARG, "face too large (%zu)", cnt);
-    // (RCCL: on the compute stream; the fused CG uses exchange_faces2 on comm_stream)
     if (c->hosted) {
         double *h = c->h_face;
-        HIP_TRY(hipMemcpyAsync(h, slo, cnt * 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipMemcpyAsync(h + cnt, shi, cnt * 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipMemcpyAsync(h, slo, cnt * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(h + cnt, shi, cnt * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
         if (c->tr.exchange(c->tr.user, h, h + cnt, h + 2 * cnt, h + 3 * cnt, (long)cnt) != 0)
             return fail(SM_ERR_ARG, "host transport exchange failed");
-        HIP_TRY(hipMemcpyAsync(rlo, h + 2 * cnt, cnt * 8, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipMemcpyAsync(rhi, h + 3 * cnt, cnt * 8, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));  // staging buffers are reused
+        HIP_TRY(hipMemcpyAsync(rlo, h + 2 * cnt, cnt * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(rhi, h + 3 * cnt, cnt * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipStreamSynchronize(s));  // staging buffers are reused
         return SM_OK;
     }
     NCCL_TRY(ncclGroupStart());
-    NCCL_TRY(ncclSend(shi, cnt, ncclDouble, up_rank(c), c->comm, c->stream));
-    NCCL_TRY(ncclRecv(rlo, cnt, ncclDouble, down_rank(c), c->comm, c->stream));
-    NCCL_TRY(ncclSend(slo, cnt, ncclDouble, down_rank(c), c->comm, c->stream));
-    NCCL_TRY(ncclRecv(rhi, cnt, ncclDouble, up_rank(c), c->comm, c->stream));
+    NCCL_TRY(ncclSend(shi, cnt, ncclDouble, up_rank(c), c->comm, s));
+    NCCL_TRY(ncclRecv(rlo, cnt, ncclDouble, down_rank(c), c->comm, s));
+    NCCL_TRY(ncclSend(slo, cnt, ncclDouble, down_rank(c), c->comm, s));
+    NCCL_TRY(ncclRecv(rhi, cnt, ncclDouble, up_rank(c), c->comm, s));
     NCCL_TRY(ncclGroupEnd());
     return SM_OK;
+}
+
+int exchange_faces(sm_ctx *c, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi, size_t cnt) {
+    return exchange_faces_on(c, c->stream, slo, shi, rlo, rhi, cnt);
 }
 
 // In-place global sum of n doubles resident on the device.
@@ -196,8 +200,28 @@ const double2 *loU(sm_ctx *c) { return c->nshard == 1 ? c->U + (c->g.Wt - 1) : c
 int apply(sm_ctx *c, const double2 *in, double2 *out, double mass, int dagger, const double2 *aux,
           double2 *partials, const CGScalars *skip) {
     TFaces f;
-    TRY(halo(c, in, 0, &f));
-    launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip);
+    const int TB = (c->g.Wt + c->cfg.bt - 1) / c->cfg.bt;
+    if (c->nshard == 1 || TB < 3) {
+        TRY(halo(c, in, 0, &f));
+        launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip);
+    } else {
+        // t-blocks 1..TB-2 never touch t = 0 / Wt-1: run them while the faces
+        // travel on the comm stream, then the two edge block-columns
+        double2 *slo = face_buf(c, 0, 0), *shi = face_buf(c, 0, 1);
+        double2 *rlo = face_buf(c, 0, 2), *rhi = face_buf(c, 0, 3);
+        HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
+        HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
+        launch_pack_faces(c->comm_stream, c->g, in, slo, shi);
+        TRY(exchange_faces_on(c, c->comm_stream, slo, shi, rlo, rhi, (size_t)4 * c->g.Nx));
+        HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
+        f = faces_for(c, in, rlo, rhi);
+        launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip,
+                      1, TB - 2);
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+        launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip, 0, 1);
+        launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip,
+                      TB - 1, 1);
+    }
     HIP_TRY(hipGetLastError());
     return SM_OK;
 }
@@ -244,9 +268,9 @@ int halo2_multi(sm_ctx *c, hipStream_t s, const double2 *const *fields, double2 
     const size_t cnt = (size_t)8 * c->g.Nx;  // doubles: 2 columns x 2 planes x Nx complex
     for (int f = 0; f < nf; ++f) launch_pack_faces2(s, c->g, fields[f], face2_send(c, f, 0), face2_send(c, f, 1));
     if (c->hosted) {
-        if (s != c->stream) HIP_TRY(hipStreamSynchronize(s));
         for (int f = 0; f < nf; ++f)
-            TRY(exchange_faces(c, face2_send(c, f, 0), face2_send(c, f, 1), faces[f], faces[f] + (size_t)4 * c->g.Nx, cnt));
+            TRY(exchange_faces_on(c, s, face2_send(c, f, 0), face2_send(c, f, 1), faces[f],
+                                  faces[f] + (size_t)4 * c->g.Nx, cnt));
         return SM_OK;
     }
     NCCL_TRY(ncclGroupStart());
@@ -666,16 +690,14 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
                         tb_hi = tb;
                     }
                 const bool split = tb_hi >= tb_lo && tb_hi >= 0;
-                if (c->hosted) {
-                    TRY(halo2_multi(c, c->stream, flds, fcs, 2));
-                } else {
-                    HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
-                    HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
-                    TRY(halo2_multi(c, c->comm_stream, flds, fcs, 2));
-                    HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
-                }
+                // (the host transport runs the same stream/event sequence; its
+                // exchange blocks the host, so it just does not overlap)
+                HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
+                HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
+                TRY(halo2_multi(c, c->comm_stream, flds, fcs, 2));
+                HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
                 if (split) pass1(tb_lo, tb_hi - tb_lo + 1);
-                if (!c->hosted) HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+                HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
                 if (split) {
                     pass1(0, tb_lo);
                     pass1(tb_hi + 1, fc.TBk - tb_hi - 1);

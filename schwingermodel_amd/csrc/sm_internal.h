@@ -60,7 +60,7 @@ LaunchCfg dslash_config(const Geometry &g);
 void launch_dslash(hipStream_t s, const Geometry &g, const LaunchCfg &c, int dagger,
                    const double2 *in, double2 *out, const double2 *U, const double2 *loU,
                    const TFaces &f, double mass, const double2 *aux, double2 *partials,
-                   const CGScalars *skip_if_done);
+                   const CGScalars *skip_if_done, int tb0 = 0, int tbn = -1);
 int dslash_blocks(const Geometry &g, const LaunchCfg &c);
 
 void launch_force(hipStream_t s, const Geometry &g, const double2 *U, const double2 *l,

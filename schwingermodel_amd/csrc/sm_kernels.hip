@@ -30,6 +30,7 @@ struct DArgs {
     long V;
     int Nx, Wt, t0, Ntg, xchunk;
     int TB, XB, xcd_remap;   // tile grid (t-blocks x x-chunks), 1-D launch
+    int tb0, tbn, part0;     // this launch covers t-blocks [tb0, tb0+tbn); partials at part0+block
     double mass;
 };
 
@@ -37,14 +38,14 @@ struct DArgs {
 // dispatcher deals to one XCD (L, L+8, L+16, ...: round-robin, speed only,
 // MI355X_MICROARCH.md) get a contiguous range of tiles, so the x-halo rows and
 // t-edge lines shared by neighbouring tiles are L2 hits on that XCD.
-__device__ __forceinline__ void block_tile(int L, int TB, int XB, int remap, int &tb, int &xc) {
+__device__ __forceinline__ void block_tile(int L, int tb0, int tbn, int XB, int remap, int &tb, int &xc) {
     int w = L;
     if (remap) {
-        const int n = TB * XB, q = n >> 3, r = n & 7, xcd = L & 7;
+        const int n = tbn * XB, q = n >> 3, r = n & 7, xcd = L & 7;
         w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
     }
-    tb = w % TB;
-    xc = w / TB;
+    tb = tb0 + w % tbn;
+    xc = w / tbn;
 }
 
 // Row loads for column t of row x: centre psi, t-neighbours psi(t-1), psi(t+1),
@@ -104,7 +105,7 @@ __device__ __forceinline__ void dslash_body(const DArgs &a) {
     __shared__ double2 sh[4];
     if (a.sc && a.sc->done) return;  // grid-uniform early exit after CG convergence
     int tb, xc;
-    block_tile(blockIdx.x, a.TB, a.XB, a.xcd_remap, tb, xc);
+    block_tile(blockIdx.x, a.tb0, a.tbn, a.XB, a.xcd_remap, tb, xc);
     const int t = tb * blockDim.x + threadIdx.x;
     const int xbeg = xc * a.xchunk;
     const int xend = min(a.Nx, xbeg + a.xchunk);
@@ -189,7 +190,7 @@ __device__ __forceinline__ void dslash_body(const DArgs &a) {
     }
     if (EPI == EPI_DOT) {
         double2 bs = block_sum(acc, sh);
-        if (threadIdx.x == 0) a.partials[blockIdx.x] = bs;
+        if (threadIdx.x == 0) a.partials[a.part0 + blockIdx.x] = bs;
     }
 }
 
@@ -231,7 +232,7 @@ int dslash_blocks(const Geometry &g, const LaunchCfg &c) {
 void launch_dslash(hipStream_t s, const Geometry &g, const LaunchCfg &c, int dagger,
                    const double2 *in, double2 *out, const double2 *U, const double2 *loU,
                    const TFaces &f, double mass, const double2 *aux, double2 *partials,
-                   const CGScalars *skip_if_done) {
+                   const CGScalars *skip_if_done, int tb0, int tbn) {
     DArgs a;
     a.in = in;
     a.out = out;
@@ -251,7 +252,15 @@ void launch_dslash(hipStream_t s, const Geometry &g, const LaunchCfg &c, int dag
     a.XB = (g.Nx + c.xchunk - 1) / c.xchunk;
     a.xcd_remap = c.xcd_remap;
     a.mass = mass;
-    dim3 grid(a.TB * a.XB);
+    if (tbn < 0) {
+        tb0 = 0;
+        tbn = a.TB;
+    }
+    if (tbn == 0) return;
+    a.tb0 = tb0;
+    a.tbn = tbn;
+    a.part0 = tb0 * a.XB;
+    dim3 grid(tbn * a.XB);
     dim3 block(c.bt);
     const bool dot = aux != nullptr;
 #define SM_LAUNCH(K)                                                                    \

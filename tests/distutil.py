@@ -14,13 +14,13 @@ def free_port():
         return s.getsockname()[1]
 
 
-def run_world(mode, fixture, world, tmp_path, timeout=300):
+def run_world(mode, fixture, world, tmp_path, timeout=300, extra_env=None):
     port = free_port()
     result = os.path.join(str(tmp_path), f"{mode}_{fixture}_{world}.json")
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="1")
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="1", **(extra_env or {}))
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"), mode, fixture, result],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = []

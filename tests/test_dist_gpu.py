@@ -20,7 +20,10 @@ pytestmark = pytest.mark.gpu
                                            # reference = one shard on the same GPU
                                            ("gen:48x1024:0.3:-0.05", 2), ("gen:32x960:0.4242:0.0", 4)])
 def test_sharded_gpu_path_matches_reference(tmp_path, fixture, world):
-    rep = run_world("gpu", fixture, world, tmp_path, timeout=600)
+    # bt = 64 so the Dirac apply of the larger shards also splits into interior
+    # and edge t-blocks (the overlapped halo path)
+    env = {"SM_BT": "64"} if fixture.startswith("gen:") else None
+    rep = run_world("gpu", fixture, world, tmp_path, timeout=600, extra_env=env)
     c = rep["checks"]
     for k in ("ref_Dpsi", "ref_Ddagchi", "ref_DDdagpsi", "ref_force"):
         assert c[k] is True, (k, c)
