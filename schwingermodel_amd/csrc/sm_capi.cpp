@@ -86,6 +86,7 @@ struct sm_ctx {
     double2 *sums = nullptr;       // 4 complex scratch (allreduce)
     double *Fbuf = nullptr;        // 2V doubles (force)
     CGScalars *sc = nullptr;       // device
+    unsigned *counters = nullptr;  // device: last-block tickets (fused pass 1, pass 2)
     CGScalars *h_sc = nullptr;     // pinned host mirror
     double2 *h_sums = nullptr;     // pinned host
     int nparts_dslash = 0, nparts_red = 0;
@@ -439,11 +440,13 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     chk(hipMalloc(&c->sums, sizeof(double2) * 4));
     chk(hipMalloc(&c->Fbuf, sizeof(double) * 2 * (size_t)c->g.V));
     chk(hipMalloc(&c->sc, sizeof(CGScalars)));
+    chk(hipMalloc(&c->counters, 256));  // two tickets on separate 128-B lines: [0], [32]
     chk(hipHostMalloc(&c->h_sc, sizeof(CGScalars)));
     chk(hipHostMalloc(&c->h_sums, sizeof(double2) * 4));
     chk(hipHostMalloc(&c->h_face, sizeof(double) * 4 * kMaxFaceDoubles * (size_t)Nx));
     chk(hipHostMalloc(&c->h_red, sizeof(double) * 8));
     if (e == hipSuccess) chk(hipMemset(c->sc, 0, sizeof(CGScalars)));
+    if (e == hipSuccess) chk(hipMemset(c->counters, 0, 256));
     if (e != hipSuccess) {
         sm_destroy(c);
         return fail(SM_ERR_HIP, "allocation failed: %s", hipGetErrorString(e));
@@ -481,7 +484,8 @@ int sm_destroy(sm_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
-    void *dev[] = {c->U, c->ghostU, c->fields, c->faces, c->faces2, c->partials, c->sums, c->Fbuf, c->sc};
+    void *dev[] = {c->U, c->ghostU, c->fields, c->faces, c->faces2, c->partials, c->sums, c->Fbuf, c->sc,
+                   c->counters};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_sc) (void)hipHostFree(c->h_sc);
@@ -663,12 +667,14 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
             double2 *dold = c->field((c->cg_issued & 1) ? F_D2 : F_D);
             double2 *dnew = c->field((c->cg_issued & 1) ? F_D : F_D2);
             const CGFusedCfg &fc = c->fcfg;
+            const bool one = c->nshard == 1;  // one shard: scalars reduced in-kernel (last block)
             auto pass1 = [&](int tb0, int tbn) {
                 launch_cg_fused(c->stream, c->g, fc, c->nshard, dold, dnew, r, x, Ad, c->U,
                                 face2_recv(c, 0), face2_recv(c, 1), face2_recv(c, 2), c->cg_mass,
-                                c->cg_issued == 0, c->sc, c->partials, tb0, tbn);
+                                c->cg_issued == 0, c->sc, c->partials, tb0, tbn,
+                                one ? c->counters : nullptr);
             };
-            if (c->nshard == 1) {
+            if (one) {
                 pass1(0, fc.TBk);
             } else {
                 // Only the first and last t-blocks read the faces: exchange them
@@ -705,10 +711,10 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
                     pass1(0, fc.TBk);
                 }
             }
-            TRY(cg_scalar(c, cg_fused_blocks(c->fcfg), 0));
+            if (!one) TRY(cg_scalar(c, cg_fused_blocks(c->fcfg), 0));
             // pass 2: r -= alpha Ad, <r, r>; stop test and beta
-            launch_cg_update_r(c->stream, n, r, Ad, c->sc, c->partials);
-            TRY(cg_scalar(c, c->nparts_red, 1));
+            launch_cg_update_r(c->stream, n, r, Ad, c->sc, c->partials, one ? c->counters + 32 : nullptr);
+            if (!one) TRY(cg_scalar(c, c->nparts_red, 1));
             c->cg_pending_x = 1;
         } else {
             double2 *d = c->field(F_D);

@@ -43,6 +43,8 @@ struct CGFArgs {
     int Nx, Wt, t0, Ntg, nshard;
     int xchunk, NWT, TBk, XB, remap, first;
     int tb0, tbn, part0;  // launch covers t-blocks [tb0, tb0+tbn); partials at part0 + blockIdx
+    unsigned *counter;    // finalize: last block sums the partials and computes alpha
+    int finalize;
     double mass;
 };
 
@@ -217,6 +219,13 @@ __global__ void __launch_bounds__(256) cg_fused_kernel(CGFArgs a) {
     }
     const double2 bs = block_sum(acc, sh);
     if (threadIdx.x == 0) a.partials[a.part0 + blockIdx.x] = bs;
+    if (a.finalize) {  // single launch over the whole shard: alpha in-kernel
+        __shared__ int last;
+        if (last_block_arrive(a.counter, gridDim.x, &last)) {
+            const double2 tot = sum_partials_block(gridDim.x, a.partials + a.part0, sh);
+            if (threadIdx.x == 0) cg_alpha_scalar(sc, tot);  // alpha = rn / <d, Ad>
+        }
+    }
 }
 
 CGFusedCfg cg_fused_config(const Geometry &g) {
@@ -240,7 +249,8 @@ int cg_fused_blocks(const CGFusedCfg &c) { return c.TBk * c.XB; }
 void launch_cg_fused(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard,
                      const double2 *dold, double2 *dnew, const double2 *r, double2 *x, double2 *Ad,
                      const double2 *U, const double2 *fd, const double2 *fr, const double2 *fU,
-                     double mass, int first, CGScalars *sc, double2 *partials, int tb0, int tbn) {
+                     double mass, int first, CGScalars *sc, double2 *partials, int tb0, int tbn,
+                     unsigned *counter) {
     if (tbn <= 0) return;
     CGFArgs a;
     a.dold = dold; a.dnew = dnew; a.r = r; a.x = x; a.Ad = Ad; a.U = U;
@@ -253,13 +263,15 @@ void launch_cg_fused(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int 
     a.tb0 = tb0;
     a.tbn = tbn;
     a.part0 = tb0 * c.XB;  // disjoint partial slots per t-block range
+    a.counter = counter;
+    a.finalize = counter != nullptr;
     hipLaunchKernelGGL(cg_fused_kernel, dim3(tbn * c.XB), dim3(256), 0, s, a);
 }
 
 // ---- pass 2: r -= alpha Ad ; partials <r, r>  (src/conjugate_gradient.cpp:39-43)
 constexpr int RB2 = 256;
 __global__ void __launch_bounds__(RB2) cg_update_r_kernel(long n, double2 *r, const double2 *Ad,
-                                                          const CGScalars *sc, double2 *part) {
+                                                          CGScalars *sc, double2 *part, unsigned *counter) {
     __shared__ double2 sh[RB2 / 64];
     if (sc->done) return;
     const double2 alpha = sc->alpha;
@@ -280,11 +292,19 @@ __global__ void __launch_bounds__(RB2) cg_update_r_kernel(long n, double2 *r, co
     for (; i < ch.end; i += RB2) f(i);
     const double2 s = block_sum(acc, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = s;
+    if (counter) {  // last block: err, stop test, beta (src/conjugate_gradient.cpp:43-61)
+        __shared__ int last;
+        if (last_block_arrive(counter, gridDim.x, &last)) {
+            const double2 tot = sum_partials_block(gridDim.x, part, sh);
+            if (threadIdx.x == 0) cg_beta_scalar(sc, tot);
+        }
+    }
 }
 
-void launch_cg_update_r(hipStream_t s, long n, double2 *r, const double2 *Ad, const CGScalars *sc,
-                        double2 *part) {
-    hipLaunchKernelGGL(cg_update_r_kernel, dim3(reduce_blocks(n)), dim3(RB2), 0, s, n, r, Ad, sc, part);
+void launch_cg_update_r(hipStream_t s, long n, double2 *r, const double2 *Ad, CGScalars *sc,
+                        double2 *part, unsigned *counter) {
+    hipLaunchKernelGGL(cg_update_r_kernel, dim3(reduce_blocks(n)), dim3(RB2), 0, s, n, r, Ad, sc, part,
+                       counter);
 }
 
 // ---- the deferred x update of the last executed iteration --------------------

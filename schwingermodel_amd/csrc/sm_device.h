@@ -4,6 +4,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "sm_internal.h"
+
 #pragma clang fp contract(off)
 
 namespace sm {
@@ -134,6 +136,57 @@ __device__ __forceinline__ Chunk block_chunk(long n) {
     c.beg = (long)blockIdx.x * per;
     c.end = c.beg + per < n ? c.beg + per : n;
     return c;
+}
+
+// Fixed-order sum of per-block partials by one block (deterministic).
+__device__ __forceinline__ double2 sum_partials_block(int nparts, const double2 *part, double2 *sh) {
+    double2 acc = make_double2(0.0, 0.0);
+    for (int i = threadIdx.x; i < nparts; i += blockDim.x) acc = cadd(acc, part[i]);
+    return block_sum(acc, sh);
+}
+
+// alpha = r_norm2 / <d, Ad>   (complex division, src/conjugate_gradient.cpp:33)
+__device__ __forceinline__ void cg_alpha_scalar(CGScalars *sc, double2 dAd) {
+    sc->alpha = cdiv(sc->rn.x, sc->rn.y, dAd.x, dAd.y);
+}
+
+// err = sqrt(Re<r,r>); stop test; beta = err^2 / r_norm2   (src/conjugate_gradient.cpp:43-61)
+__device__ __forceinline__ void cg_beta_scalar(CGScalars *sc, double2 rr) {
+    const double err_sqr = rr.x;
+    const double err = sqrt(err_sqr);
+    sc->err = err;
+    sc->k = sc->k + 1;
+    if (err < sc->tol * sc->phi_norm) {
+        sc->done = 1;
+        sc->converged = 1;
+        return;
+    }
+    sc->beta = cdiv(err_sqr, 0.0, sc->rn.x, sc->rn.y);
+    sc->rn = make_double2(err_sqr, 0.0);
+}
+
+// In-launch "last block reduces" hand-off (cdna_hip_programming.md §6
+// Guideline 16, split-K recipe): every block has stored its partial; the block
+// whose agent-scope ticket is nblocks-1 returns true (in all its threads) and
+// may then read every block's partial with plain loads. It also re-arms the
+// counter for the next launch (zeroed once at context creation).
+__device__ __forceinline__ bool last_block_arrive(unsigned *counter, unsigned nblocks, int *sh_flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its stores issued and done
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = t == nblocks - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        *sh_flag = last;
+    }
+    __syncthreads();
+    return *sh_flag != 0;
 }
 
 }  // namespace sm

@@ -100,9 +100,10 @@ int cg_fused_blocks(const CGFusedCfg &c);
 void launch_cg_fused(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard,
                      const double2 *dold, double2 *dnew, const double2 *r, double2 *x, double2 *Ad,
                      const double2 *U, const double2 *fd, const double2 *fr, const double2 *fU,
-                     double mass, int first, CGScalars *sc, double2 *partials, int tb0, int tbn);
-void launch_cg_update_r(hipStream_t s, long n, double2 *r, const double2 *Ad, const CGScalars *sc,
-                        double2 *part);
+                     double mass, int first, CGScalars *sc, double2 *partials, int tb0, int tbn,
+                     unsigned *counter);  // counter != null: last block computes alpha
+void launch_cg_update_r(hipStream_t s, long n, double2 *r, const double2 *Ad, CGScalars *sc,
+                        double2 *part, unsigned *counter);  // counter != null: last block: beta
 void launch_cg_finish_x(hipStream_t s, long n, double2 *x, const double2 *d0, const double2 *d1,
                         const CGScalars *sc);
 void launch_pack_faces2(hipStream_t s, const Geometry &g, const double2 *field, double2 *lo,

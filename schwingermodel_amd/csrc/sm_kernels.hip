@@ -367,12 +367,6 @@ __global__ void __launch_bounds__(RB) dot_partial_kernel(long n, const double2 *
     if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
-__device__ __forceinline__ double2 sum_partials_block(int nparts, const double2 *part, double2 *sh) {
-    double2 acc = make_double2(0.0, 0.0);
-    for (int i = threadIdx.x; i < nparts; i += RB) acc = cadd(acc, part[i]);
-    return block_sum(acc, sh);
-}
-
 __global__ void __launch_bounds__(RB) sum_partials_kernel(int nparts, const double2 *part, double2 *out) {
     __shared__ double2 sh[RB / 64];
     double2 s = sum_partials_block(nparts, part, sh);
@@ -449,11 +443,6 @@ void launch_cg_finalize_init(hipStream_t s, int nparts, const double2 *part_rr,
     hipLaunchKernelGGL(cg_finalize_init_kernel, dim3(1), dim3(RB), 0, s, nparts, part_rr, part_pp, sc, tol);
 }
 
-// alpha = r_norm2 / <d, Ad>   (complex division, src/conjugate_gradient.cpp:33)
-__device__ __forceinline__ void cg_alpha_scalar(CGScalars *sc, double2 dAd) {
-    sc->alpha = cdiv(sc->rn.x, sc->rn.y, dAd.x, dAd.y);
-}
-
 __global__ void __launch_bounds__(RB) cg_alpha_kernel(int nparts, const double2 *part, CGScalars *sc) {
     __shared__ double2 sh[RB / 64];
     if (sc->done) return;
@@ -486,21 +475,6 @@ __global__ void __launch_bounds__(RB) cg_update_xr_kernel(long n, double2 *x, do
 void launch_cg_update_xr(hipStream_t s, long n, double2 *x, double2 *r, const double2 *d,
                          const double2 *Ad, CGScalars *sc, double2 *part) {
     hipLaunchKernelGGL(cg_update_xr_kernel, dim3(reduce_blocks(n)), dim3(RB), 0, s, n, x, r, d, Ad, sc, part);
-}
-
-// err = sqrt(Re<r,r>); stop test; beta = err^2 / r_norm2   (src/conjugate_gradient.cpp:43-61)
-__device__ __forceinline__ void cg_beta_scalar(CGScalars *sc, double2 rr) {
-    const double err_sqr = rr.x;
-    const double err = sqrt(err_sqr);
-    sc->err = err;
-    sc->k = sc->k + 1;
-    if (err < sc->tol * sc->phi_norm) {
-        sc->done = 1;
-        sc->converged = 1;
-        return;
-    }
-    sc->beta = cdiv(err_sqr, 0.0, sc->rn.x, sc->rn.y);
-    sc->rn = make_double2(err_sqr, 0.0);
 }
 
 __global__ void __launch_bounds__(RB) cg_beta_kernel(int nparts, const double2 *part, CGScalars *sc) {
