@@ -114,8 +114,11 @@ int sm_synchronize(sm_ctx *ctx);
  * variant selects the stencil code variant. Values <= 0 (< 0 for xcd_remap
  * and variant) keep the current setting. */
 int sm_tune(sm_ctx *ctx, int bt, int xchunk, int xcd_remap, int variant);
-/* CG path: fused = 1 runs an iteration in two HBM passes (sm_cgfused.hip),
- * 0 the six-kernel sequence; xchunk = rows per block of the fused kernel. */
+/* CG path: fused = 1 runs an iteration in two HBM passes (sm_cgfused.hip)
+ * each followed by a one-block scalar kernel (alpha, beta; the default),
+ * 2 the same two passes with alpha and beta reduced in-kernel by the last
+ * block of each pass (one shard only), 0 the six-kernel
+ * sequence; xchunk = rows per block of the fused kernel. < 0 / <= 0 keep. */
 int sm_tune_cg(sm_ctx *ctx, int fused, int xchunk);
 /* Streaming-bandwidth ceiling on the ctx stream (measured roofline reference):
  * out = a + b (two_reads = 1: the stencil's 2-read/1-write byte mix) or

@@ -68,6 +68,10 @@ struct sm_ctx {
     LaunchCfg cfg{};
     CGFusedCfg fcfg{};
     int cg_fused = 1;               // 1: two-pass fused CG iteration (sm_cgfused.hip)
+    // one shard: alpha/beta by the last block of each pass instead of two
+    // one-block kernels. Measured equal at 4096^2 and 19 % slower at 1024^2
+    // (every block of a one-wave grid hits the ticket at once), so off by default.
+    int cg_inkernel = 0;
     hipStream_t own_stream = nullptr, stream = nullptr;
     hipStream_t comm_stream = nullptr;  // halo exchange overlapped with interior compute
     hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
@@ -503,7 +507,11 @@ int sm_destroy(sm_ctx *c) {
 
 int sm_tune_cg(sm_ctx *c, int fused, int xchunk) {
     if (!c) return fail(SM_ERR_ARG, "null context");
-    if (fused >= 0) c->cg_fused = fused;
+    if (fused > 2) return fail(SM_ERR_ARG, "fused must be 0, 1 or 2");
+    if (fused >= 0) {
+        c->cg_fused = fused != 0;
+        c->cg_inkernel = fused == 2;
+    }
     if (xchunk > 0) {
         CGFusedCfg f = c->fcfg;
         f.xchunk = xchunk;
@@ -667,14 +675,14 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
             double2 *dold = c->field((c->cg_issued & 1) ? F_D2 : F_D);
             double2 *dnew = c->field((c->cg_issued & 1) ? F_D : F_D2);
             const CGFusedCfg &fc = c->fcfg;
-            const bool one = c->nshard == 1;  // one shard: scalars reduced in-kernel (last block)
+            const bool one = c->nshard == 1 && c->cg_inkernel;  // scalars reduced in-kernel (last block)
             auto pass1 = [&](int tb0, int tbn) {
                 launch_cg_fused(c->stream, c->g, fc, c->nshard, dold, dnew, r, x, Ad, c->U,
                                 face2_recv(c, 0), face2_recv(c, 1), face2_recv(c, 2), c->cg_mass,
                                 c->cg_issued == 0, c->sc, c->partials, tb0, tbn,
                                 one ? c->counters : nullptr);
             };
-            if (one) {
+            if (c->nshard == 1) {
                 pass1(0, fc.TBk);
             } else {
                 // Only the first and last t-blocks read the faces: exchange them

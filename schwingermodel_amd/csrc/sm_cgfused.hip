@@ -218,11 +218,13 @@ __global__ void __launch_bounds__(256) cg_fused_kernel(CGFArgs a) {
         }
     }
     const double2 bs = block_sum(acc, sh);
-    if (threadIdx.x == 0) a.partials[a.part0 + blockIdx.x] = bs;
-    if (a.finalize) {  // single launch over the whole shard: alpha in-kernel
+    if (!a.finalize) {
+        if (threadIdx.x == 0) a.partials[a.part0 + blockIdx.x] = bs;
+    } else {  // single launch over the whole shard: alpha in-kernel
+        if (threadIdx.x == 0) publish_partial(a.partials + blockIdx.x, bs);
         __shared__ int last;
         if (last_block_arrive(a.counter, gridDim.x, &last)) {
-            const double2 tot = sum_partials_block(gridDim.x, a.partials + a.part0, sh);
+            const double2 tot = sum_published_block(gridDim.x, a.partials, sh);
             if (threadIdx.x == 0) cg_alpha_scalar(sc, tot);  // alpha = rn / <d, Ad>
         }
     }
@@ -291,11 +293,13 @@ __global__ void __launch_bounds__(RB2) cg_update_r_kernel(long n, double2 *r, co
     }
     for (; i < ch.end; i += RB2) f(i);
     const double2 s = block_sum(acc, sh);
-    if (threadIdx.x == 0) part[blockIdx.x] = s;
-    if (counter) {  // last block: err, stop test, beta (src/conjugate_gradient.cpp:43-61)
+    if (!counter) {
+        if (threadIdx.x == 0) part[blockIdx.x] = s;
+    } else {  // last block: err, stop test, beta (src/conjugate_gradient.cpp:43-61)
+        if (threadIdx.x == 0) publish_partial(part + blockIdx.x, s);
         __shared__ int last;
         if (last_block_arrive(counter, gridDim.x, &last)) {
-            const double2 tot = sum_partials_block(gridDim.x, part, sh);
+            const double2 tot = sum_published_block(gridDim.x, part, sh);
             if (threadIdx.x == 0) cg_beta_scalar(sc, tot);
         }
     }

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--sixkernel", action="store_true")
+    ap.add_argument("--paths", default="fused", help="comma list of fused (scalar kernels), fused2 (in-kernel scalars)")
     a = ap.parse_args()
     import torch
     import schwingermodel_amd as sm
@@ -39,14 +40,14 @@ def main():
     dU, dp = U.cuda(), p.cuda()
     x = torch.empty_like(dp)
     sm.check(sm.lib.sm_upload_gauge_dev(L.ctx, vp(dU.data_ptr())))
-    configs = [("fused", int(c)) for c in a.xchunk.split(",")]
+    configs = [(p, int(c)) for p in a.paths.split(",") for c in a.xchunk.split(",")]
     if a.sixkernel:
         configs.append(("sixkernel", 0))
     res = {c: [] for c in configs}
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(a.rounds):
         for c in configs:
-            sm.check(sm.lib.sm_tune_cg(L.ctx, 1 if c[0] == "fused" else 0, c[1]))
+            sm.check(sm.lib.sm_tune_cg(L.ctx, {"fused": 1, "fused2": 2, "sixkernel": 0}[c[0]], c[1]))
             sm.check(sm.lib.sm_cg_begin(L.ctx, vp(dp.data_ptr()), vp(x.data_ptr()), -0.06, 0.0))
             sm.check(sm.lib.sm_cg_iterate(L.ctx, 3))
             e0.record(s)
