@@ -19,15 +19,33 @@
 //   bench <ranks_x> <ranks_t> <seed_U> <sigma> <seed_psi> <m0> <napply> <ncg>
 //       generates the synthetic fields per rank (sm_fields.h), times napply
 //       D_phi applies and ncg CG iterations (tol = 0), prints one JSON line.
-#include "conjugate_gradient.h"
-#include "mpi_setup.h"
-#include "sm_fields.h"
-
+//   md <dir> <ranks_x> <ranks_t> <m0> <beta> <tau> <md_steps> <tol> <max_iter>
+//       reads U.bin, chi.bin and P.bin (momenta: two real planes) and runs the
+//       reference's gauge / molecular-dynamics code on them: plaquette field,
+//       Sp, gauge action, staples, Force_G alone, Force (fermion + gauge) at
+//       U, Hamiltonian(U, P, phi = D chi), Leapfrog(phi) -> (U', P') and
+//       Hamiltonian(U', P', phi). HMC's members are private, so hmc.h is
+//       included with `private` mapped to `public` (this TU only; the class
+//       layout is unchanged).
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
+#include <iomanip>
+#include <iostream>
+#include <random>
+#include <sstream>
 #include <string>
 #include <vector>
+
+#include "conjugate_gradient.h"
+#include "gauge_conf.h"
+#include "mpi_setup.h"
+#include "sm_fields.h"
+#define private public
+#include "hmc.h"
+#undef private
 
 static long g_ddag_calls = 0;
 extern "C" void __real__Z14D_D_dagger_phiRK6spinorS1_RS_RKd(const spinor &, const spinor &,
@@ -52,6 +70,24 @@ static void setup(int rx, int rt) {
 
 static int x_begin() { return mpi::coords[0] * mpi::width_x; }
 static int t_begin() { return mpi::coords[1] * mpi::width_t; }
+
+// Read this rank's block of a global two-plane real field (re_field).
+static bool read_block_real(const std::string &path, re_field &s) {
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) return false;
+    std::vector<double> g((size_t)2 * LV::Ntot);
+    size_t got = fread(g.data(), sizeof(double), g.size(), f);
+    fclose(f);
+    if (got != g.size()) return false;
+    for (int x = 0; x < mpi::width_x; x++)
+        for (int t = 0; t < mpi::width_t; t++) {
+            long ng = (long)(x_begin() + x) * LV::Nt + t_begin() + t;
+            int n = x * mpi::width_t + t;
+            s.mu0[n] = g[ng];
+            s.mu1[n] = g[LV::Ntot + ng];
+        }
+    return true;
+}
 
 // Read this rank's block of a global two-plane complex field.
 static bool read_block(const std::string &path, spinor &s) {
@@ -153,6 +189,54 @@ static int run_fixture(const std::string &dir, double m0, double tol, int max_it
     return 0;
 }
 
+static int run_md(const std::string &dir, double m0, double beta, double tau, int md_steps,
+                  double tol, int max_iter) {
+    GaugeConf G;
+    spinor chi(mpi::maxSize);
+    re_field P(mpi::maxSize);
+    if (!(read_block(dir + "/U.bin", G.Conf) && read_block(dir + "/chi.bin", chi) &&
+          read_block_real(dir + "/P.bin", P))) {
+        if (mpi::rank == 0) fprintf(stderr, "cannot read md inputs in %s\n", dir.c_str());
+        return 1;
+    }
+    CG::tol = tol;
+    CG::max_iter = max_iter;
+    G.Compute_Plaquette01();
+    const double sp = G.MeasureSp_HMC(), gS = G.Compute_gaugeAction(beta);
+    write_global(dir + "/ref_plaq.bin", reinterpret_cast<const double *>(G.Plaquette01),
+                 reinterpret_cast<const double *>(G.Plaquette01), 2);
+    G.Compute_Staple();
+    write_spinor(dir + "/ref_staple.bin", G.Staples);
+    HMC h(G, md_steps, tau, 0, 1, 0, beta, LV::Nx, LV::Nt, m0, 0);
+    h.PConf = P;
+    spinor phi(mpi::maxSize);
+    D_phi(G.Conf, chi, phi, m0);
+    write_spinor(dir + "/ref_phi.bin", phi);
+    // gauge force alone (Forces zeroed first)
+    for (int n = 0; n < mpi::maxSize; n++) h.Forces.mu0[n] = h.Forces.mu1[n] = 0.0;
+    h.Force_G(h.GConf);
+    write_global(dir + "/ref_gforce.bin", h.Forces.mu0, h.Forces.mu1, 1);
+    long c0 = g_ddag_calls;
+    h.Force(h.GConf, phi);
+    long force_iters = g_ddag_calls - c0 - 1;
+    write_global(dir + "/ref_mdforce.bin", h.Forces.mu0, h.Forces.mu1, 1);
+    const double H0 = h.Hamiltonian(h.GConf, h.PConf, phi);
+    c0 = g_ddag_calls;
+    h.Leapfrog(phi);
+    long lf_calls = g_ddag_calls - c0;
+    write_spinor(dir + "/ref_U1.bin", h.GConf_copy.Conf);
+    write_global(dir + "/ref_P1.bin", h.PConf_copy.mu0, h.PConf_copy.mu1, 1);
+    const double H1 = h.Hamiltonian(h.GConf_copy, h.PConf_copy, phi);
+    if (mpi::rank == 0)
+        printf("{\"Nx\": %d, \"Nt\": %d, \"ranks_x\": %d, \"ranks_t\": %d, \"m0\": %.17g, "
+               "\"beta\": %.17g, \"tau\": %.17g, \"md_steps\": %d, \"sp\": %.17g, "
+               "\"gauge_action\": %.17g, \"force_cg_iters\": %ld, \"leapfrog_ddag_calls\": %ld, "
+               "\"H0\": %.17g, \"H1\": %.17g, \"dH\": %.17g, \"cg_convergence\": %d}\n",
+               LV::Nx, LV::Nt, mpi::ranks_x, mpi::ranks_t, m0, beta, tau, md_steps, sp, gS,
+               force_iters, lf_calls, H0, H1, H1 - H0, h.CG_convergence);
+    return 0;
+}
+
 static int run_bench(unsigned long long seedU, double sigma, unsigned long long seedP, double m0,
                      int napply, int ncg) {
     spinor U(mpi::maxSize), psi(mpi::maxSize), out(mpi::maxSize), x(mpi::maxSize);
@@ -226,12 +310,16 @@ int main(int argc, char **argv) {
     } else if (argc >= 8 && !strcmp(argv[1], "fixture")) {
         setup(atoi(argv[3]), atoi(argv[4]));
         rc = run_fixture(argv[2], atof(argv[5]), atof(argv[6]), atoi(argv[7]));
+    } else if (argc >= 11 && !strcmp(argv[1], "md")) {
+        setup(atoi(argv[3]), atoi(argv[4]));
+        rc = run_md(argv[2], atof(argv[5]), atof(argv[6]), atof(argv[7]), atoi(argv[8]), atof(argv[9]),
+                    atoi(argv[10]));
     } else if (argc >= 10 && !strcmp(argv[1], "bench")) {
         setup(atoi(argv[2]), atoi(argv[3]));
         rc = run_bench(strtoull(argv[4], 0, 10), atof(argv[5]), strtoull(argv[6], 0, 10),
                        atof(argv[7]), atoi(argv[8]), atoi(argv[9]));
     } else {
-        fprintf(stderr, "usage: gen <dir> seedU sigma seedP seedC | fixture <dir> rx rt m0 tol max_iter | bench rx rt seedU sigma seedP m0 napply ncg\n");
+        fprintf(stderr, "usage: gen <dir> seedU sigma seedP seedC | fixture <dir> rx rt m0 tol max_iter | bench rx rt seedU sigma seedP m0 napply ncg | md <dir> rx rt m0 beta tau md_steps tol max_iter\n");
     }
     MPI_Finalize();
     return rc;

@@ -276,3 +276,154 @@ int oracle_cg(int Nx, int Nt, const double *U0, const double *U1,
     *err_out = err;
     return conv;
 }
+
+/* ===================== gauge field / molecular dynamics =====================
+ * the rest of the MD force step and the HMC
+ * Hamiltonian, restated from src/gauge_conf.cpp and src/hmc.cpp in the
+ * reference's evaluation order (single domain; the reference's MPI variants
+ * compute the same expressions with halo values, bitwise equal). */
+#include <complex.h>
+#include <float.h>
+
+/* U_01(n) = U_0(n) U_1(n+0) U*_0(n+1) U*_1(n), src/gauge_conf.cpp:45-49. */
+static cplx plaq_site(int Nx, int Nt, const double *U0, const double *U1, int x, int t) {
+    const long n = (long)x * Nt + t;
+    const long nt = (long)x * Nt + (t + 1) % Nt;     /* RightPB[2n]   */
+    const long nx = (long)((x + 1) % Nx) * Nt + t;   /* RightPB[2n+1] */
+    return cmul(cmul(cmul(ld(U0, n), ld(U1, nt)), cconj(ld(U0, nx))), cconj(ld(U1, n)));
+}
+
+void oracle_plaquette(int Nx, int Nt, const double *U0, const double *U1, double *P) {
+    for (int x = 0; x < Nx; x++)
+        for (int t = 0; t < Nt; t++) st(P, (long)x * Nt + t, plaq_site(Nx, Nt, U0, U1, x, t));
+}
+
+void oracle_plaquette_sums(int Nx, int Nt, const double *U0, const double *U1, double beta,
+                           double *sp, double *action) {
+    /* MeasureSp_HMC (src/gauge_conf.cpp:430-440) and Compute_gaugeAction
+     * (:444-453): sequential sums over n. */
+    double s = 0.0, a = 0.0;
+    for (int x = 0; x < Nx; x++)
+        for (int t = 0; t < Nt; t++) {
+            const cplx p = plaq_site(Nx, Nt, U0, U1, x, t);
+            s += p.re;
+            a += beta * (1.0 - p.re);   /* beta * real(1.0 - P) */
+        }
+    *sp = s;
+    *action = a;
+}
+
+void oracle_staples(int Nx, int Nt, const double *U0, const double *U1, double *S0, double *S1) {
+    /* Compute_Staple, src/gauge_conf.cpp:95-125 (size == 1 branch). */
+    for (int x = 0; x < Nx; x++)
+        for (int t = 0; t < Nt; t++) {
+            const long n = (long)x * Nt + t;
+            const int xp = (x + 1) % Nx, xm = (x - 1 + Nx) % Nx;
+            const int tp = (t + 1) % Nt, tm = (t - 1 + Nt) % Nt;
+            const long x1 = (long)xp * Nt + t, x_1 = (long)xm * Nt + t;
+            const long t1 = (long)x * Nt + tp, t_1 = (long)x * Nt + tm;
+            const long x_1_t1 = (long)xm * Nt + tp, x1_t_1 = (long)xp * Nt + tm;
+            /* mu = 0: U_1(n) U_0(n+1) U*_1(n+0) + U*_1(n-1) U_0(n-1) U_1(n-1+0) */
+            st(S0, n, cadd(cmul(cmul(ld(U1, n), ld(U0, x1)), cconj(ld(U1, t1))),
+                           cmul(cmul(cconj(ld(U1, x_1)), ld(U0, x_1)), ld(U1, x_1_t1))));
+            /* mu = 1: U_0(n) U_1(n+0) U*_0(n+1) + U*_0(n-0) U_1(n-0) U_0(n+1-0) */
+            st(S1, n, cadd(cmul(cmul(ld(U0, n), ld(U1, t1)), cconj(ld(U0, x1))),
+                           cmul(cmul(cconj(ld(U0, t_1)), ld(U1, t_1)), ld(U0, x1_t_1))));
+        }
+}
+
+void oracle_gauge_force(int Nx, int Nt, const double *U0, const double *U1, double beta,
+                        double *F0, double *F1) {
+    /* HMC::Force_G, src/hmc.cpp:31-40: F += -beta Im(U conj(staple)). */
+    const long S = (long)Nx * Nt;
+    double *St = (double *)malloc(sizeof(double) * 4 * S);
+    oracle_staples(Nx, Nt, U0, U1, St, St + 2 * S);
+    for (long n = 0; n < S; n++) {
+        F0[n] += -beta * cmul(ld(U0, n), cconj(ld(St, n))).im;
+        F1[n] += -beta * cmul(ld(U1, n), cconj(ld(St + 2 * S, n))).im;
+    }
+    free(St);
+}
+
+int oracle_md_force(int Nx, int Nt, const double *U0, const double *U1, const double *phi0,
+                    const double *phi1, double m0, double beta, double tol, int max_iter,
+                    double *F0, double *F1, int *iters) {
+    /* HMC::Force, src/hmc.cpp:44-60: psi = (DD^dag)^-1 phi (x0 = phi),
+     * F = phi_dag_partialD_phi(U, psi, D^dag psi) + gauge force. The
+     * ill-conditioned-conf save on CG failure is not restated. */
+    const long S = (long)Nx * Nt;
+    double *buf = (double *)malloc(sizeof(double) * 8 * S);
+    double *ps0 = buf, *ps1 = buf + 2 * S, *T0 = buf + 4 * S, *T1 = buf + 6 * S;
+    double err;
+    const int conv = oracle_cg(Nx, Nt, U0, U1, phi0, phi1, ps0, ps1, m0, tol, max_iter, iters, &err);
+    oracle_dirac(Nx, Nt, U0, U1, ps0, ps1, T0, T1, m0, 1);
+    oracle_force(Nx, Nt, U0, U1, ps0, ps1, T0, T1, F0, F1);
+    oracle_gauge_force(Nx, Nt, U0, U1, beta, F0, F1);
+    free(buf);
+    return conv;
+}
+
+/* U *= exp(i coef P) with std::exp(complex) = glibc cexp of (+-0, coef*P):
+ * (cos y, sin y) for |y| > DBL_MIN, (1, y) below (s_cexp_template.c). */
+static void link_update(long S, double *U, const double *P, double coef) {
+    for (long n = 0; n < S; n++) {
+        const double complex w = cexp(CMPLX(0.0, coef * P[n]));
+        st(U, n, cmul(ld(U, n), C(creal(w), cimag(w))));
+    }
+}
+
+int oracle_leapfrog(int Nx, int Nt, double *U0, double *U1, double *P0, double *P1,
+                    const double *phi0, const double *phi1, double m0, double beta, double tau,
+                    int md_steps, double tol, int max_iter, long *cg_iters) {
+    /* HMC::Leapfrog, src/hmc.cpp:63-101, on the copies (U, P updated in place),
+     * including its loop bound: forces are evaluated md_steps - 1 times. */
+    const long S = (long)Nx * Nt;
+    const double eps = tau / (md_steps * 1.0);
+    double *F = (double *)malloc(sizeof(double) * 2 * S);
+    int ok = 1, it;
+    long total = 0;
+    link_update(S, U0, P0, 0.5 * eps);
+    link_update(S, U1, P1, 0.5 * eps);
+    ok &= oracle_md_force(Nx, Nt, U0, U1, phi0, phi1, m0, beta, tol, max_iter, F, F + S, &it);
+    total += it;
+    for (int step = 1; step < md_steps - 1; step++) {
+        for (long n = 0; n < S; n++) {
+            P0[n] += eps * F[n];
+            P1[n] += eps * F[S + n];
+        }
+        link_update(S, U0, P0, eps);
+        link_update(S, U1, P1, eps);
+        ok &= oracle_md_force(Nx, Nt, U0, U1, phi0, phi1, m0, beta, tol, max_iter, F, F + S, &it);
+        total += it;
+    }
+    for (long n = 0; n < S; n++) {
+        P0[n] += eps * F[n];
+        P1[n] += eps * F[S + n];
+    }
+    link_update(S, U0, P0, 0.5 * eps);
+    link_update(S, U1, P1, 0.5 * eps);
+    free(F);
+    *cg_iters = total;
+    return ok;
+}
+
+double oracle_hamiltonian(int Nx, int Nt, const double *U0, const double *U1, const double *P0,
+                          const double *P1, const double *phi0, const double *phi1, double m0,
+                          double beta, double tol, int max_iter, int *iters) {
+    /* HMC::Hamiltonian + HMC::Action, src/hmc.cpp:104-148:
+     * H = sum 0.5 Pi^2 + (beta sum Re(1 - U_01) + Re dot((DD^dag)^-1 phi, phi)). */
+    const long S = (long)Nx * Nt;
+    double K = 0.0;
+    for (long n = 0; n < S; n++) {
+        K += 0.5 * P0[n] * P0[n];
+        K += 0.5 * P1[n] * P1[n];
+    }
+    double sp, action, err, z[2];
+    oracle_plaquette_sums(Nx, Nt, U0, U1, beta, &sp, &action);
+    double *x = (double *)malloc(sizeof(double) * 4 * S);
+    oracle_cg(Nx, Nt, U0, U1, phi0, phi1, x, x + 2 * S, m0, tol, max_iter, iters, &err);
+    oracle_dot(S, x, x + 2 * S, phi0, phi1, z);
+    free(x);
+    action += z[0];
+    return K + action;
+}

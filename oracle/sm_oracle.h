@@ -14,6 +14,10 @@
  *   conjugate_gradient    src/conjugate_gradient.cpp:4-66
  *   dot                   include/variables.h:181-192
  *   periodic_boundary     include/dirac_operator.h:35-62 (signs / neighbours)
+ *   Compute_Plaquette01   src/gauge_conf.cpp:41-85; MeasureSp_HMC :430-440;
+ *   Compute_gaugeAction   :444-453; Compute_Staple :89-373
+ *   HMC::Force_G / Force  src/hmc.cpp:31-60; Leapfrog :63-101;
+ *   HMC::Action / Hamiltonian :104-148
  *
  * Parity is PINNED: tests/test_oracle_golden.py checks every function here
  * bit-for-bit against fixtures produced by the unmodified reference sources
@@ -77,6 +81,30 @@ int oracle_cg(int Nx, int Nt, const double *U0, const double *U1,
 void oracle_dirac_mt(int Nx, int Nt, const double *U0, const double *U1,
                      const double *in0, const double *in1, double *out0, double *out1,
                      double m0, int dagger, int nthreads);
+
+/* ---- gauge field and molecular dynamics (single domain) ---- */
+/* Per-site plaquette U_01(n); P is S complex (interleaved). */
+void oracle_plaquette(int Nx, int Nt, const double *U0, const double *U1, double *P);
+/* sp = sum Re U_01 (MeasureSp_HMC), action = sum beta Re(1 - U_01), sequential. */
+void oracle_plaquette_sums(int Nx, int Nt, const double *U0, const double *U1, double beta,
+                           double *sp, double *action);
+/* Staples of both directions (Compute_Staple), S0/S1 complex planes. */
+void oracle_staples(int Nx, int Nt, const double *U0, const double *U1, double *S0, double *S1);
+/* F += -beta Im(U conj(staple)) (HMC::Force_G). */
+void oracle_gauge_force(int Nx, int Nt, const double *U0, const double *U1, double beta,
+                        double *F0, double *F1);
+/* HMC::Force: CG solve, D^dag, fermion bilinear, gauge force. Returns CG convergence. */
+int oracle_md_force(int Nx, int Nt, const double *U0, const double *U1, const double *phi0,
+                    const double *phi1, double m0, double beta, double tol, int max_iter,
+                    double *F0, double *F1, int *iters);
+/* HMC::Leapfrog on (U, P) in place; returns 1 if every CG converged. */
+int oracle_leapfrog(int Nx, int Nt, double *U0, double *U1, double *P0, double *P1,
+                    const double *phi0, const double *phi1, double m0, double beta, double tau,
+                    int md_steps, double tol, int max_iter, long *cg_iters);
+/* HMC::Hamiltonian(U, P, phi). */
+double oracle_hamiltonian(int Nx, int Nt, const double *U0, const double *U1, const double *P0,
+                          const double *P1, const double *phi0, const double *phi1, double m0,
+                          double beta, double tol, int max_iter, int *iters);
 
 #ifdef __cplusplus
 }

@@ -3,7 +3,6 @@
 // Owns one t-shard of the lattice on one GPU: device-resident gauge field,
 // CG work fields, halo faces, reduction partials and the device CG scalars.
 // Kernels are in sm_kernels.hip; the multi-GPU transport is RCCL (xGMI).
-#include "../../include/sm_hip.h"
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -16,13 +15,17 @@
 #include <string>
 
 #include "sm_fields.h"
+#include "sm_ctx.h"
 #include "sm_internal.h"
 
 using namespace sm;
+using namespace sm_host;
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
+
+namespace sm_host {
 
 int fail(int code, const char *fmt, ...) {
     char buf[512];
@@ -33,79 +36,6 @@ int fail(int code, const char *fmt, ...) {
     g_err = buf;
     return code;
 }
-
-#define HIP_TRY(expr)                                                                   \
-    do {                                                                                \
-        hipError_t e_ = (expr);                                                         \
-        if (e_ != hipSuccess)                                                           \
-            return fail(SM_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
-                        __FILE__, __LINE__);                                            \
-    } while (0)
-
-#define NCCL_TRY(expr)                                                                     \
-    do {                                                                                   \
-        ncclResult_t r_ = (expr);                                                          \
-        if (r_ != ncclSuccess)                                                             \
-            return fail(SM_ERR_RCCL, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(r_), \
-                        __FILE__, __LINE__);                                               \
-    } while (0)
-
-#define TRY(expr)                  \
-    do {                           \
-        int rc_ = (expr);          \
-        if (rc_ != SM_OK) return rc_; \
-    } while (0)
-
-}  // namespace
-
-// Work fields, each 2*V complex (plane mu0 then mu1).
-enum { F_IN, F_OUT, F_TMP, F_X, F_R, F_D, F_D2, F_T, F_AD, F_PHI, F_L, F_RR, NFIELDS };
-
-struct sm_ctx {
-    int device = 0;
-    int nshard = 1, shard = 0;
-    Geometry g{};
-    LaunchCfg cfg{};
-    CGFusedCfg fcfg{};
-    int cg_fused = 1;               // 1: two-pass fused CG iteration (sm_cgfused.hip)
-    // one shard: alpha/beta by the last block of each pass instead of two
-    // one-block kernels. Measured equal at 4096^2 and 19 % slower at 1024^2
-    // (every block of a one-wave grid hits the ticket at once), so off by default.
-    int cg_inkernel = 0;
-    hipStream_t own_stream = nullptr, stream = nullptr;
-    hipStream_t comm_stream = nullptr;  // halo exchange overlapped with interior compute
-    hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
-    ncclComm_t comm = nullptr;
-    bool hosted = false;            // host-callback transport instead of RCCL
-    sm_host_transport tr{};
-    double *h_face = nullptr;       // pinned: send_lo, send_hi, recv_lo, recv_hi (4 x up to 8Nx doubles)
-    double *h_red = nullptr;        // pinned: all-reduce staging (8 doubles)
-    bool have_gauge = false;
-    double2 *U = nullptr;          // 2V
-    double2 *ghostU = nullptr;     // Nx: U_t at local t = -1 (lower neighbour's last column)
-    double2 *fields = nullptr;     // NFIELDS * 2V
-    double2 *faces = nullptr;      // 4 * 2Nx per spinor being exchanged (x2 for force)
-    double2 *faces2 = nullptr;     // 2-deep faces: send lo/hi of 2 fields (4Nx each), recv d, r, U (8Nx each)
-    double2 *partials = nullptr;   // 2 * max(nparts)
-    double2 *sums = nullptr;       // 4 complex scratch (allreduce)
-    double *Fbuf = nullptr;        // 2V doubles (force)
-    CGScalars *sc = nullptr;       // device
-    unsigned *counters = nullptr;  // device: last-block tickets (fused pass 1, pass 2)
-    CGScalars *h_sc = nullptr;     // pinned host mirror
-    double2 *h_sums = nullptr;     // pinned host
-    int nparts_dslash = 0, nparts_red = 0;
-    // active CG
-    double cg_mass = 0.0;
-    const double2 *cg_phi = nullptr;
-    double2 *cg_x = nullptr;
-    int cg_active = 0;
-    long cg_issued = 0;             // iterations enqueued since sm_cg_begin
-    int cg_pending_x = 0;           // fused path: last x update deferred to sm_cg_finish
-
-    double2 *field(int i) { return fields + (size_t)i * 2 * g.V; }
-};
-
-namespace {
 
 // Neighbour sources for `in`: periodic aliases (1 GPU) or received faces.
 TFaces faces_for(sm_ctx *c, const double2 *in, const double2 *recv_lo, const double2 *recv_hi) {
@@ -140,8 +70,6 @@ int down_rank(const sm_ctx *c) { return (c->shard - 1 + c->nshard) % c->nshard; 
 // My t = Wt-1 column goes up (it is the up-neighbour's t = -1), my t = 0
 // column goes down (the down-neighbour's t = Wt). The face buffers are
 // [plane][x], 4*Nx doubles.
-// Largest face exchanged, in doubles per x: 2 columns x 2 planes x complex.
-constexpr size_t kMaxFaceDoubles = 8;
 
 int exchange_faces_on(sm_ctx *c, hipStream_t s, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi,
                       size_t cnt) {
@@ -308,7 +236,7 @@ int exchange_ghost_U(sm_ctx *c) {
     return SM_OK;
 }
 
-}  // namespace
+}  // namespace sm_host
 
 // ============================================================================
 extern "C" {

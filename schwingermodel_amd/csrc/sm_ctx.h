@@ -1,0 +1,114 @@
+// sm_ctx.h -- private host-side state of one lattice shard (the opaque
+// sm_ctx of include/sm_hip.h) and the transport / launch helpers shared by
+// sm_capi.cpp (operators, CG) and sm_md.cpp (gauge field, MD, HMC).
+#pragma once
+#include "../../include/sm_hip.h"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstddef>
+
+#include "sm_internal.h"
+
+namespace sm_host {
+
+int fail(int code, const char *fmt, ...);
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return ::sm_host::fail(SM_ERR_HIP, "%s failed: %s (%s:%d)", #expr,           \
+                                   hipGetErrorString(e_), __FILE__, __LINE__);          \
+    } while (0)
+
+#define NCCL_TRY(expr)                                                                     \
+    do {                                                                                   \
+        ncclResult_t r_ = (expr);                                                          \
+        if (r_ != ncclSuccess)                                                             \
+            return ::sm_host::fail(SM_ERR_RCCL, "%s failed: %s (%s:%d)", #expr,             \
+                                   ncclGetErrorString(r_), __FILE__, __LINE__);            \
+    } while (0)
+
+#define TRY(expr)                     \
+    do {                              \
+        int rc_ = (expr);             \
+        if (rc_ != SM_OK) return rc_; \
+    } while (0)
+
+}  // namespace sm_host
+
+
+// Work fields, each 2*V complex (plane mu0 then mu1).
+enum { F_IN, F_OUT, F_TMP, F_X, F_R, F_D, F_D2, F_T, F_AD, F_PHI, F_L, F_RR, NFIELDS };
+
+struct sm_ctx {
+    int device = 0;
+    int nshard = 1, shard = 0;
+    sm::Geometry g{};
+    sm::LaunchCfg cfg{};
+    sm::CGFusedCfg fcfg{};
+    int cg_fused = 1;               // 1: two-pass fused CG iteration (sm_cgfused.hip)
+    // one shard: alpha/beta by the last block of each pass instead of two
+    // one-block kernels. Measured equal at 4096^2 and 19 % slower at 1024^2
+    // (every block of a one-wave grid hits the ticket at once), so off by default.
+    int cg_inkernel = 0;
+    hipStream_t own_stream = nullptr, stream = nullptr;
+    hipStream_t comm_stream = nullptr;  // halo exchange overlapped with interior compute
+    hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
+    ncclComm_t comm = nullptr;
+    bool hosted = false;            // host-callback transport instead of RCCL
+    sm_host_transport tr{};
+    double *h_face = nullptr;       // pinned: send_lo, send_hi, recv_lo, recv_hi (4 x up to 8Nx doubles)
+    double *h_red = nullptr;        // pinned: all-reduce staging (8 doubles)
+    bool have_gauge = false;
+    double2 *U = nullptr;          // 2V
+    double2 *ghostU = nullptr;     // Nx: U_t at local t = -1 (lower neighbour's last column)
+    double2 *fields = nullptr;     // NFIELDS * 2V
+    double2 *faces = nullptr;      // 4 * 2Nx per spinor being exchanged (x2 for force)
+    double2 *faces2 = nullptr;     // 2-deep faces: send lo/hi of 2 fields (4Nx each), recv d, r, U (8Nx each)
+    double2 *partials = nullptr;   // 2 * max(nparts)
+    double2 *sums = nullptr;       // 4 complex scratch (allreduce)
+    double *Fbuf = nullptr;        // 2V doubles (force)
+    sm::CGScalars *sc = nullptr;       // device
+    unsigned *counters = nullptr;  // device: last-block tickets (fused pass 1, pass 2)
+    sm::CGScalars *h_sc = nullptr;     // pinned host mirror
+    double2 *h_sums = nullptr;     // pinned host
+    int nparts_dslash = 0, nparts_red = 0;
+    // active CG
+    double cg_mass = 0.0;
+    const double2 *cg_phi = nullptr;
+    double2 *cg_x = nullptr;
+    int cg_active = 0;
+    long cg_issued = 0;             // iterations enqueued since sm_cg_begin
+    int cg_pending_x = 0;           // fused path: last x update deferred to sm_cg_finish
+
+    double2 *field(int i) { return fields + (size_t)i * 2 * g.V; }
+};
+
+namespace sm_host {
+
+using namespace sm;
+
+// Largest face exchanged, in doubles per x: 2 columns x 2 planes x complex.
+constexpr size_t kMaxFaceDoubles = 8;
+
+TFaces faces_for(sm_ctx *c, const double2 *in, const double2 *recv_lo, const double2 *recv_hi);
+double2 *face_buf(sm_ctx *c, int set, int which);
+int exchange_faces_on(sm_ctx *c, hipStream_t s, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi,
+                      size_t cnt);
+int exchange_faces(sm_ctx *c, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi, size_t cnt);
+int allreduce_dev(sm_ctx *c, double *dev, int n);
+int halo(sm_ctx *c, const double2 *field, int set, TFaces *f);
+const double2 *loU(sm_ctx *c);
+int apply(sm_ctx *c, const double2 *in, double2 *out, double mass, int dagger, const double2 *aux,
+          double2 *partials, const CGScalars *skip);
+int global_sum(sm_ctx *c, int nparts, const double2 *part, int slot);
+int check_ready(sm_ctx *c);
+int upload_plane_pair(sm_ctx *c, double2 *dst, const double *p0, const double *p1);
+int download_plane_pair(sm_ctx *c, const double2 *src, double *p0, double *p1);
+double2 *face2_recv(sm_ctx *c, int which);  // 0: d, 1: r, 2: U
+int exchange_ghost_U(sm_ctx *c);
+
+}  // namespace sm_host

@@ -33,6 +33,17 @@ def oracle():
                               ctypes.POINTER(ci), ctypes.POINTER(cd)]
     lib.oracle_cg.restype = ci
     lib.oracle_dirac_mt.argtypes = [ci, ci, vp, vp, vp, vp, vp, vp, cd, ci, ci]
+    lib.oracle_plaquette.argtypes = [ci, ci, vp, vp, vp]
+    lib.oracle_plaquette_sums.argtypes = [ci, ci, vp, vp, cd, vp, vp]
+    lib.oracle_staples.argtypes = [ci, ci, vp, vp, vp, vp]
+    lib.oracle_gauge_force.argtypes = [ci, ci, vp, vp, cd, vp, vp]
+    lib.oracle_md_force.argtypes = [ci, ci, vp, vp, vp, vp, cd, cd, cd, ci, vp, vp, ctypes.POINTER(ci)]
+    lib.oracle_md_force.restype = ci
+    lib.oracle_leapfrog.argtypes = [ci, ci, vp, vp, vp, vp, vp, vp, cd, cd, cd, ci, cd, ci,
+                                    ctypes.POINTER(ctypes.c_long)]
+    lib.oracle_leapfrog.restype = ci
+    lib.oracle_hamiltonian.argtypes = [ci, ci, vp, vp, vp, vp, vp, vp, cd, cd, cd, ci, ctypes.POINTER(ci)]
+    lib.oracle_hamiltonian.restype = cd
     return lib
 
 
@@ -50,6 +61,17 @@ def load_fixture(name):
 
 def fixture_names():
     return sorted(load_manifest()["fixtures"].keys())
+
+
+def load_md_fixture(name):
+    meta = load_manifest()["md"][name]
+    with np.load(os.path.join(GOLDEN, meta["file"]), allow_pickle=False) as z:
+        arrs = {k: z[k].copy() for k in z.files}
+    return meta, arrs
+
+
+def md_fixture_names():
+    return sorted(load_manifest().get("md", {}).keys())
 
 
 def ptr(a):

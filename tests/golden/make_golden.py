@@ -52,6 +52,20 @@ FIXTURES = [
 
 OUTS = ["ref_Dpsi", "ref_Ddagchi", "ref_DDdagpsi", "ref_force", "ref_cgx"]
 
+# Molecular-dynamics fixtures: the reference's gauge / HMC code
+# (`sm_ref_* md`) on U (generator), chi (generator) and momenta P (numpy,
+# seeded, stored in the fixture): plaquette field, staples, Force_G, Force,
+# phi = D chi, Leapfrog -> (U', P'), Hamiltonians before / after.
+# name, Nx, Nt, sigma, m0, beta, tau, md_steps
+MD_FIXTURES = [
+    ("md8x8_b2_m0p1", 8, 8, 0.4242, 0.1, 2.0, 1.0, 5),
+    ("md16x16_hot_m0", 16, 16, -1.0, 0.0, 2.0, 1.0, 4),
+    ("md32x48_b3_m0p1", 32, 48, 0.3246, 0.1, 3.0, 0.5, 6),
+    ("md64x64_b2_m0", 64, 64, 0.4242, 0.0, 2.0, 1.0, 10),
+]
+MD_OUTS = ["ref_plaq", "ref_staple", "ref_gforce", "ref_phi", "ref_mdforce", "ref_U1", "ref_P1"]
+SEED_P = 2468
+
 
 def run(cmd, **kw):
     env = dict(os.environ, HOSTNAME=os.environ.get("HOSTNAME", "localhost"))
@@ -102,14 +116,62 @@ def make_large(name, nx, nt, sigma, m0, workdir=None):
     return meta
 
 
+def make_md(name, nx, nt, sigma, m0, beta, tau, steps, mpi=None):
+    exe = os.path.join(REF_DIR, f"sm_ref_{nx}x{nt}")
+    S = nx * nt
+    with tempfile.TemporaryDirectory() as d:
+        run([exe, "gen", d, str(SEED_U), repr(sigma), str(SEED_PSI), str(SEED_CHI)])
+        np.random.default_rng(SEED_P).standard_normal(2 * S).tofile(os.path.join(d, "P.bin"))
+        args = [repr(m0), repr(beta), repr(tau), str(steps), "1e-10", "10000"]
+        meta = json.loads(run([exe, "md", d, "1", "1"] + args, cwd=d))
+        arrs = {k: np.fromfile(os.path.join(d, k + ".bin"), dtype=np.float64)
+                for k in ["U", "chi", "P"] + MD_OUTS}
+        arrs["ref_plaq"] = arrs["ref_plaq"][:2 * S]  # written as two identical planes
+        if mpi and nx % 2 == 0 and nt % 2 == 0 and nx >= 4 and nt >= 4:
+            meta2 = json.loads(run([mpi, "-n", "4", exe, "md", d, "2", "2"] + args, cwd=d, timeout=900))
+            dec = {}
+            for k in MD_OUTS:
+                a = np.fromfile(os.path.join(d, k + ".bin"), dtype=np.float64)
+                if k == "ref_plaq":
+                    a = a[:2 * S]
+                b = arrs[k]
+                dec[k] = "bitwise" if np.array_equal(a.view(np.uint64), b.view(np.uint64)) \
+                    else f"max_abs={np.abs(a - b).max():.3e}"
+            for k in ("sp", "gauge_action", "H0", "H1"):
+                dec[k] = meta2[k]
+            meta["decomposition_2x2"] = dec
+    meta.update({"sigma": sigma, "file": name + ".npz", "seed_P": SEED_P})
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
+    return meta
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mpi", action="store_true", help="also run 2x2 ranks (mpirun)")
     ap.add_argument("--large", action="store_true", help="also the 1024^2 summary fixture (~4 min CPU)")
     ap.add_argument("--large-workdir", default=None, help="reuse an existing reference run directory")
     ap.add_argument("--mpirun", default="/opt/conda/bin/mpirun")
+    ap.add_argument("--md-only", action="store_true", help="regenerate only the MD fixtures")
     args = ap.parse_args()
-    sizes = sorted({f"{nx}x{nt}" for _, nx, nt, _, _ in FIXTURES})
+    if args.md_only:
+        sizes = sorted({f"{nx}x{nt}" for _, nx, nt, *_ in MD_FIXTURES})
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref", "oracle",
+                        "REF_SIZES=" + " ".join(sizes)], check=True)
+        path = os.path.join(HERE, "manifest.json")
+        with open(path) as f:
+            manifest = json.load(f)
+        manifest["md"] = {}
+        for name, nx, nt, sigma, m0, beta, tau, steps in MD_FIXTURES:
+            manifest["md"][name] = make_md(name, nx, nt, sigma, m0, beta, tau, steps,
+                                           args.mpirun if args.mpi else None)
+            print(name, json.dumps(manifest["md"][name]), file=sys.stderr)
+        manifest["md_params"] = {"seed_P": SEED_P, "P": "numpy default_rng(seed_P).standard_normal(2S)",
+                                 "cg": {"tol": 1e-10, "max_iter": 10000}}
+        with open(path, "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+        return
+    sizes = sorted({f"{nx}x{nt}" for _, nx, nt, _, _ in FIXTURES} |
+                   {f"{nx}x{nt}" for _, nx, nt, *_ in MD_FIXTURES})
     subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref", "oracle",
                     "REF_SIZES=" + " ".join(sizes)], check=True)
     manifest = {"generator": "tests/golden/make_golden.py",
@@ -142,6 +204,12 @@ def main():
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
         manifest["fixtures"][name] = meta
         print(name, json.dumps(meta), file=sys.stderr)
+    manifest["md"] = {}
+    for name, nx, nt, sigma, m0, beta, tau, steps in MD_FIXTURES:
+        manifest["md"][name] = make_md(name, nx, nt, sigma, m0, beta, tau, steps,
+                                       args.mpirun if args.mpi else None)
+    manifest["md_params"] = {"seed_P": SEED_P, "P": "numpy default_rng(seed_P).standard_normal(2S)",
+                             "cg": {"tol": 1e-10, "max_iter": 10000}}
     if args.large:
         subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref", "REF_SIZES=1024x1024"], check=True)
         manifest["large"] = {}
