@@ -168,6 +168,87 @@ int sm_cg_status(sm_ctx *ctx, sm_cg_result *res);
  * then x lags one update behind the reference's x. */
 int sm_cg_finish(sm_ctx *ctx, sm_cg_result *res);
 
+/* ==== gauge field, molecular dynamics and HMC =====
+ * The next layer out from the Dirac/CG path: the whole MD force step of
+ * src/hmc.cpp with U, momenta and forces resident on the device (the drop-in
+ * shim above re-uploads U per call; these never do). Every sum is global over
+ * shards (all ranks call in lockstep). Momenta: two planes of V doubles. */
+
+/* Copy this shard's gauge field to the host (reference layout). */
+int sm_download_gauge(sm_ctx *ctx, double *U0, double *U1);
+/* Draw the gauge field on the device with the sm_fill_gauge generator
+ * (sigma > 0 Gaussian angle, < 0 hot start as GaugeConf::initialization
+ * src/gauge_conf.cpp:32-37, 0 cold). Same distribution as the host draw;
+ * the device's log/sincos may differ from glibc in the last bit. */
+int sm_fill_gauge_dev(sm_ctx *ctx, uint64_t seed, double sigma);
+
+/* Compute_Plaquette01 + MeasureSp_HMC + Compute_gaugeAction
+ * (src/gauge_conf.cpp:41-85, 430-453): *sp = sum_n Re U_01(n),
+ * *gauge_action = sum_n beta Re(1 - U_01(n)). plaq (host, nullable) receives
+ * this shard's U_01(n) field (V complex). */
+int sm_plaquette(sm_ctx *ctx, double beta, double *sp, double *gauge_action, double *plaq);
+/* GaugeConf::Compute_Staple (src/gauge_conf.cpp:89-373): both directions,
+ * host output (reference spinor layout). */
+int sm_staples(sm_ctx *ctx, double *S0, double *S1);
+/* HMC::Force_G (src/hmc.cpp:31-40): F += -beta Im(U conj(staple)), host F. */
+int sm_gauge_force(sm_ctx *ctx, double beta, double *F0, double *F1);
+
+/* HMC parameters (src/main.cpp:19-27 inputs + the CG settings). */
+typedef struct {
+    double m0;          /* bare mass                                       */
+    double beta;        /* gauge coupling                                  */
+    double tau;         /* trajectory length                               */
+    int md_steps;       /* leapfrog steps (the reference evaluates the force
+                           md_steps - 1 times, src/hmc.cpp:76)             */
+    double cg_tol;      /* CG::tol (1e-10 in src/main.cpp:27)              */
+    int cg_max_iter;    /* CG::max_iter (10000)                            */
+    uint64_t seed;      /* counter-based draws: momenta, sources, Metropolis */
+} sm_hmc_params;
+
+/* HMC::Force (src/hmc.cpp:44-60) at the current U: psi = (DD^dag)^-1 phi,
+ * F = phi_dag_partialD_phi(U, psi, D^dag psi) + gauge force. res: the CG. */
+int sm_md_force(sm_ctx *ctx, const sm_hmc_params *p, const double *phi0, const double *phi1, double *F0,
+                double *F1, sm_cg_result *res);
+int sm_md_force_dev(sm_ctx *ctx, const sm_hmc_params *p, const double *phi, double *F, sm_cg_result *res);
+/* HMC::Leapfrog (src/hmc.cpp:63-101): evolves the context's U and the
+ * momenta P (in/out) along one trajectory; *cg_iters = CG loop passes summed
+ * over the force evaluations; *cg_failures = non-converged solves. */
+int sm_leapfrog(sm_ctx *ctx, const sm_hmc_params *p, const double *phi0, const double *phi1, double *P0,
+                double *P1, long *cg_iters, int *cg_failures);
+int sm_leapfrog_dev(sm_ctx *ctx, const sm_hmc_params *p, const double *phi, double *P, long *cg_iters,
+                    int *cg_failures);
+/* HMC::Hamiltonian (src/hmc.cpp:104-148) at the current U:
+ * H = sum 0.5 P^2 + (beta sum Re(1 - U_01) + Re dot((DD^dag)^-1 phi, phi)). */
+typedef struct {
+    double H;             /* the Hamiltonian                                */
+    double kinetic;       /* sum 0.5 P^2                                    */
+    double gauge_action;  /* beta sum Re(1 - U_01)                          */
+    double fermion;       /* Re dot((DD^dag)^-1 phi, phi)                   */
+    double sp;            /* sum Re U_01                                    */
+    int cg_iterations;
+    int cg_converged;
+} sm_hamiltonian_terms;
+int sm_hamiltonian(sm_ctx *ctx, const sm_hmc_params *p, const double *phi0, const double *phi1, const double *P0,
+                   const double *P1, sm_hamiltonian_terms *out);
+int sm_hamiltonian_dev(sm_ctx *ctx, const sm_hmc_params *p, const double *phi, const double *P,
+                       sm_hamiltonian_terms *out);
+
+/* One HMC update, HMC::HMC_Update (src/hmc.cpp:151-178), entirely on the
+ * device: momenta and chi drawn for trajectory `traj` (counter-based, the
+ * same on every rank), phi = D chi, leapfrog on a copy of U, Metropolis with
+ * r = uniform(seed, traj) (identical on all ranks, no broadcast). On reject
+ * the previous U is restored by a buffer swap. */
+typedef struct {
+    double H_old, H_new, dH;
+    double r;              /* the Metropolis uniform                          */
+    int accepted;
+    double sp;             /* sum Re U_01 of the configuration kept           */
+    double gauge_action;   /* beta sum Re(1 - U_01) of the configuration kept */
+    long cg_iterations;    /* all solves: H_old, the forces, H_new            */
+    int cg_failures;
+} sm_hmc_result;
+int sm_hmc_trajectory(sm_ctx *ctx, const sm_hmc_params *p, uint64_t traj, sm_hmc_result *out);
+
 #ifdef __cplusplus
 }
 #endif

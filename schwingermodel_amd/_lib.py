@@ -20,6 +20,25 @@ class CGResult(ctypes.Structure):
                 ("residual", ctypes.c_double), ("phi_norm", ctypes.c_double)]
 
 
+class HMCParams(ctypes.Structure):
+    _fields_ = [("m0", ctypes.c_double), ("beta", ctypes.c_double), ("tau", ctypes.c_double),
+                ("md_steps", ctypes.c_int), ("cg_tol", ctypes.c_double), ("cg_max_iter", ctypes.c_int),
+                ("seed", ctypes.c_uint64)]
+
+
+class HamiltonianTerms(ctypes.Structure):
+    _fields_ = [("H", ctypes.c_double), ("kinetic", ctypes.c_double), ("gauge_action", ctypes.c_double),
+                ("fermion", ctypes.c_double), ("sp", ctypes.c_double), ("cg_iterations", ctypes.c_int),
+                ("cg_converged", ctypes.c_int)]
+
+
+class HMCResult(ctypes.Structure):
+    _fields_ = [("H_old", ctypes.c_double), ("H_new", ctypes.c_double), ("dH", ctypes.c_double),
+                ("r", ctypes.c_double), ("accepted", ctypes.c_int), ("sp", ctypes.c_double),
+                ("gauge_action", ctypes.c_double), ("cg_iterations", ctypes.c_long),
+                ("cg_failures", ctypes.c_int)]
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`"
@@ -63,6 +82,20 @@ def _load():
         "sm_cg_status": ([vp, ctypes.POINTER(CGResult)], ci),
         "sm_cg_finish": ([vp, ctypes.POINTER(CGResult)], ci),
         "sm_tune_cg": ([vp, ci, ci], ci),
+        # gauge field / molecular dynamics / HMC
+        "sm_download_gauge": ([vp, vp, vp], ci),
+        "sm_fill_gauge_dev": ([vp, u64, cd], ci),
+        "sm_plaquette": ([vp, cd, ctypes.POINTER(cd), ctypes.POINTER(cd), vp], ci),
+        "sm_staples": ([vp, vp, vp], ci),
+        "sm_gauge_force": ([vp, cd, vp, vp], ci),
+        "sm_md_force": ([vp, ctypes.POINTER(HMCParams), vp, vp, vp, vp, ctypes.POINTER(CGResult)], ci),
+        "sm_md_force_dev": ([vp, ctypes.POINTER(HMCParams), vp, vp, ctypes.POINTER(CGResult)], ci),
+        "sm_leapfrog": ([vp, ctypes.POINTER(HMCParams), vp, vp, vp, vp, ctypes.POINTER(cl),
+                         ctypes.POINTER(ci)], ci),
+        "sm_leapfrog_dev": ([vp, ctypes.POINTER(HMCParams), vp, vp, ctypes.POINTER(cl), ctypes.POINTER(ci)], ci),
+        "sm_hamiltonian": ([vp, ctypes.POINTER(HMCParams), vp, vp, vp, vp, ctypes.POINTER(HamiltonianTerms)], ci),
+        "sm_hamiltonian_dev": ([vp, ctypes.POINTER(HMCParams), vp, vp, ctypes.POINTER(HamiltonianTerms)], ci),
+        "sm_hmc_trajectory": ([vp, ctypes.POINTER(HMCParams), u64, ctypes.POINTER(HMCResult)], ci),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

@@ -13,8 +13,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libsm_hip.so")
-SOURCES = ["sm_kernels.hip", "sm_cgfused.hip", "sm_capi.cpp"]
-HEADERS = ["sm_internal.h", "sm_fields.h", "sm_device.h"]
+SOURCES = ["sm_kernels.hip", "sm_cgfused.hip", "sm_gauge.hip", "sm_capi.cpp", "sm_md.cpp"]
+HEADERS = ["sm_internal.h", "sm_fields.h", "sm_device.h", "sm_ctx.h"]
 
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")

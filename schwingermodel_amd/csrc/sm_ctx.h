@@ -76,6 +76,10 @@ struct sm_ctx {
     sm::CGScalars *h_sc = nullptr;     // pinned host mirror
     double2 *h_sums = nullptr;     // pinned host
     int nparts_dslash = 0, nparts_red = 0;
+    // molecular dynamics (sm_md.cpp; allocated on first use)
+    double2 *U_alt = nullptr;       // 2V: the other gauge buffer (leapfrog copy / kept conf)
+    double *Pmd = nullptr;          // 2V: momenta
+    double *Fmd = nullptr;          // 2V: MD force
     // active CG
     double cg_mass = 0.0;
     const double2 *cg_phi = nullptr;

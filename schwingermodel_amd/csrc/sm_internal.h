@@ -112,6 +112,20 @@ void launch_pack_faces2(hipStream_t s, const Geometry &g, const double2 *field, 
 void launch_stream(hipStream_t s, int two, long n, const double2 *a, const double2 *b, double2 *out,
                    int blocks);
 
+// ---- gauge field / molecular dynamics (sm_gauge.hip) ----
+// fU: the 2-deep U faces (nshard > 1; ignored for one shard, which wraps).
+int gauge_reduce_blocks(const Geometry &g);
+void launch_plaquette(hipStream_t s, const Geometry &g, int nshard, const double2 *U, const double2 *fU,
+                      double beta, double2 *field, double2 *partials);
+void launch_staple_force(hipStream_t s, const Geometry &g, int nshard, const double2 *U, const double2 *fU,
+                         double beta, double *F, double2 *staples);
+void launch_md_update(hipStream_t s, const Geometry &g, double2 *U, double *P, const double *F, double eps,
+                      int do_p, double coef);
+void launch_kinetic(hipStream_t s, const Geometry &g, const double *P, double2 *partials);
+void launch_draw_momenta(hipStream_t s, const Geometry &g, uint64_t seed, double *P);
+void launch_draw_source(hipStream_t s, const Geometry &g, uint64_t seed, double2 *chi);
+void launch_draw_gauge(hipStream_t s, const Geometry &g, uint64_t seed, double sigma, double2 *U);
+
 // Pack the t = 0 and t = Wt-1 columns (both planes) into contiguous faces.
 void launch_pack_faces(hipStream_t s, const Geometry &g, const double2 *field, double2 *lo_face,
                        double2 *hi_face);

@@ -10,6 +10,7 @@ import ctypes
 import os
 import re
 import struct
+import subprocess
 
 import numpy as np
 import pytest
@@ -112,3 +113,26 @@ def test_no_gpu_fails_loudly():
     assert rc != 0 and h.value is None
     with pytest.raises(sm.SMError):
         sm.init(8, 8)
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """The ctypes mirrors of the ABI structs have the C header's size and offsets."""
+    import schwingermodel_amd._lib as L
+    structs = {"sm_cg_result": L.CGResult, "sm_hmc_params": L.HMCParams,
+               "sm_hamiltonian_terms": L.HamiltonianTerms, "sm_hmc_result": L.HMCResult}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "sm_hip.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            lines.append(f'printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines.append("return 0; }")
+    src = tmp_path / "probe.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    got = {tuple(ln.split()[:2]): int(ln.split()[2]) for ln in out if ln}
+    for cname, py in structs.items():
+        assert got[(cname, "size")] == ctypes.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert got[(cname, fname)] == getattr(py, fname).offset, (cname, fname)
