@@ -249,6 +249,39 @@ typedef struct {
 } sm_hmc_result;
 int sm_hmc_trajectory(sm_ctx *ctx, const sm_hmc_params *p, uint64_t traj, sm_hmc_result *out);
 
+/* HMC::HMC_algorithm (src/hmc.cpp:181-213): optional hot start
+ * (GaugeConf::initialization, drawn on the device), Ntherm thermalisation
+ * updates, then Nmeas measurements of Sp and the gauge action separated by
+ * Nsteps decorrelation updates. Ep = mean(Sp)/V, dEp = Jackknife_error(Sp,
+ * 20)/V, gS and dgS likewise (src/statistics.cpp:4-34, restated with its
+ * integer binning), V = Nx*Nt. Trajectories are numbered 0, 1, ... from
+ * first_traj (the counter-based draws' key). acceptance = accepted /
+ * (Nmeas + Nsteps*(Nmeas-1)): the updates of the measurement phase (the
+ * reference's SimData value, src/main.cpp:169). sp_series / gs_series
+ * (nullable, Nmeas doubles) receive the measured Sp / gauge action.
+ * save_prefix (nullable): after measurement i, shard 0 writes
+ * <save_prefix>_<i>.ctxt in the 28-byte record format (SaveConf). */
+typedef struct {
+    double Ep, dEp, gS, dgS;
+    double acceptance;
+    long accepted;          /* measurement-phase accepts                  */
+    long trajectories;      /* all updates run                            */
+    long cg_iterations;
+    int cg_failures;
+} sm_hmc_summary;
+int sm_hmc_run(sm_ctx *ctx, const sm_hmc_params *p, int hot_start, uint64_t first_traj, int Ntherm, int Nmeas,
+               int Nsteps, const char *save_prefix, sm_hmc_summary *out, double *sp_series, double *gs_series);
+
+/* Jackknife_error (src/statistics.cpp:25-34) with its binning as written:
+ * bin blocks of n/bin samples; leftover samples only enter the mean. */
+double sm_jackknife_error(const double *dat, int n, int bin);
+
+/* Gather the sharded gauge field to shard 0 (SaveConf's MPI_Gatherv,
+ * src/gauge_conf.cpp:378-396): U0/U1 on shard 0 receive the global
+ * Nx x Nt field (n = x*Nt + t); other shards may pass NULL. RCCL transport
+ * or one shard only. */
+int sm_gather_gauge(sm_ctx *ctx, double *U0, double *U1);
+
 #ifdef __cplusplus
 }
 #endif

@@ -310,6 +310,12 @@ int main(int argc, char **argv) {
     } else if (argc >= 8 && !strcmp(argv[1], "fixture")) {
         setup(atoi(argv[3]), atoi(argv[4]));
         rc = run_fixture(argv[2], atof(argv[5]), atof(argv[6]), atoi(argv[7]));
+    } else if (argc >= 3 && !strcmp(argv[1], "jk")) {
+        // jk <bin> v1 v2 ...: the reference's Jackknife_error and mean
+        std::vector<double> v;
+        for (int i = 3; i < argc; i++) v.push_back(strtod(argv[i], nullptr));
+        printf("%.17g %.17g\n", Jackknife_error(v, atoi(argv[2])), mean(v));
+        rc = 0;
     } else if (argc >= 11 && !strcmp(argv[1], "md")) {
         setup(atoi(argv[3]), atoi(argv[4]));
         rc = run_md(argv[2], atof(argv[5]), atof(argv[6]), atof(argv[7]), atoi(argv[8]), atof(argv[9]),

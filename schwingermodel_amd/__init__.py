@@ -25,7 +25,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import CGResult, HamiltonianTerms, HMCParams, HMCResult, SMError, check, lib
+from ._lib import CGResult, HamiltonianTerms, HMCParams, HMCResult, HMCSummary, SMError, check, lib
 
 __all__ = ["spinor", "re_field", "c_double", "I_number", "CG", "init", "lattice", "Lattice",
            "D_phi", "D_dagger_phi", "D_D_dagger_phi", "phi_dag_partialD_phi",

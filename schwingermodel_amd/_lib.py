@@ -32,6 +32,12 @@ class HamiltonianTerms(ctypes.Structure):
                 ("cg_converged", ctypes.c_int)]
 
 
+class HMCSummary(ctypes.Structure):
+    _fields_ = [("Ep", ctypes.c_double), ("dEp", ctypes.c_double), ("gS", ctypes.c_double),
+                ("dgS", ctypes.c_double), ("acceptance", ctypes.c_double), ("accepted", ctypes.c_long),
+                ("trajectories", ctypes.c_long), ("cg_iterations", ctypes.c_long), ("cg_failures", ctypes.c_int)]
+
+
 class HMCResult(ctypes.Structure):
     _fields_ = [("H_old", ctypes.c_double), ("H_new", ctypes.c_double), ("dH", ctypes.c_double),
                 ("r", ctypes.c_double), ("accepted", ctypes.c_int), ("sp", ctypes.c_double),
@@ -96,6 +102,10 @@ def _load():
         "sm_hamiltonian": ([vp, ctypes.POINTER(HMCParams), vp, vp, vp, vp, ctypes.POINTER(HamiltonianTerms)], ci),
         "sm_hamiltonian_dev": ([vp, ctypes.POINTER(HMCParams), vp, vp, ctypes.POINTER(HamiltonianTerms)], ci),
         "sm_hmc_trajectory": ([vp, ctypes.POINTER(HMCParams), u64, ctypes.POINTER(HMCResult)], ci),
+        "sm_hmc_run": ([vp, ctypes.POINTER(HMCParams), ci, u64, ci, ci, ci, ctypes.c_char_p,
+                        ctypes.POINTER(HMCSummary), vp, vp], ci),
+        "sm_jackknife_error": ([vp, ci, ci], cd),
+        "sm_gather_gauge": ([vp, vp, vp], ci),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

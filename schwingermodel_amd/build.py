@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libsm_hip.so")
-SOURCES = ["sm_kernels.hip", "sm_cgfused.hip", "sm_gauge.hip", "sm_capi.cpp", "sm_md.cpp"]
+SOURCES = ["sm_kernels.hip", "sm_cgfused.hip", "sm_gauge.hip", "sm_capi.cpp", "sm_md.cpp", "sm_hmc.cpp"]
 HEADERS = ["sm_internal.h", "sm_fields.h", "sm_device.h", "sm_ctx.h"]
 
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
@@ -50,6 +50,33 @@ def build_library(force=False, verbose=True):
     return LIB
 
 
+CLI = os.path.join(HERE, "sm_hmc")
+MPI_ROOT = os.environ.get("SM_MPI_ROOT", "/opt/conda")
+
+
+def build_cli(force=False, verbose=True):
+    """`sm_hmc`: the reference's HMC program (src/main.cpp) on the device
+    layer, one MPI rank per GPU. Needs an MPI (the image's MPICH under
+    /opt/conda, as the reference); skipped with a note when absent."""
+    src = os.path.join(CSRC, "sm_hmc_main.cpp")
+    mpi_so = os.path.join(MPI_ROOT, "lib", "libmpi.so")
+    if not os.path.exists(os.path.join(MPI_ROOT, "include", "mpi.h")) or not os.path.exists(mpi_so):
+        print(f"sm_hmc not built: no MPI under {MPI_ROOT}", file=sys.stderr)
+        return None
+    if not force and not _stale(CLI, [src, LIB, os.path.join(REPO, "include", "sm_hip.h")]):
+        return CLI
+    cmd = ["g++", "-O2", "-std=c++17", f"-I{os.path.join(REPO, 'include')}", f"-I{MPI_ROOT}/include", src,
+           "-o", CLI + ".tmp", mpi_so, f"-Wl,-rpath,{MPI_ROOT}/lib", "-static-libstdc++", "-static-libgcc",
+           # conda's old libstdc++ must not shadow the system one libsm_hip.so needs
+           "-Wl,-rpath-link,/usr/lib/x86_64-linux-gnu", f"-Wl,-rpath-link,{ROCM}/lib",
+           f"-L{HERE}", "-lsm_hip", "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(CLI + ".tmp", CLI)
+    return CLI
+
+
 def build_oracle(with_reference=None):
     """Test checker: oracle/liboracle.so, plus oracle/_ref/ when /root/reference exists."""
     oracle_dir = os.path.join(REPO, "oracle")
@@ -64,3 +91,4 @@ def build_oracle(with_reference=None):
 
 if __name__ == "__main__":
     build_library(force="--force" in sys.argv)
+    build_cli(force="--force" in sys.argv)

@@ -8,6 +8,9 @@ mode "oracle" (CPU, gloo): every rank applies the ORACLE's local operator to its
     t-shard with faces exchanged by schwingermodel_amd.dist.exchange_faces (the
     protocol of the GPU path) and the geometry of sm_shard_plan; rank 0 checks
     the gathered result bit-for-bit against the reference's golden vectors.
+mode "md" (one GPU, gloo host transport): the molecular-dynamics layer
+    (plaquette, staples, gauge force, MD force, Hamiltonian, leapfrog, one HMC
+    trajectory) on t-shards vs the reference's MD fixture / one shard.
 mode "gpu" (one GPU shared by all ranks, gloo host transport): every rank runs
     the HIP kernels on its shard through sm_create_hosted (same kernels, face
     packing, ghost links, sign ownership and scalar reductions as the RCCL
@@ -80,11 +83,117 @@ def single_reference(sm, a, meta):
     L.close()
 
 
+def shard_real(flat, Nx, Nt, t0, Wt):
+    """Global two-plane real field (re_field) -> this shard's two planes."""
+    S = Nx * Nt
+    return [np.ascontiguousarray(flat[S * p: S * (p + 1)].reshape(Nx, Nt)[:, t0:t0 + Wt]).reshape(-1)
+            for p in range(2)]
+
+
+def run_md(name, result_path, dist, rank, world):
+    """mode "md": the MD layer on t-shards (hosted transport) vs the reference's
+    MD fixture, plus one HMC trajectory vs the same trajectory on one shard."""
+    from conftest import bits_equal, load_md_fixture
+    import schwingermodel_amd as sm
+    from schwingermodel_amd import dist as smd
+    meta, a = load_md_fixture(name)
+    Nx, Nt = meta["Nx"], meta["Nt"]
+    S = Nx * Nt
+    t0, Wt = ctypes.c_int(), ctypes.c_int()
+    sm.check(sm.lib.sm_shard_plan(Nt, world, rank, ctypes.byref(t0), ctypes.byref(Wt)))
+    t0, Wt = t0.value, Wt.value
+    V = Nx * Wt
+    P_ = lambda x: ctypes.c_void_p(x.ctypes.data)  # noqa: E731
+    U = shard_field(a["U"], Nx, Nt, t0, Wt)
+    phi = shard_field(a["ref_phi"], Nx, Nt, t0, Wt)
+    Pm = shard_real(a["P"], Nx, Nt, t0, Wt)
+    prm = sm.HMCParams(meta["m0"], meta["beta"], meta["tau"], meta["md_steps"], 1e-10, 10000, 99)
+    dev = int(os.environ.get("SM_DEVICE", "0"))
+    ctx, tr = smd.create_hosted_context(Nx, Nt, device=dev)
+    sm.check(sm.lib.sm_upload_gauge(ctx, P_(U[0]), P_(U[1])))
+    local = {}
+    sp, act = ctypes.c_double(), ctypes.c_double()
+    plaq = np.empty(V, complex)
+    sm.check(sm.lib.sm_plaquette(ctx, meta["beta"], ctypes.byref(sp), ctypes.byref(act), P_(plaq)))
+    local["sums"] = (sp.value, act.value)
+    local["ref_plaq"] = (plaq, plaq)
+    S0, S1 = np.empty(V, complex), np.empty(V, complex)
+    sm.check(sm.lib.sm_staples(ctx, P_(S0), P_(S1)))
+    local["ref_staple"] = (S0, S1)
+    F0, F1 = np.zeros(V), np.zeros(V)
+    sm.check(sm.lib.sm_gauge_force(ctx, meta["beta"], P_(F0), P_(F1)))
+    local["ref_gforce"] = (F0, F1)
+    G0, G1 = np.empty(V), np.empty(V)
+    res = sm.CGResult()
+    sm.check(sm.lib.sm_md_force(ctx, ctypes.byref(prm), P_(phi[0]), P_(phi[1]), P_(G0), P_(G1), ctypes.byref(res)))
+    local["ref_mdforce"] = (G0, G1)
+    h = sm.HamiltonianTerms()
+    sm.check(sm.lib.sm_hamiltonian(ctx, ctypes.byref(prm), P_(phi[0]), P_(phi[1]), P_(Pm[0]), P_(Pm[1]),
+                                   ctypes.byref(h)))
+    local["H0"] = h.H
+    it, fails = ctypes.c_long(), ctypes.c_int()
+    sm.check(sm.lib.sm_leapfrog(ctx, ctypes.byref(prm), P_(phi[0]), P_(phi[1]), P_(Pm[0]), P_(Pm[1]),
+                                ctypes.byref(it), ctypes.byref(fails)))
+    U1a, U1b = np.empty(V, complex), np.empty(V, complex)
+    sm.check(sm.lib.sm_download_gauge(ctx, P_(U1a), P_(U1b)))
+    local["ref_U1"] = (U1a, U1b)
+    local["ref_P1"] = (Pm[0].copy(), Pm[1].copy())
+    sm.check(sm.lib.sm_hamiltonian(ctx, ctypes.byref(prm), P_(phi[0]), P_(phi[1]), P_(Pm[0]), P_(Pm[1]),
+                                   ctypes.byref(h)))
+    local["H1"] = h.H
+    # one full HMC trajectory from the fixture's U (device draws keyed on the
+    # global site: every sharding draws the same momenta and sources)
+    sm.check(sm.lib.sm_upload_gauge(ctx, P_(U[0]), P_(U[1])))
+    r = sm.HMCResult()
+    sm.check(sm.lib.sm_hmc_trajectory(ctx, ctypes.byref(prm), 3, ctypes.byref(r)))
+    Ua, Ub = np.empty(V, complex), np.empty(V, complex)
+    sm.check(sm.lib.sm_download_gauge(ctx, P_(Ua), P_(Ub)))
+    local["traj"] = (r.dH, r.accepted, r.r)
+    local["traj_U"] = (Ua, Ub)
+    sm.lib.sm_destroy(ctx)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, local)
+    if rank == 0:
+        rep = {"world": world, "fixture": name, "checks": {}}
+        for key in ("ref_plaq", "ref_staple", "ref_gforce"):
+            dtype = float if key == "ref_gforce" else complex
+            g = unshard([d[key] for d in gathered], Nx, Nt, Wt, dtype)
+            if key == "ref_plaq":
+                g = g[:2 * S]
+            rep["checks"][key] = bool(bits_equal(g, a[key]))
+        for key in ("ref_mdforce", "ref_P1"):
+            g = unshard([d[key] for d in gathered], Nx, Nt, Wt, float)
+            rep["checks"][key] = float(np.linalg.norm(g - a[key]) / np.linalg.norm(a[key]))
+        g = unshard([d["ref_U1"] for d in gathered], Nx, Nt, Wt, complex)
+        rep["checks"]["ref_U1"] = float(np.linalg.norm(g - a["ref_U1"]) / np.linalg.norm(a["ref_U1"]))
+        rep["sums"] = [d["sums"] for d in gathered]
+        rep["H0"] = [d["H0"] for d in gathered]
+        rep["H1"] = [d["H1"] for d in gathered]
+        rep["meta"] = {k: meta[k] for k in ("sp", "gauge_action", "H0", "H1")}
+        # the same trajectory on one shard of the same GPU
+        L = sm.Lattice(Nx, Nt, device=dev)
+        sm.check(sm.lib.sm_upload_gauge(L.ctx, P_(a["U"]), P_(a["U"][2 * S:])))
+        r1 = sm.HMCResult()
+        sm.check(sm.lib.sm_hmc_trajectory(L.ctx, ctypes.byref(prm), 3, ctypes.byref(r1)))
+        U1 = np.empty(4 * S)
+        sm.check(sm.lib.sm_download_gauge(L.ctx, P_(U1), P_(U1[2 * S:])))
+        L.close()
+        g = unshard([d["traj_U"] for d in gathered], Nx, Nt, Wt, complex)
+        rep["traj"] = {"sharded": [d["traj"] for d in gathered], "single": (r1.dH, r1.accepted, r1.r),
+                       "U_rel": float(np.linalg.norm(g - U1) / np.linalg.norm(U1))}
+        with open(result_path, "w") as f:
+            json.dump(rep, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     mode, name, result_path = sys.argv[1], sys.argv[2], sys.argv[3]
     import torch.distributed as dist
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
+    if mode == "md":
+        return run_md(name, result_path, dist, rank, world)
     from conftest import bits_equal, load_fixture
     import schwingermodel_amd as sm
     from schwingermodel_amd import dist as smd

@@ -116,6 +116,56 @@ def make_large(name, nx, nt, sigma, m0, workdir=None):
     return meta
 
 
+def make_jackknife():
+    """Reference Jackknife_error(dat, 20) and mean(dat) (src/statistics.cpp)
+    on seeded series, including lengths that are not multiples of the 20 bins
+    and shorter than one sample per bin (the reference's integer binning)."""
+    exe = os.path.join(REF_DIR, "sm_ref_8x8")
+    rng = np.random.default_rng(1357)
+    cases = []
+    for n in (3, 19, 20, 22, 45, 100, 257):
+        dat = (0.7 + 0.05 * rng.standard_normal(n)).tolist()
+        out = run([exe, "jk", "20"] + [repr(v) for v in dat]).split()
+        cases.append({"bin": 20, "data": dat, "jackknife_error": float(out[0]), "mean": float(out[1])})
+    return cases
+
+
+# Statistical HMC reference (SURVEY.md §8f row 3): the unmodified reference
+# program (oracle/_ref/SM_64x64_ref, built by `make -C oracle refapp`) on its
+# own stdin parameters. Its RNG is seeded from the clock, so parity with it is
+# statistical: Ep, gS within their jackknife errors, acceptance close.
+HMC_STAT = {"name": "hmc64x64_b2_m0", "Nx": 64, "Nt": 64, "m0": 0.0, "md_steps": 10, "tau": 0.3, "beta": 2.0,
+            "Ntherm": 50, "Nmeas": 100, "Nsteps": 1}
+
+
+def parse_hmc_output(stdout, simdata):
+    import re
+    ep = re.search(r"Ep = (\S+) dEp = (\S+)", stdout)
+    gs = re.search(r"gS = (\S+) dgS = (\S+)", stdout)
+    lines = [ln for ln in simdata.splitlines() if ln and not ln.startswith("#")]
+    acc_file = float(lines[-2])  # "#Acceptance rate" value, then "#Execution time"
+    t = re.search(r"Execution time = (\S+) s", stdout)
+    return {"Ep": float(ep.group(1)), "dEp": float(ep.group(2)), "gS": float(gs.group(1)),
+            "dgS": float(gs.group(2)), "acceptance": acc_file, "seconds": float(t.group(1))}
+
+
+def make_hmc_stat(log_dir=None):
+    c = HMC_STAT
+    params = f"1\n1\n{c['m0']}\n{c['md_steps']}\n{c['tau']}\n{c['beta']}\n{c['Ntherm']}\n{c['Nmeas']}\n{c['Nsteps']}\n0\n"
+    exe = os.path.join(REF_DIR, f"SM_{c['Nx']}x{c['Nt']}_ref")
+    with tempfile.TemporaryDirectory() as d:
+        d = log_dir or d
+        if not os.path.exists(os.path.join(d, "run1.log")):
+            out = run([exe], input=params, cwd=d, timeout=1800)
+        else:
+            with open(os.path.join(d, "run1.log")) as f:
+                out = f.read()
+        sim = [f for f in os.listdir(d) if f.endswith("_SimData.txt")][0]
+        with open(os.path.join(d, sim)) as f:
+            res = parse_hmc_output(out, f.read())
+    return dict(c, **res, program="reference src/main.cpp (CPU, 1 rank)")
+
+
 def make_md(name, nx, nt, sigma, m0, beta, tau, steps, mpi=None):
     exe = os.path.join(REF_DIR, f"sm_ref_{nx}x{nt}")
     S = nx * nt
@@ -152,7 +202,18 @@ def main():
     ap.add_argument("--large-workdir", default=None, help="reuse an existing reference run directory")
     ap.add_argument("--mpirun", default="/opt/conda/bin/mpirun")
     ap.add_argument("--md-only", action="store_true", help="regenerate only the MD fixtures")
+    ap.add_argument("--hmc-stat", action="store_true", help="(re)run the reference HMC program (~2 min)")
+    ap.add_argument("--hmc-log-dir", default=None, help="reuse a finished reference HMC run directory")
     args = ap.parse_args()
+    if args.hmc_stat:
+        path = os.path.join(HERE, "manifest.json")
+        with open(path) as f:
+            manifest = json.load(f)
+        manifest["hmc_stat"] = make_hmc_stat(args.hmc_log_dir)
+        print(json.dumps(manifest["hmc_stat"]), file=sys.stderr)
+        with open(path, "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+        return
     if args.md_only:
         sizes = sorted({f"{nx}x{nt}" for _, nx, nt, *_ in MD_FIXTURES})
         subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref", "oracle",
@@ -167,6 +228,7 @@ def main():
             print(name, json.dumps(manifest["md"][name]), file=sys.stderr)
         manifest["md_params"] = {"seed_P": SEED_P, "P": "numpy default_rng(seed_P).standard_normal(2S)",
                                  "cg": {"tol": 1e-10, "max_iter": 10000}}
+        manifest["jackknife"] = make_jackknife()
         with open(path, "w") as f:
             json.dump(manifest, f, indent=1, sort_keys=True)
         return
@@ -210,6 +272,7 @@ def main():
                                        args.mpirun if args.mpi else None)
     manifest["md_params"] = {"seed_P": SEED_P, "P": "numpy default_rng(seed_P).standard_normal(2S)",
                              "cg": {"tol": 1e-10, "max_iter": 10000}}
+    manifest["jackknife"] = make_jackknife()
     if args.large:
         subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref", "REF_SIZES=1024x1024"], check=True)
         manifest["large"] = {}

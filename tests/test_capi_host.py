@@ -119,7 +119,8 @@ def test_struct_layouts_match_header(tmp_path):
     """The ctypes mirrors of the ABI structs have the C header's size and offsets."""
     import schwingermodel_amd._lib as L
     structs = {"sm_cg_result": L.CGResult, "sm_hmc_params": L.HMCParams,
-               "sm_hamiltonian_terms": L.HamiltonianTerms, "sm_hmc_result": L.HMCResult}
+               "sm_hamiltonian_terms": L.HamiltonianTerms, "sm_hmc_result": L.HMCResult,
+               "sm_hmc_summary": L.HMCSummary}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "sm_hip.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
@@ -136,3 +137,16 @@ def test_struct_layouts_match_header(tmp_path):
         assert got[(cname, "size")] == ctypes.sizeof(py), cname
         for fname, _ in py._fields_:
             assert got[(cname, fname)] == getattr(py, fname).offset, (cname, fname)
+
+
+def test_jackknife_matches_reference():
+    """sm_jackknife_error == the reference's Jackknife_error(dat, 20) bit for bit
+    (golden values from src/statistics.cpp via make_golden.py), including its
+    integer binning for series shorter than / not a multiple of 20."""
+    import json
+    with open(os.path.join(REPO, "tests", "golden", "manifest.json")) as f:
+        cases = json.load(f)["jackknife"]
+    for c in cases:
+        d = np.array(c["data"])
+        got = sm.lib.sm_jackknife_error(d.ctypes.data, len(d), c["bin"])
+        assert got == c["jackknife_error"], (len(d), got, c["jackknife_error"])

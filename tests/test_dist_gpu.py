@@ -32,3 +32,28 @@ def test_sharded_gpu_path_matches_reference(tmp_path, fixture, world):
     assert len(set(rep["cg_iters"])) == 1 and abs(rep["cg_iters"][0] - ref) <= max(1, ref // 100)
     assert all(rep["cg_converged"])
     assert len({tuple(d) for d in rep["dots"]}) == 1  # identical global dot on every shard
+
+
+@pytest.mark.parametrize("fixture,world", [("md16x16_hot_m0", 2), ("md32x48_b3_m0p1", 4), ("md64x64_b2_m0", 2)])
+def test_sharded_md_matches_reference(tmp_path, fixture, world):
+    """MD layer on t-shards: bitwise plaquette / staples / gauge force, the
+    CG-dependent MD force, leapfrog and Hamiltonians within the test_md_gpu
+    tolerances, and an HMC trajectory equal to the one-shard trajectory."""
+    rep = run_world("md", fixture, world, tmp_path, timeout=900)
+    c = rep["checks"]
+    for k in ("ref_plaq", "ref_staple", "ref_gforce"):
+        assert c[k] is True, (k, c)
+    for k in ("ref_mdforce", "ref_U1", "ref_P1"):
+        assert c[k] <= 1e-8, (k, c)
+    m = rep["meta"]
+    assert len({tuple(s) for s in rep["sums"]}) == 1  # every shard has the global sums
+    sp, act = rep["sums"][0]
+    assert abs(sp - m["sp"]) <= 1e-12 * max(1.0, abs(m["sp"])) and abs(act - m["gauge_action"]) <= 1e-12 * m["gauge_action"]
+    for key in ("H0", "H1"):
+        assert len(set(rep[key])) == 1 and abs(rep[key][0] - m[key]) <= 1e-10 * abs(m[key])
+    t = rep["traj"]
+    assert len({tuple(x) for x in t["sharded"]}) == 1
+    dH, acc, r = t["sharded"][0]
+    assert abs(dH - t["single"][0]) <= 1e-6 * max(1.0, abs(t["single"][0]))
+    assert acc == t["single"][1] and r == t["single"][2]
+    assert t["U_rel"] <= 1e-8

@@ -1,0 +1,104 @@
+"""The HMC driver on the device: sm_hmc_run and the
+`sm_hmc` program (the reference's src/main.cpp over libsm_hip.so).
+
+The reference seeds its RNG from the clock, so parity of a Markov chain is
+statistical: the same physics parameters as a recorded run of the unmodified
+reference program (tests/golden/manifest.json "hmc_stat", make_golden.py
+--hmc-stat) must give the average plaquette and gauge action within their
+combined jackknife errors (4 sigma) and a similar acceptance rate. Everything
+else is checked exactly: the summary statistics against a restatement over
+the returned series, the trajectory count, and the configuration files.
+"""
+import ctypes
+import json
+import math
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, REPO, ptr
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sm():
+    import schwingermodel_amd
+    return schwingermodel_amd
+
+
+@pytest.fixture(scope="module")
+def ref():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return json.load(f)["hmc_stat"]
+
+
+def seq_mean(x):
+    s = 0.0
+    for v in x:
+        s += v
+    return s / len(x)
+
+
+def test_hmc_run_matches_reference_statistics(sm, ref):
+    N, Nt = ref["Nx"], ref["Nt"]
+    V = N * Nt
+    L = sm.Lattice(N, Nt)
+    p = sm.HMCParams(ref["m0"], ref["beta"], ref["tau"], ref["md_steps"], 1e-10, 10000, 20261015)
+    s = sm.HMCSummary()
+    n = ref["Nmeas"]
+    sp, gs = np.empty(n), np.empty(n)
+    sm.check(sm.lib.sm_hmc_run(L.ctx, ctypes.byref(p), 1, 0, ref["Ntherm"], n, ref["Nsteps"], None, ctypes.byref(s),
+                               ptr(sp), ptr(gs)))
+    L.close()
+    assert s.cg_failures == 0
+    assert s.trajectories == ref["Ntherm"] + n + ref["Nsteps"] * (n - 1)
+    # summary = the reference's statistics over the measured series
+    assert s.Ep == seq_mean(sp) / V
+    assert s.dEp == sm.lib.sm_jackknife_error(sp.ctypes.data, n, 20) / V
+    assert s.gS == seq_mean(gs) / V
+    assert abs(s.gS - ref["beta"] * (1.0 - s.Ep)) <= 1e-12  # S_G = beta sum (1 - Re U_01)
+    assert s.acceptance == s.accepted / (n + ref["Nsteps"] * (n - 1))
+    # statistical parity with the reference program
+    sig = math.hypot(s.dEp, ref["dEp"])
+    assert abs(s.Ep - ref["Ep"]) <= 4 * sig + 1e-3, (s.Ep, s.dEp, ref["Ep"], ref["dEp"])
+    sig = math.hypot(s.dgS, ref["dgS"])
+    assert abs(s.gS - ref["gS"]) <= 4 * sig + 2e-3, (s.gS, ref["gS"])
+    assert abs(s.acceptance - ref["acceptance"]) <= 0.15, (s.acceptance, ref["acceptance"])
+
+
+def test_sm_hmc_program(tmp_path, sm):
+    """The CLI: reference stdin, banner/results, SimData file, saved confs."""
+    exe = os.path.join(REPO, "schwingermodel_amd", "sm_hmc")
+    if not os.path.exists(exe):
+        pytest.fail("schwingermodel_amd/sm_hmc not built (build_cli needs MPI under /opt/conda)")
+    N, Nmeas = 32, 6
+    params = f"1\n1\n0.1\n6\n0.5\n2\n3\n{Nmeas}\n1\n1\n"
+    env = dict(os.environ, HOSTNAME="box")
+    r = subprocess.run([exe, str(N), str(N), "77"], input=params, capture_output=True, text=True, cwd=tmp_path,
+                       env=env, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    ep = float(re.search(r"Ep = (\S+) dEp", r.stdout).group(1))
+    assert "Acceptance rate:" in r.stdout and "Execution time" in r.stdout
+    sim = tmp_path / f"2D_U1_{N}x{N}_m00.10000000000000001_SimData.txt"
+    assert sim.exists(), os.listdir(tmp_path)
+    assert "#Ep" in sim.read_text()
+    confs = sorted(tmp_path.glob(f"2D_U1_Ns{N}_Nt{N}_b20000_m01000_*.ctxt"))
+    assert len(confs) == Nmeas
+    S = N * N
+    L = sm.Lattice(N, N)
+    sps = []
+    for c in confs:
+        assert c.stat().st_size == S * 2 * 28
+        U = np.empty(4 * S)
+        sm.check(sm.lib.sm_conf_read(str(c).encode(), N, N, ptr(U[:2 * S]), ptr(U[2 * S:])))
+        sm.check(sm.lib.sm_upload_gauge(L.ctx, ptr(U[:2 * S]), ptr(U[2 * S:])))
+        sp, act = ctypes.c_double(), ctypes.c_double()
+        sm.check(sm.lib.sm_plaquette(L.ctx, 2.0, ctypes.byref(sp), ctypes.byref(act), None))
+        sps.append(sp.value)
+    L.close()
+    # the printed Ep (6 significant digits) is the mean plaquette of the saved confs
+    assert abs(np.mean(sps) / S - ep) <= 1e-5 * abs(ep)
