@@ -7,9 +7,13 @@ config 2: 1024^2, beta=3 field (sigma 0.3246), m0=-0.10, CG to 1e-10
 config 3: 4096^2, beta=5 field (sigma 0.2374), m0=-0.06, CG to 1e-10
 config 5: 8192^2, beta=2 field (sigma 0.4242), m0=-0.19 (near m_crit), CG to 1e-10,
           here on ONE GPU (8 GiB per field fits the 288 GB HBM)
---hmc:    config 1, the reference HMC program (64^2, beta=2, m0=0, 10 MD steps)
-          on the GPU through the drop-in shim vs the unmodified CPU reference,
-          same stdin parameters (oracle/_ref/SM_64x64_hip vs SM_64x64_ref).
+--hmc:    config 1 (64^2, beta=2, m0=0, 10 MD steps) with the parameters of the
+          recorded reference run (manifest "hmc_stat": 50 + 100 + 99 trajectories):
+          `sm_hmc` (whole HMC on the device), the reference program with its
+          D/CG on the GPU through the drop-in shim (oracle/_ref/SM_64x64_hip),
+          and with --hmc-ref the unmodified CPU reference (SM_64x64_ref, ~4 min).
+--hmc-large N: seconds per device HMC trajectory at N^2 (beta=3 field start,
+          m0=0.10, tau=0.5, 10 MD steps), the MD step at production size.
 Inputs are resident in HBM before timing; the solve includes sm_cg_begin
 (x0 = phi, r0, norms) and the final x update, like conjugate_gradient().
 """
@@ -85,33 +89,71 @@ def run_config(cid, tol=1e-10):
     return out
 
 
-def run_hmc():
-    params = "1\n1\n0\n10\n1\n2\n10\n20\n0\n0\n"  # rx rt m0 MD tau beta Ntherm Nmeas Nsteps save
-    out = {"config": 1, "lattice": "64x64", "params": "m0=0 MD=10 tau=1 beta=2 Ntherm=10 Nmeas=20 Nsteps=0"}
-    for tag in ("hip", "ref"):
-        exe = os.path.join(REPO, "oracle", "_ref", f"SM_64x64_{tag}")
-        if not os.path.exists(exe):
+def run_hmc(with_ref=False):
+    import re
+    import tempfile
+    with open(os.path.join(REPO, "tests", "golden", "manifest.json")) as f:
+        c = json.load(f)["hmc_stat"]
+    params = (f"1\n1\n{c['m0']}\n{c['md_steps']}\n{c['tau']}\n{c['beta']}\n{c['Ntherm']}\n{c['Nmeas']}\n"
+              f"{c['Nsteps']}\n0\n")
+    ntraj = c["Ntherm"] + c["Nmeas"] + c["Nsteps"] * (c["Nmeas"] - 1)
+    out = {"config": 1, "lattice": "64x64", "trajectories": ntraj,
+           "params": {k: c[k] for k in ("m0", "md_steps", "tau", "beta", "Ntherm", "Nmeas", "Nsteps")},
+           "reference_recorded": {k: c[k] for k in ("Ep", "dEp", "acceptance", "seconds")}}
+    progs = {"sm_hmc": [os.path.join(REPO, "schwingermodel_amd", "sm_hmc"), "64", "64", "1"],
+             "dropin_shim": [os.path.join(REPO, "oracle", "_ref", "SM_64x64_hip")]}
+    if with_ref:
+        progs["reference_cpu"] = [os.path.join(REPO, "oracle", "_ref", "SM_64x64_ref")]
+    env = dict(os.environ, HOSTNAME=os.environ.get("HOSTNAME", "box"))
+    for tag, cmd in progs.items():
+        if not os.path.exists(cmd[0]):
             out[tag] = None
             continue
-        env = dict(os.environ, HOSTNAME=os.environ.get("HOSTNAME", "box"))
-        with __import__("tempfile").TemporaryDirectory() as d:
+        with tempfile.TemporaryDirectory() as d:
             t = time.perf_counter()
-            r = subprocess.run([exe], input=params, capture_output=True, text=True, env=env, cwd=d, timeout=900)
+            r = subprocess.run(cmd, input=params, capture_output=True, text=True, env=env, cwd=d, timeout=1200)
             dt = time.perf_counter() - t
-        line = [ln for ln in r.stdout.splitlines() if "Execution time" in ln]
-        out[tag] = {"wall_s": round(dt, 2), "reported": line[-1] if line else r.stderr[-300:]}
+        ep = re.search(r"Ep = (\S+) dEp = (\S+)", r.stdout)
+        acc = re.search(r"Acceptance rate: (\S+)", r.stdout)
+        rep = re.search(r"Execution time = (\S+) s", r.stdout)
+        out[tag] = {"wall_s": round(dt, 2), "hmc_s": float(rep.group(1)) if rep else None,
+                    "Ep": float(ep.group(1)) if ep else None, "dEp": float(ep.group(2)) if ep else None,
+                    "acceptance_stdout": float(acc.group(1)) if acc else None,
+                    "rc": r.returncode, "err": r.stderr[-300:] if r.returncode else ""}
     return out
+
+
+def run_hmc_large(N, ntraj=3):
+    import ctypes
+    import schwingermodel_amd as sm
+    L = sm.Lattice(N, N)
+    sm.check(sm.lib.sm_fill_gauge_dev(L.ctx, 4321, 0.3246))
+    p = sm.HMCParams(0.10, 3.0, 0.5, 10, 1e-10, 10000, 7)
+    rows = []
+    for traj in range(ntraj):
+        r = sm.HMCResult()
+        t = time.perf_counter()
+        sm.check(sm.lib.sm_hmc_trajectory(L.ctx, ctypes.byref(p), traj, ctypes.byref(r)))
+        dt = time.perf_counter() - t
+        rows.append({"traj": traj, "seconds": round(dt, 3), "cg_iterations": r.cg_iterations, "dH": r.dH,
+                     "accepted": r.accepted, "ms_per_cg_it": round(1e3 * dt / max(1, r.cg_iterations), 4)})
+    L.close()
+    return {"hmc_large": f"{N}x{N}", "beta": 3.0, "m0": 0.10, "tau": 0.5, "md_steps": 10, "trajectories": rows}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="2,3,5")
     ap.add_argument("--hmc", action="store_true")
+    ap.add_argument("--hmc-ref", action="store_true", help="with --hmc: also the CPU reference (~4 min)")
+    ap.add_argument("--hmc-large", type=int, default=0)
     a = ap.parse_args()
     for cid in [int(v) for v in a.configs.split(",") if v]:
         print(json.dumps(run_config(cid)), flush=True)
     if a.hmc:
-        print(json.dumps(run_hmc()), flush=True)
+        print(json.dumps(run_hmc(a.hmc_ref)), flush=True)
+    if a.hmc_large:
+        print(json.dumps(run_hmc_large(a.hmc_large)), flush=True)
 
 
 if __name__ == "__main__":
