@@ -114,10 +114,12 @@ int sm_synchronize(sm_ctx *ctx);
  * variant selects the stencil code variant. Values <= 0 (< 0 for xcd_remap
  * and variant) keep the current setting. */
 int sm_tune(sm_ctx *ctx, int bt, int xchunk, int xcd_remap, int variant);
-/* CG path: fused = 1 runs an iteration in two HBM passes (sm_cgfused.hip)
- * each followed by a one-block scalar kernel (alpha, beta; the default),
- * 2 the same two passes with alpha and beta reduced in-kernel by the last
- * block of each pass (one shard only), 0 the six-kernel
+/* CG path: fused = 3 (the default) runs an iteration in ONE HBM pass: the
+ * residual update r -= alpha Ad is folded into the next pass, beta comes from
+ * that pass's direct dots (sm_cgfused.hip). 1 runs two passes each followed
+ * by a one-block scalar kernel (alpha, beta), 2 the same two passes with
+ * alpha and beta reduced in-kernel by the last block of each pass (one shard
+ * only), 0 the six-kernel
  * sequence; xchunk = rows per block of the fused kernel. < 0 / <= 0 keep. */
 int sm_tune_cg(sm_ctx *ctx, int fused, int xchunk);
 /* Streaming-bandwidth ceiling on the ctx stream (measured roofline reference):

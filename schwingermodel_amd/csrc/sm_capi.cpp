@@ -187,8 +187,11 @@ int download_plane_pair(sm_ctx *c, const double2 *src, double *p0, double *p1) {
 }
 
 // 2-deep faces of the fused CG kernel: 4 columns [-2,-1,Wt,Wt+1][plane][x].
-double2 *face2_recv(sm_ctx *c, int which) {  // 0: d, 1: r, 2: U
-    return c->faces2 + (size_t)(16 + 8 * which) * c->g.Nx;
+// faces2 layout (complex, units of Nx): send slots of up to 3 fields at 8f
+// (lo 4Nx, hi 4Nx), then receive slots at 24 + 8*which (which 0: d, 1: r,
+// 2: U, 3: Ad), 56 Nx in all.
+double2 *face2_recv(sm_ctx *c, int which) {  // 0: d, 1: r, 2: U, 3: Ad
+    return c->faces2 + (size_t)(24 + 8 * which) * c->g.Nx;
 }
 double2 *face2_send(sm_ctx *c, int f, int hi) {  // send buffers of field slot f
     return c->faces2 + (size_t)(8 * f + 4 * hi) * c->g.Nx;
@@ -364,7 +367,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     chk(hipMalloc(&c->ghostU, sizeof(double2) * (size_t)Nx));
     chk(hipMalloc(&c->fields, fb * NFIELDS));
     chk(hipMalloc(&c->faces, sizeof(double2) * 2 * (size_t)Nx * 8));
-    chk(hipMalloc(&c->faces2, sizeof(double2) * 40 * (size_t)Nx));
+    chk(hipMalloc(&c->faces2, sizeof(double2) * 56 * (size_t)Nx));
     chk(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
     chk(hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming));
     chk(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
@@ -435,16 +438,16 @@ int sm_destroy(sm_ctx *c) {
 
 int sm_tune_cg(sm_ctx *c, int fused, int xchunk) {
     if (!c) return fail(SM_ERR_ARG, "null context");
-    if (fused > 2) return fail(SM_ERR_ARG, "fused must be 0, 1 or 2");
+    if (fused > 3) return fail(SM_ERR_ARG, "fused must be 0, 1, 2 or 3");
     if (fused >= 0) {
-        c->cg_fused = fused != 0;
+        c->cg_fused = fused == 3 ? 3 : (fused != 0);
         c->cg_inkernel = fused == 2;
     }
     if (xchunk > 0) {
         CGFusedCfg f = c->fcfg;
         f.xchunk = xchunk;
         f.XB = (c->g.Nx + xchunk - 1) / xchunk;
-        if (cg_fused_blocks(f) > kMaxPartials) return fail(SM_ERR_ARG, "too many blocks");
+        if (3 * cg_fused_blocks(f) > 2 * kMaxPartials) return fail(SM_ERR_ARG, "too many blocks");
         c->fcfg = f;
     }
     return SM_OK;
@@ -591,6 +594,60 @@ static int cg_scalar(sm_ctx *c, int nparts, int which) {
     return SM_OK;
 }
 
+// One pass of the one-pass CG (sm_cgfused.hip: cg_onepass_kernel): pass j
+// reads the j-1 fields (d, r, Ad), writes the j fields into the other
+// buffers, updates x in place, then the scalar kernel forms err / stop,
+// alpha_j and beta_j.
+static int cg_onepass(sm_ctx *c) {
+    const long j = c->cg_issued;
+    const bool odd = j & 1, first = j == 0;
+    double2 *dold = c->field(odd ? F_D2 : F_D), *dnew = c->field(odd ? F_D : F_D2);
+    double2 *rold = c->field(odd ? F_R2 : F_R), *rnew = c->field(odd ? F_R : F_R2);
+    double2 *aold = c->field(odd ? F_AD2 : F_AD), *anew = c->field(odd ? F_AD : F_AD2);
+    const CGFusedCfg &fc = c->fcfg;
+    auto pass = [&](int tb0, int tbn) {
+        launch_cg_onepass(c->stream, c->g, fc, c->nshard, dold, rold, aold, dnew, rnew, anew, c->cg_x, c->U,
+                          face2_recv(c, 0), face2_recv(c, 1), face2_recv(c, 3), face2_recv(c, 2), c->cg_mass,
+                          first, c->sc, c->partials, tb0, tbn);
+    };
+    const int nparts = cg_fused_blocks(fc);
+    if (c->nshard == 1) {
+        pass(0, fc.TBk);
+        launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
+        return SM_OK;
+    }
+    // interior t-blocks while the 2-deep faces of d, r, Ad travel (one round)
+    const double2 *flds[3] = {dold, rold, aold};
+    double2 *fcs[3] = {face2_recv(c, 0), face2_recv(c, 1), face2_recv(c, 3)};
+    auto interior = [&](int tb) {
+        const int g_lo = 4 * tb, g_hi = std::min(4 * tb + 3, fc.NWT - 1);
+        return kFusedWaveCols * g_lo - 2 >= 0 && kFusedWaveCols * g_hi + kFusedWaveCols + 1 <= c->g.Wt - 1;
+    };
+    int tb_lo = 0, tb_hi = -1;
+    for (int tb = 0; tb < fc.TBk; ++tb)
+        if (interior(tb)) {
+            if (tb_hi < 0) tb_lo = tb;
+            tb_hi = tb;
+        }
+    const bool split = tb_hi >= tb_lo && tb_hi >= 0;
+    HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
+    HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
+    TRY(halo2_multi(c, c->comm_stream, flds, fcs, 3));
+    HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
+    if (split) pass(tb_lo, tb_hi - tb_lo + 1);
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+    if (split) {
+        pass(0, tb_lo);
+        pass(tb_hi + 1, fc.TBk - tb_hi - 1);
+    } else {
+        pass(0, fc.TBk);
+    }
+    launch_cg1_local_sum(c->stream, nparts, c->partials, c->sc);
+    TRY(allreduce_dev(c, (double *)c->sc->sum3, 6));
+    launch_cg1_from_sums(c->stream, c->sc, first);
+    return SM_OK;
+}
+
 int sm_cg_iterate(sm_ctx *c, int niter) {
     TRY(check_ready(c));
     if (!c->cg_active) return fail(SM_ERR_STATE, "sm_cg_iterate before sm_cg_begin");
@@ -598,7 +655,9 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
     double2 *r = c->field(F_R), *Ad = c->field(F_AD), *t = c->field(F_T);
     double2 *x = c->cg_x;
     for (int i = 0; i < niter; ++i) {
-        if (c->cg_fused) {
+        if (c->cg_fused == 3) {
+            TRY(cg_onepass(c));
+        } else if (c->cg_fused) {
             // pass 1: d_k, deferred x update, Ad = D D^dag d_k, <d_k, Ad>
             double2 *dold = c->field((c->cg_issued & 1) ? F_D2 : F_D);
             double2 *dnew = c->field((c->cg_issued & 1) ? F_D : F_D2);
@@ -696,9 +755,16 @@ int sm_cg_dev(sm_ctx *c, const double *phi, double *x, double m0, double tol, in
     TRY(sm_cg_begin(c, phi, x, m0, tol));
     // Enqueue iterations in chunks; each CG kernel is a no-op once the device
     // flag `done` is set, so overshooting a chunk costs only empty launches.
+    // The one-pass path runs max_iter + 1 passes (pass 0 forms Ad_0) and stops
+    // itself at k == max_iter.
+    int passes = max_iter;
+    if (c->cg_fused == 3) {
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)&c->sc->max_iter, max_iter, 1, c->stream));
+        passes = max_iter + 1;
+    }
     int issued = 0, chunk = 4;
-    while (issued < max_iter) {
-        const int nb = (max_iter - issued) < chunk ? (max_iter - issued) : chunk;
+    while (issued < passes) {
+        const int nb = (passes - issued) < chunk ? (passes - issued) : chunk;
         TRY(sm_cg_iterate(c, nb));
         issued += nb;
         TRY(sm_cg_status(c, res));

@@ -230,6 +230,332 @@ __global__ void __launch_bounds__(256) cg_fused_kernel(CGFArgs a) {
     }
 }
 
+// ---- one-pass CG iteration (pass 2 folded into the next pass 1) ----------------
+// Pass j (j >= 1), every per-element operation the reference's:
+//     r_j  = r_{j-1} - alpha_{j-1} Ad_{j-1}          (src/conjugate_gradient.cpp:38-39)
+//     d_j  = d_{j-1} beta_{j-1} + r_j                (:55-58)
+//     x_j  = x_{j-1} + alpha_{j-1} d_{j-1}           (:36-37)
+//     Ad_j = D D^dag d_j ; partials of <d_j,Ad_j>, <r_j,Ad_j>, |r_j|^2, |Ad_j|^2
+// Then (cg1_scalar_kernel): err = sqrt|r_j|^2 (direct, as the reference) and its
+// stop test; alpha_j = |r_j|^2 / <d_j,Ad_j>; and beta_j from the expansion
+//     |r_{j+1}|^2 = |r_j|^2 - 2 Re(conj(alpha_j) <r_j,Ad_j>) + |alpha_j|^2 |Ad_j|^2
+// of the pass's own direct dots (no conjugacy assumed), so r_{j+1} never has
+// to be written before d_{j+1} is formed. Pass 0 only forms Ad_0 (d_0 = r_0).
+// r, d and Ad ping-pong (halo lanes / rows of neighbouring tiles read the
+// j-1 fields while owners write the j fields).
+// HBM bytes per site and iteration: read d, r, Ad, x, U (160), write d, r, Ad,
+// x (128) = 288, against 320 for the two-pass iteration and 576 for the
+// reference's sequence.
+struct CG1Args {
+    const double2 *dold, *rold, *aold;
+    double2 *dnew, *rnew, *anew;
+    double2 *x;
+    const double2 *U;
+    const double2 *fd, *fr, *fa, *fU;  // nshard > 1: 4-column faces
+    CGScalars *sc;
+    double2 *partials;                 // 3 per block: <d,Ad>, <r,Ad>, (|r|^2, |Ad|^2)
+    long V;
+    int Nx, Wt, t0, Ntg, nshard;
+    int xchunk, NWT, TBk, XB, remap, first;
+    int tb0, tbn, part0;
+    double mass;
+};
+
+struct Raw3 {
+    double2 d0, d1, r0, r1, a0, a1, ut, ux, x0, x1;
+};
+
+__device__ __forceinline__ CSrc csrc1(const double2 *base, const double2 *face, int c, const CG1Args &a) {
+    CSrc s;
+    if (c >= 0 && c < a.Wt) {
+        s.p = base + c;
+        s.xs = a.Wt;
+        s.ps = a.V;
+    } else if (a.nshard == 1) {
+        int cw = c % a.Wt;
+        if (cw < 0) cw += a.Wt;
+        s.p = base + cw;
+        s.xs = a.Wt;
+        s.ps = a.V;
+    } else {
+        int fc = c < 0 ? c + 2 : c - a.Wt + 2;
+        fc = fc < 0 ? 0 : (fc > 3 ? 3 : fc);
+        s.p = face + (long)fc * 2 * a.Nx;
+        s.xs = 1;
+        s.ps = a.Nx;
+    }
+    return s;
+}
+
+__global__ void __launch_bounds__(256) cg_onepass_kernel(CG1Args a) {
+    __shared__ double2 sh[4];
+    CGScalars *sc = a.sc;
+    if (sc->done) return;  // grid-uniform: converged (or max_iter) in an earlier pass
+    const double2 alpha = sc->alpha, beta = sc->beta;  // alpha_{j-1}, beta_{j-1}
+    int tb, xc;
+    {
+        int w = blockIdx.x;
+        if (a.remap) {
+            const int n = a.tbn * a.XB, q = n >> 3, rr = n & 7, xcd = w & 7;
+            w = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (w >> 3);
+        }
+        tb = a.tb0 + w % a.tbn;
+        xc = w / a.tbn;
+    }
+    const int lane = threadIdx.x & 63;
+    const int g = tb * 4 + (threadIdx.x >> 6);
+    const int x0 = xc * a.xchunk;
+    const int xe = min(a.Nx, x0 + a.xchunk);
+    double2 acc_dA = make_double2(0.0, 0.0), acc_rA = make_double2(0.0, 0.0);
+    double2 acc_n = make_double2(0.0, 0.0);  // (|r|^2, |Ad|^2)
+    if (g < a.NWT && x0 < xe) {
+        const int Nx = a.Nx, Wt = a.Wt;
+        const int c = g * FW - 2 + lane;
+        const bool own = lane >= 2 && lane < FW + 2 && c < Wt;
+        int tg = (a.t0 + c) % a.Ntg;
+        if (tg < 0) tg += a.Ntg;
+        const double sr0 = tg == a.Ntg - 1 ? -1.0 : 1.0;
+        const double sl0 = tg == 0 ? -1.0 : 1.0;
+        const CSrc Sd = csrc1(a.dold, a.fd, c, a), Sr = csrc1(a.rold, a.fr, c, a);
+        const CSrc Sa = csrc1(a.aold, a.fa, c, a), Su = csrc1(a.U, a.fU, c, a);
+        const int cx = c < 0 ? 0 : (c >= Wt ? Wt - 1 : c);
+        const bool first = a.first != 0;
+        auto wrap = [Nx](int x) { int w = x % Nx; return w < 0 ? w + Nx : w; };
+        auto load = [&](int xr, Raw3 &R) {
+            const long pr = (long)wrap(xr);
+            const double2 *pd = Sd.p + pr * Sd.xs, *pq = Sr.p + pr * Sr.xs, *pa = Sa.p + pr * Sa.xs;
+            R.d0 = pd[0];
+            R.d1 = pd[Sd.ps];
+            R.r0 = pq[0];
+            R.r1 = pq[Sr.ps];
+            R.a0 = pa[0];
+            R.a1 = pa[Sa.ps];
+            const double2 *pu = Su.p + (long)wrap(min(xr, xe)) * Su.xs;
+            R.ut = pu[0];
+            R.ux = pu[Su.ps];
+            const long nx = (long)wrap(min(max(xr, x0), xe - 1)) * Wt + cx;
+            R.x0 = a.x[nx];
+            R.x1 = a.x[nx + a.V];
+        };
+        // r_j and d_j of row xr; on owned rows store r_j, d_j, x_j, add |r_j|^2
+        auto form = [&](int xr, const Raw3 &R, Sp &rj) {
+            rj.a = first ? R.r0 : csub(R.r0, cmul(alpha, R.a0));
+            rj.b = first ? R.r1 : csub(R.r1, cmul(alpha, R.a1));
+            Sp d;
+            d.a = first ? R.d0 : cadd(cmul(R.d0, beta), rj.a);
+            d.b = first ? R.d1 : cadd(cmul(R.d1, beta), rj.b);
+            if (xr >= x0 && xr < xe && own) {
+                const long n = (long)xr * Wt + c;
+                st_nt(a.rnew + n, rj.a);
+                st_nt(a.rnew + n + a.V, rj.b);
+                st_nt(a.dnew + n, d.a);
+                st_nt(a.dnew + n + a.V, d.b);
+                if (!first) {
+                    st_nt(a.x + n, cadd(R.x0, cmul(alpha, R.d0)));
+                    st_nt(a.x + n + a.V, cadd(R.x1, cmul(alpha, R.d1)));
+                }
+                acc_n.x += cmul(rj.a, cconj(rj.a)).x;  // Re dot(r, r), include/variables.h:185-188
+                acc_n.x += cmul(rj.b, cconj(rj.b)).x;
+            }
+            return d;
+        };
+        auto ddag = [&](const Sp &p, const Sp &pxm, const Sp &pxp, double2 ut, double2 ux, double2 uxm,
+                        double2 &utm_out) {
+            const Sp pm = shr(p), pp = shl(p);
+            utm_out = dpp_shr1(ut);
+            Sp o;
+            dirac_site<1>(a.mass, sr0, sl0, p.a, p.b, pp.a, pp.b, pxp.a, pxp.b, pm.a, pm.b, pxm.a, pxm.b, ut, ux,
+                          utm_out, uxm, o.a, o.b);
+            return o;
+        };
+        Raw3 R;
+        Sp rj;
+        load(x0 - 2, R);
+        Sp dm2 = form(x0 - 2, R, rj);
+        double2 uxm2 = R.ux;
+        load(x0 - 1, R);
+        Sp dm1 = form(x0 - 1, R, rj);
+        double2 utm1 = R.ut, uxm1 = R.ux;
+        load(x0, R);
+        Sp rc;
+        Sp dc = form(x0, R, rc);
+        double2 utc = R.ut, uxc = R.ux;
+        load(x0 + 1, R);
+        Sp rn;
+        Sp dn = form(x0 + 1, R, rn);
+        double2 utn = R.ut, uxn = R.ux;
+        load(x0 + 2, R);
+        double2 dummy;
+        Sp Tp = ddag(dm1, dm2, dc, utm1, uxm1, uxm2, dummy);
+        double2 utmc;
+        Sp Tc = ddag(dc, dm1, dn, utc, uxc, uxm1, utmc);
+        double2 uxp = uxm1;
+        for (int x = x0; x < xe; ++x) {
+            Sp r2;
+            const Sp d2 = form(x + 2, R, r2);
+            const double2 ut2 = R.ut, ux2 = R.ux;
+            load(min(x + 3, xe + 1), R);
+            __builtin_amdgcn_sched_barrier(0);
+            double2 utmn;
+            const Sp Tn = ddag(dn, dc, d2, utn, uxn, uxc, utmn);
+            const Sp Tm = shr(Tc), Tq = shl(Tc);
+            Sp o;
+            dirac_site<0>(a.mass, sr0, sl0, Tc.a, Tc.b, Tq.a, Tq.b, Tn.a, Tn.b, Tm.a, Tm.b, Tp.a, Tp.b, utc, uxc,
+                          utmc, uxp, o.a, o.b);
+            if (own) {
+                const long n = (long)x * Wt + c;
+                st_nt(a.anew + n, o.a);
+                st_nt(a.anew + n + a.V, o.b);
+                acc_dA = cadd(acc_dA, cmul(dc.a, cconj(o.a)));  // dot(d, Ad)
+                acc_dA = cadd(acc_dA, cmul(dc.b, cconj(o.b)));
+                acc_rA = cadd(acc_rA, cmul(rc.a, cconj(o.a)));  // dot(r, Ad)
+                acc_rA = cadd(acc_rA, cmul(rc.b, cconj(o.b)));
+                acc_n.y += cmul(o.a, cconj(o.a)).x;            // |Ad|^2
+                acc_n.y += cmul(o.b, cconj(o.b)).x;
+            }
+            Tp = Tc;
+            Tc = Tn;
+            dc = dn;
+            dn = d2;
+            rc = rn;
+            rn = r2;
+            uxp = uxc;
+            utc = utn;
+            uxc = uxn;
+            utmc = utmn;
+            utn = ut2;
+            uxn = ux2;
+        }
+    }
+    const double2 s0 = block_sum(acc_dA, sh);
+    __syncthreads();
+    const double2 s1 = block_sum(acc_rA, sh);
+    __syncthreads();
+    const double2 s2 = block_sum(acc_n, sh);
+    if (threadIdx.x == 0) {
+        double2 *p = a.partials + 3 * (long)(a.part0 + blockIdx.x);
+        p[0] = s0;
+        p[1] = s1;
+        p[2] = s2;
+    }
+}
+
+// Scalars after pass j: a single block sums the 3*nparts partials in a fixed
+// order (1024 threads, four independent loads in flight per thread).
+constexpr int SB = 1024;
+__device__ void sum3_partials(int nparts, const double2 *part, double2 out[3]) {
+    __shared__ double2 sh[3][SB / 64];
+    double2 acc[3] = {make_double2(0.0, 0.0), make_double2(0.0, 0.0), make_double2(0.0, 0.0)};
+    for (int i = threadIdx.x; i < nparts; i += SB) {
+        const double2 *p = part + 3 * (long)i;
+        const double2 v0 = p[0], v1 = p[1], v2 = p[2];
+        acc[0] = cadd(acc[0], v0);
+        acc[1] = cadd(acc[1], v1);
+        acc[2] = cadd(acc[2], v2);
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        double2 v = acc[q];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            v.x += __shfl_xor(v.x, off);
+            v.y += __shfl_xor(v.y, off);
+        }
+        if (lane == 0) sh[q][wid] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            double2 r = make_double2(0.0, 0.0);
+            for (int w = 0; w < SB / 64; ++w) r = cadd(r, sh[q][w]);
+            out[q] = r;
+        }
+}
+
+// From the three global sums: stop test on the direct |r_j|^2 (j >= 1), then
+// alpha_j and beta_j (src/conjugate_gradient.cpp:33, 43-61).
+__device__ __attribute__((noinline)) void cg1_scalars(CGScalars *sc, int first, double2 dA, double2 rA, double2 nn) {
+    const double rr = nn.x, AA = nn.y;
+    if (!first) {
+        sc->err = sqrt(rr);
+        sc->k += 1;
+        if (sc->err < sc->tol * sc->phi_norm) {
+            sc->done = 1;
+            sc->converged = 1;
+            return;
+        }
+        if (sc->k >= sc->max_iter) {
+            sc->done = 1;
+            return;
+        }
+    }
+    sc->rn = make_double2(rr, 0.0);
+    const double2 al = cdiv(rr, 0.0, dA.x, dA.y);   // r_norm2 / dot(d, Ad)
+    sc->alpha = al;
+    const double est = rr - 2.0 * (al.x * rA.x + al.y * rA.y) + (al.x * al.x + al.y * al.y) * AA;
+    sc->beta = cdiv(est, 0.0, rr, 0.0);             // err^2 / r_norm2
+}
+
+__global__ void __launch_bounds__(SB) cg1_scalar_kernel(int nparts, const double2 *part, CGScalars *sc, int first) {
+    if (sc->done) return;
+    double2 t[3];
+    sum3_partials(nparts, part, t);
+    if (threadIdx.x == 0) cg1_scalars(sc, first, t[0], t[1], t[2]);
+}
+
+// Multi-shard: local sums into sc->sum3 (all-reduced by the host), then the scalars.
+__global__ void __launch_bounds__(SB) cg1_local_sum_kernel(int nparts, const double2 *part, CGScalars *sc) {
+    if (sc->done) return;
+    double2 t[3];
+    sum3_partials(nparts, part, t);
+    if (threadIdx.x == 0) {
+        sc->sum3[0] = t[0];
+        sc->sum3[1] = t[1];
+        sc->sum3[2] = t[2];
+    }
+}
+
+__global__ void cg1_from_sums_kernel(CGScalars *sc, int first) {
+    if (sc->done) return;
+    cg1_scalars(sc, first, sc->sum3[0], sc->sum3[1], sc->sum3[2]);
+}
+
+void launch_cg_onepass(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard,
+                       const double2 *dold, const double2 *rold, const double2 *aold, double2 *dnew,
+                       double2 *rnew, double2 *anew, double2 *x, const double2 *U, const double2 *fd,
+                       const double2 *fr, const double2 *fa, const double2 *fU, double mass, int first,
+                       CGScalars *sc, double2 *partials, int tb0, int tbn) {
+    if (tbn <= 0) return;
+    CG1Args a;
+    a.dold = dold; a.rold = rold; a.aold = aold;
+    a.dnew = dnew; a.rnew = rnew; a.anew = anew;
+    a.x = x; a.U = U;
+    a.fd = fd; a.fr = fr; a.fa = fa; a.fU = fU;
+    a.sc = sc; a.partials = partials;
+    a.V = g.V; a.Nx = g.Nx; a.Wt = g.Wt; a.t0 = g.t0; a.Ntg = g.Ntg; a.nshard = nshard;
+    a.xchunk = c.xchunk; a.NWT = c.NWT; a.TBk = c.TBk; a.XB = c.XB; a.remap = c.remap;
+    a.first = first;
+    a.mass = mass;
+    a.tb0 = tb0;
+    a.tbn = tbn;
+    a.part0 = tb0 * c.XB;
+    hipLaunchKernelGGL(cg_onepass_kernel, dim3(tbn * c.XB), dim3(256), 0, s, a);
+}
+
+void launch_cg1_scalars(hipStream_t s, int nparts, const double2 *partials, CGScalars *sc, int first) {
+    hipLaunchKernelGGL(cg1_scalar_kernel, dim3(1), dim3(SB), 0, s, nparts, partials, sc, first);
+}
+
+void launch_cg1_local_sum(hipStream_t s, int nparts, const double2 *partials, CGScalars *sc) {
+    hipLaunchKernelGGL(cg1_local_sum_kernel, dim3(1), dim3(SB), 0, s, nparts, partials, sc);
+}
+
+void launch_cg1_from_sums(hipStream_t s, CGScalars *sc, int first) {
+    hipLaunchKernelGGL(cg1_from_sums_kernel, dim3(1), dim3(1), 0, s, sc, first);
+}
+
 CGFusedCfg cg_fused_config(const Geometry &g) {
     CGFusedCfg c;
     c.NWT = (g.Wt + FW - 1) / FW;

@@ -41,7 +41,8 @@ int fail(int code, const char *fmt, ...);
 
 
 // Work fields, each 2*V complex (plane mu0 then mu1).
-enum { F_IN, F_OUT, F_TMP, F_X, F_R, F_D, F_D2, F_T, F_AD, F_PHI, F_L, F_RR, NFIELDS };
+// F_R2 / F_AD2: the second r / Ad buffers of the one-pass CG (ping-pong with F_R / F_AD).
+enum { F_IN, F_OUT, F_TMP, F_X, F_R, F_D, F_D2, F_T, F_AD, F_PHI, F_L, F_RR, F_R2, F_AD2, NFIELDS };
 
 struct sm_ctx {
     int device = 0;
@@ -49,7 +50,10 @@ struct sm_ctx {
     sm::Geometry g{};
     sm::LaunchCfg cfg{};
     sm::CGFusedCfg fcfg{};
-    int cg_fused = 1;               // 1: two-pass fused CG iteration (sm_cgfused.hip)
+    // CG iteration: 0 six kernels, 1 two-pass fused (scalar kernels), 2 two-pass
+    // fused with in-kernel scalars, 3 one-pass (sm_cgfused.hip; the default:
+    // 288 B/site, 0.979 vs 1.040 ms per iteration at 4096^2, tools/tune_cg.py)
+    int cg_fused = 3;
     // one shard: alpha/beta by the last block of each pass instead of two
     // one-block kernels. Measured equal at 4096^2 and 19 % slower at 1024^2
     // (every block of a one-wave grid hits the ticket at once), so off by default.
@@ -112,7 +116,7 @@ int global_sum(sm_ctx *c, int nparts, const double2 *part, int slot);
 int check_ready(sm_ctx *c);
 int upload_plane_pair(sm_ctx *c, double2 *dst, const double *p0, const double *p1);
 int download_plane_pair(sm_ctx *c, const double2 *src, double *p0, double *p1);
-double2 *face2_recv(sm_ctx *c, int which);  // 0: d, 1: r, 2: U
+double2 *face2_recv(sm_ctx *c, int which);  // 0: d, 1: r, 2: U, 3: Ad
 int exchange_ghost_U(sm_ctx *c);
 
 }  // namespace sm_host

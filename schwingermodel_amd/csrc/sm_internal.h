@@ -40,7 +40,8 @@ struct CGScalars {
     int k;               // iterations executed
     int done;            // 1 once converged: every later CG kernel is a no-op
     int converged;
-    int pad;
+    int max_iter;        // one-pass path: the device stops itself at k == max_iter
+    double2 sum3[3];     // one-pass path, multi-shard: all-reduced <d,Ad>, <r,Ad>, (|r|^2,|Ad|^2)
 };
 
 enum Epilogue { EPI_NONE = 0, EPI_DOT = 1 };
@@ -102,6 +103,15 @@ void launch_cg_fused(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int 
                      const double2 *U, const double2 *fd, const double2 *fr, const double2 *fU,
                      double mass, int first, CGScalars *sc, double2 *partials, int tb0, int tbn,
                      unsigned *counter);  // counter != null: last block computes alpha
+// One-pass iteration (pass 2 folded into the next pass): partials are 3 per block.
+void launch_cg_onepass(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard,
+                       const double2 *dold, const double2 *rold, const double2 *aold, double2 *dnew,
+                       double2 *rnew, double2 *anew, double2 *x, const double2 *U, const double2 *fd,
+                       const double2 *fr, const double2 *fa, const double2 *fU, double mass, int first,
+                       CGScalars *sc, double2 *partials, int tb0, int tbn);
+void launch_cg1_scalars(hipStream_t s, int nparts, const double2 *partials, CGScalars *sc, int first);
+void launch_cg1_local_sum(hipStream_t s, int nparts, const double2 *partials, CGScalars *sc);
+void launch_cg1_from_sums(hipStream_t s, CGScalars *sc, int first);
 void launch_cg_update_r(hipStream_t s, long n, double2 *r, const double2 *Ad, CGScalars *sc,
                         double2 *part, unsigned *counter);  // counter != null: last block: beta
 void launch_cg_finish_x(hipStream_t s, long n, double2 *x, const double2 *d0, const double2 *d1,

@@ -426,6 +426,7 @@ __device__ __forceinline__ void cg_init_scalars(CGScalars *sc, double2 rr, doubl
     sc->k = 0;
     sc->done = 0;
     sc->converged = 0;
+    sc->max_iter = 0x7fffffff;  // sm_cg_dev sets the caller's limit (one-pass path)
 }
 
 __global__ void __launch_bounds__(RB) cg_finalize_init_kernel(int nparts, const double2 *prr,

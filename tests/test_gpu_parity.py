@@ -51,12 +51,12 @@ def test_operators_bitwise_vs_reference(sm, name):
     assert bits_equal(np.concatenate([F.mu0, F.mu1]), a["ref_force"])
 
 
-@pytest.mark.parametrize("fused", [1, 2, 0], ids=["fused", "fused_inkernel", "sixkernel"])
+@pytest.mark.parametrize("fused", [3, 1, 2, 0], ids=["onepass", "fused", "fused_inkernel", "sixkernel"])
 @pytest.mark.parametrize("name", NAMES)
 def test_cg_vs_reference(sm, name, fused):
-    """Every CG path: the two-pass fused iteration with scalar kernels (default),
-    the same with alpha/beta reduced in-kernel by the last block, and the
-    six-kernel sequence."""
+    """Every CG path: the one-pass iteration (pass 2 folded into the next pass),
+    the two-pass fused iteration with scalar kernels, the same with alpha/beta
+    reduced in-kernel by the last block, and the six-kernel sequence."""
     meta, a = load_fixture(name)
     Nx, Nt, m0 = meta["Nx"], meta["Nt"], meta["m0"]
     S = Nx * Nt
