@@ -357,6 +357,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     c->nparts_red = reduce_blocks(2 * c->g.V);
     c->fcfg = cg_fused_config(c->g);
     if (const char *e = getenv("SM_CG_FUSED")) c->cg_fused = atoi(e);
+    if (const char *e = getenv("SM_CG_INKERNEL_MAX_BLOCKS")) c->cg_inkernel_max_blocks = atoi(e);
     const int np = kMaxPartials;
     const size_t fb = sizeof(double2) * 2 * (size_t)c->g.V;
     hipError_t e = hipSuccess;
@@ -605,15 +606,18 @@ static int cg_onepass(sm_ctx *c) {
     double2 *rold = c->field(odd ? F_R2 : F_R), *rnew = c->field(odd ? F_R : F_R2);
     double2 *aold = c->field(odd ? F_AD2 : F_AD), *anew = c->field(odd ? F_AD : F_AD2);
     const CGFusedCfg &fc = c->fcfg;
+    const int nparts = cg_fused_blocks(fc);
+    // small one-shard grids: the pass's last block forms the scalars (saves a
+    // latency-bound launch per iteration); large grids contend on the ticket
+    const bool inkernel = c->nshard == 1 && nparts <= c->cg_inkernel_max_blocks;
     auto pass = [&](int tb0, int tbn) {
         launch_cg_onepass(c->stream, c->g, fc, c->nshard, dold, rold, aold, dnew, rnew, anew, c->cg_x, c->U,
                           face2_recv(c, 0), face2_recv(c, 1), face2_recv(c, 3), face2_recv(c, 2), c->cg_mass,
-                          first, c->sc, c->partials, tb0, tbn);
+                          first, c->sc, c->partials, tb0, tbn, inkernel ? c->counters : nullptr);
     };
-    const int nparts = cg_fused_blocks(fc);
     if (c->nshard == 1) {
         pass(0, fc.TBk);
-        launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
+        if (!inkernel) launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
         return SM_OK;
     }
     // interior t-blocks while the 2-deep faces of d, r, Ad travel (one round)

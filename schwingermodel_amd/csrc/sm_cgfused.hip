@@ -254,12 +254,15 @@ struct CG1Args {
     const double2 *fd, *fr, *fa, *fU;  // nshard > 1: 4-column faces
     CGScalars *sc;
     double2 *partials;                 // 3 per block: <d,Ad>, <r,Ad>, (|r|^2, |Ad|^2)
+    unsigned *counter;                 // small one-shard grids: the last block forms the scalars
     long V;
     int Nx, Wt, t0, Ntg, nshard;
     int xchunk, NWT, TBk, XB, remap, first;
     int tb0, tbn, part0;
     double mass;
 };
+
+__device__ void cg1_scalars(CGScalars *sc, int first, double2 dA, double2 rA, double2 nn);
 
 struct Raw3 {
     double2 d0, d1, r0, r1, a0, a1, ut, ux, x0, x1;
@@ -432,11 +435,37 @@ __global__ void __launch_bounds__(256) cg_onepass_kernel(CG1Args a) {
     const double2 s1 = block_sum(acc_rA, sh);
     __syncthreads();
     const double2 s2 = block_sum(acc_n, sh);
+    double2 *p = a.partials + 3 * (long)(a.part0 + blockIdx.x);
+    if (!a.counter) {
+        if (threadIdx.x == 0) {
+            p[0] = s0;
+            p[1] = s1;
+            p[2] = s2;
+        }
+        return;
+    }
+    // small grid, one shard: write-through publish + ticket; the last block
+    // sums all partials (sc1 loads, fixed order) and forms the scalars
     if (threadIdx.x == 0) {
-        double2 *p = a.partials + 3 * (long)(a.part0 + blockIdx.x);
-        p[0] = s0;
-        p[1] = s1;
-        p[2] = s2;
+        publish_partial(p, s0);
+        publish_partial(p + 1, s1);
+        publish_partial(p + 2, s2);
+    }
+    __shared__ int last;
+    if (last_block_arrive(a.counter, gridDim.x, &last)) {
+        double2 t[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            __syncthreads();
+            double2 acc = make_double2(0.0, 0.0);
+            for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) {
+                const double2 *pi = a.partials + 3 * (long)i + q;
+                acc = cadd(acc, make_double2(__hip_atomic_load(&pi->x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                             __hip_atomic_load(&pi->y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+            }
+            t[q] = block_sum(acc, sh);
+        }
+        if (threadIdx.x == 0) cg1_scalars(sc, a.first, t[0], t[1], t[2]);
     }
 }
 
@@ -526,7 +555,7 @@ void launch_cg_onepass(hipStream_t s, const Geometry &g, const CGFusedCfg &c, in
                        const double2 *dold, const double2 *rold, const double2 *aold, double2 *dnew,
                        double2 *rnew, double2 *anew, double2 *x, const double2 *U, const double2 *fd,
                        const double2 *fr, const double2 *fa, const double2 *fU, double mass, int first,
-                       CGScalars *sc, double2 *partials, int tb0, int tbn) {
+                       CGScalars *sc, double2 *partials, int tb0, int tbn, unsigned *counter) {
     if (tbn <= 0) return;
     CG1Args a;
     a.dold = dold; a.rold = rold; a.aold = aold;
@@ -541,6 +570,7 @@ void launch_cg_onepass(hipStream_t s, const Geometry &g, const CGFusedCfg &c, in
     a.tb0 = tb0;
     a.tbn = tbn;
     a.part0 = tb0 * c.XB;
+    a.counter = counter;
     hipLaunchKernelGGL(cg_onepass_kernel, dim3(tbn * c.XB), dim3(256), 0, s, a);
 }
 

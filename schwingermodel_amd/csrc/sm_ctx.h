@@ -58,6 +58,7 @@ struct sm_ctx {
     // one-block kernels. Measured equal at 4096^2 and 19 % slower at 1024^2
     // (every block of a one-wave grid hits the ticket at once), so off by default.
     int cg_inkernel = 0;
+    int cg_inkernel_max_blocks = sm::kInKernelScalarMaxBlocks;  // one-pass path (sm_cgfused.hip)
     hipStream_t own_stream = nullptr, stream = nullptr;
     hipStream_t comm_stream = nullptr;  // halo exchange overlapped with interior compute
     hipEvent_t ev_ready = nullptr, ev_halo = nullptr;

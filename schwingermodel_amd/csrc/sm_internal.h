@@ -108,7 +108,11 @@ void launch_cg_onepass(hipStream_t s, const Geometry &g, const CGFusedCfg &c, in
                        const double2 *dold, const double2 *rold, const double2 *aold, double2 *dnew,
                        double2 *rnew, double2 *anew, double2 *x, const double2 *U, const double2 *fd,
                        const double2 *fr, const double2 *fa, const double2 *fU, double mass, int first,
-                       CGScalars *sc, double2 *partials, int tb0, int tbn);
+                       CGScalars *sc, double2 *partials, int tb0, int tbn,
+                       unsigned *counter);  // counter != null: the last block forms the scalars
+// one-pass: in-kernel scalars up to this grid size (64^2: 64 blocks, 12.2 vs 14.2 us per
+// iteration; 256^2: 512 blocks, 18.9 vs 17.0 us -- the ticket contends; tools/tune_cg.py)
+constexpr int kInKernelScalarMaxBlocks = 128;
 void launch_cg1_scalars(hipStream_t s, int nparts, const double2 *partials, CGScalars *sc, int first);
 void launch_cg1_local_sum(hipStream_t s, int nparts, const double2 *partials, CGScalars *sc);
 void launch_cg1_from_sums(hipStream_t s, CGScalars *sc, int first);
