@@ -205,6 +205,11 @@ typedef struct {
     double cg_tol;      /* CG::tol (1e-10 in src/main.cpp:27)              */
     int cg_max_iter;    /* CG::max_iter (10000)                            */
     uint64_t seed;      /* counter-based draws: momenta, sources, Metropolis */
+    int even_odd;       /* 0: the reference's action phi^dag (DD^dag)^-1 phi;
+                           1: the even-odd preconditioned action
+                           phi_e^dag (Dhat Dhat^dag)^-1 phi_e, same gauge
+                           distribution, one half-lattice CG per force
+                           (one shard, even Nt; see sm_eo_* below)          */
 } sm_hmc_params;
 
 /* HMC::Force (src/hmc.cpp:44-60) at the current U: psi = (DD^dag)^-1 phi,
@@ -277,6 +282,15 @@ int sm_hmc_run(sm_ctx *ctx, const sm_hmc_params *p, int hot_start, uint64_t firs
 /* Jackknife_error (src/statistics.cpp:25-34) with its binning as written:
  * bin blocks of n/bin samples; leftover samples only enter the mean. */
 double sm_jackknife_error(const double *dat, int n, int bin);
+
+/* Even-odd pieces, for tests and callers of the preconditioned action:
+ * Dhat = m - (1/m) D_eo D_oe on the even sites (m = m0 + 2): out = Dhat in
+ * (dagger = 0) or Dhat^dag in, on the even sites of full-layout fields (odd
+ * sites of out are 0); sm_eo_cg solves Dhat Dhat^dag x = phi_e the same way. */
+int sm_eo_dhat(sm_ctx *ctx, int dagger, const double *in0, const double *in1, double *out0, double *out1,
+               double m0);
+int sm_eo_cg(sm_ctx *ctx, const double *phi0, const double *phi1, double *x0, double *x1, double m0, double tol,
+             int max_iter, sm_cg_result *res);
 
 /* Gather the sharded gauge field to shard 0 (SaveConf's MPI_Gatherv,
  * src/gauge_conf.cpp:378-396): U0/U1 on shard 0 receive the global

@@ -23,7 +23,7 @@ class CGResult(ctypes.Structure):
 class HMCParams(ctypes.Structure):
     _fields_ = [("m0", ctypes.c_double), ("beta", ctypes.c_double), ("tau", ctypes.c_double),
                 ("md_steps", ctypes.c_int), ("cg_tol", ctypes.c_double), ("cg_max_iter", ctypes.c_int),
-                ("seed", ctypes.c_uint64)]
+                ("seed", ctypes.c_uint64), ("even_odd", ctypes.c_int)]
 
 
 class HamiltonianTerms(ctypes.Structure):
@@ -106,6 +106,8 @@ def _load():
                         ctypes.POINTER(HMCSummary), vp, vp], ci),
         "sm_jackknife_error": ([vp, ci, ci], cd),
         "sm_gather_gauge": ([vp, vp, vp], ci),
+        "sm_eo_dhat": ([vp, ci, vp, vp, vp, vp, cd], ci),
+        "sm_eo_cg": ([vp, vp, vp, vp, vp, cd, cd, ci, ctypes.POINTER(CGResult)], ci),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

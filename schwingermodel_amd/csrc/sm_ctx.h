@@ -85,6 +85,9 @@ struct sm_ctx {
     double2 *U_alt = nullptr;       // 2V: the other gauge buffer (leapfrog copy / kept conf)
     double *Pmd = nullptr;          // 2V: momenta
     double *Fmd = nullptr;          // 2V: MD force
+    // even-odd action (sm_eo.cpp; allocated on first use)
+    double2 *eo = nullptr;          // checkerboard work vectors, V complex each
+    double2 *Ucb = nullptr;         // gauge field in checkerboard layout (even, odd)
     // active CG
     double cg_mass = 0.0;
     const double2 *cg_phi = nullptr;
@@ -119,5 +122,12 @@ int upload_plane_pair(sm_ctx *c, double2 *dst, const double *p0, const double *p
 int download_plane_pair(sm_ctx *c, const double2 *src, double *p0, double *p1);
 double2 *face2_recv(sm_ctx *c, int which);  // 0: d, 1: r, 2: U, 3: Ad
 int exchange_ghost_U(sm_ctx *c);
+
+// even-odd preconditioned pseudofermion action (sm_eo.cpp); phi / chi in the
+// full layout, only their even sites used
+int eo_ready(sm_ctx *c);
+int eo_md_force(sm_ctx *c, const sm_hmc_params *p, const double2 *phi_full, double *F, sm_cg_result *res);
+int eo_fermion_action(sm_ctx *c, const sm_hmc_params *p, const double2 *phi_full, double *S, sm_cg_result *res);
+int eo_pseudofermion(sm_ctx *c, const sm_hmc_params *p, const double2 *chi_full, double2 *phi_full);
 
 }  // namespace sm_host

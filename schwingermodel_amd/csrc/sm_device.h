@@ -44,12 +44,16 @@ __device__ __forceinline__ double2 cdiv(double a, double b, double c, double d) 
 // One site of D (eq. 34; src/dirac_operator.cpp:31-43) or D^dagger
 // (eqs. 35-36; :255-267). Hop coefficients a,b (forward) c,e (backward)
 // carry the gauge link times the boundary sign, exactly as (U*Sign)*combo.
+// Hopping bracket of eq. (34) (DAG = 0) / eqs. (35)-(36) (DAG = 1) at one site:
+// D psi = mass psi - 0.5 * bracket, the four terms summed in the reference's
+// order. p*: t+1 neighbour (pt), x+1 (px), t-1 (pm), x-1 (pxm); Ut, Ux: links
+// of this site, Utm = U_t(n - t^), Uxm = U_x(n - x^); sr0 / sl0: the
+// antiperiodic signs of the forward / backward t hop.
 template <int DAG>
-__device__ __forceinline__ void dirac_site(double mass, double sr0, double sl0, double2 p0,
-                                           double2 p1, double2 pt0, double2 pt1, double2 px0,
-                                           double2 px1, double2 pm0, double2 pm1, double2 pxm0,
-                                           double2 pxm1, double2 Ut, double2 Ux, double2 Utm,
-                                           double2 Uxm, double2 &s0, double2 &s1) {
+__device__ __forceinline__ void dirac_bracket(double sr0, double sl0, double2 pt0, double2 pt1, double2 px0,
+                                              double2 px1, double2 pm0, double2 pm1, double2 pxm0,
+                                              double2 pxm1, double2 Ut, double2 Ux, double2 Utm, double2 Uxm,
+                                              double2 &h0, double2 &h1) {
     const double2 one = make_double2(1.0, 0.0);
     const double2 a = cmul(Ut, make_double2(sr0, 0.0));
     const double2 b = cmul(Ux, one);
@@ -60,22 +64,35 @@ __device__ __forceinline__ void dirac_site(double mass, double sr0, double sl0, 
         double2 B = cmul(b, cadd(px0, cmul(I_NUM, px1)));
         double2 C = cmul(c, cadd(pm0, pm1));
         double2 E = cmul(e, csub(pxm0, cmul(I_NUM, pxm1)));
-        s0 = csub(rmul(mass, p0), rmul(0.5, cadd(cadd(cadd(A, B), C), E)));
+        h0 = cadd(cadd(cadd(A, B), C), E);
         A = cmul(a, cadd(cneg(pt0), pt1));
         B = cmul(b, cadd(cmul(MI_NUM, px0), px1));
         E = cmul(e, cadd(cmul(I_NUM, pxm0), pxm1));
-        s1 = csub(rmul(mass, p1), rmul(0.5, cadd(cadd(cadd(A, B), C), E)));
+        h1 = cadd(cadd(cadd(A, B), C), E);
     } else {
         double2 C = cmul(c, csub(pm0, pm1));
         double2 E = cmul(e, cadd(pxm0, cmul(I_NUM, pxm1)));
         double2 A = cmul(a, cadd(pt0, pt1));
         double2 B = cmul(b, csub(px0, cmul(I_NUM, px1)));
-        s0 = csub(rmul(mass, p0), rmul(0.5, cadd(cadd(cadd(C, E), A), B)));
+        h0 = cadd(cadd(cadd(C, E), A), B);
         C = cmul(c, cadd(cneg(pm0), pm1));
         E = cmul(e, cadd(cmul(MI_NUM, pxm0), pxm1));
         B = cmul(b, cadd(cmul(I_NUM, px0), px1));
-        s1 = csub(rmul(mass, p1), rmul(0.5, cadd(cadd(cadd(C, E), A), B)));
+        h1 = cadd(cadd(cadd(C, E), A), B);
     }
+}
+
+// One site of D (DAG = 0) / D^dagger (DAG = 1): mass*psi - 0.5*bracket.
+template <int DAG>
+__device__ __forceinline__ void dirac_site(double mass, double sr0, double sl0, double2 p0,
+                                           double2 p1, double2 pt0, double2 pt1, double2 px0,
+                                           double2 px1, double2 pm0, double2 pm1, double2 pxm0,
+                                           double2 pxm1, double2 Ut, double2 Ux, double2 Utm,
+                                           double2 Uxm, double2 &s0, double2 &s1) {
+    double2 h0, h1;
+    dirac_bracket<DAG>(sr0, sl0, pt0, pt1, px0, px1, pm0, pm1, pxm0, pxm1, Ut, Ux, Utm, Uxm, h0, h1);
+    s0 = csub(rmul(mass, p0), rmul(0.5, h0));
+    s1 = csub(rmul(mass, p1), rmul(0.5, h1));
 }
 
 // Deterministic block sum: wave butterfly, then lane-0 sums waves in order.

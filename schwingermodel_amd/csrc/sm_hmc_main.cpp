@@ -3,14 +3,16 @@
 // through libsm_hip.so (sm_hmc_run: device trajectories, Dirac/CG kernels,
 // RCCL halos over xGMI).
 //
-//   mpirun -n P ./sm_hmc <Nx> <Nt> [seed]  < params
+//   mpirun -n P ./sm_hmc <Nx> <Nt> [seed] [--even-odd]  < params
 //
 // stdin takes the reference's parameters in its order (src/main.cpp:30-53):
 // ranks_x ranks_t m0 MD_steps trajectory_length beta Ntherm Nmeas Nsteps
 // saveconf. The lattice is t-sharded: ranks_x must be 1 and ranks_t == P.
 // Nx/Nt are runtime arguments (the reference's compile-time NS/NT). The
 // reference seeds rand() from the clock; here every draw is counter-based
-// from `seed` (default: the clock), identical on all ranks.
+// from `seed` (default: the clock), identical on all ranks. --even-odd uses
+// the even-odd preconditioned pseudofermion action (same gauge distribution,
+// one half-lattice CG per force; one rank).
 //
 // Output: the reference's banner and result lines on stdout and its
 // 2D_U1_<Nx>x<Nt>_m0<m0>_SimData.txt file; with saveconf = 1 the
@@ -20,6 +22,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <ctime>
 #include <fstream>
 #include <iomanip>
@@ -52,13 +55,19 @@ int main(int argc, char **argv) {
     int size = 1, rank = 0;
     MPI_Comm_size(MPI_COMM_WORLD, &size);
     MPI_Comm_rank(MPI_COMM_WORLD, &rank);
-    if (argc < 3) {
-        if (rank == 0) std::cerr << "usage: sm_hmc <Nx> <Nt> [seed] < params" << std::endl;
+    int even_odd = 0, npos = 0;
+    const char *pos[3] = {nullptr, nullptr, nullptr};
+    for (int i = 1; i < argc; i++) {
+        if (!strcmp(argv[i], "--even-odd")) even_odd = 1;
+        else if (npos < 3) pos[npos++] = argv[i];
+    }
+    if (npos < 2) {
+        if (rank == 0) std::cerr << "usage: sm_hmc <Nx> <Nt> [seed] [--even-odd] < params" << std::endl;
         MPI_Finalize();
         return 2;
     }
-    const int Nx = atoi(argv[1]), Nt = atoi(argv[2]);
-    unsigned long long seed = argc > 3 ? strtoull(argv[3], nullptr, 10) : (unsigned long long)time(nullptr);
+    const int Nx = atoi(pos[0]), Nt = atoi(pos[1]);
+    unsigned long long seed = npos > 2 ? strtoull(pos[2], nullptr, 10) : (unsigned long long)time(nullptr);
     MPI_Bcast(&seed, 1, MPI_UNSIGNED_LONG_LONG, 0, MPI_COMM_WORLD);
 
     int ranks_x = 1, ranks_t = 1, MD_steps = 0, Ntherm = 0, Nmeas = 0, Nsteps = 0, saveconf = 0;
@@ -173,7 +182,8 @@ int main(int argc, char **argv) {
         std::cout << "* Each rank has " << V << " lattice sites" << std::endl;
         std::cout << "* Host: " << (hostname ? hostname : "unknown") << std::endl;
         std::cout << "* Start time: " << start_time_str << std::endl;
-        std::cout << "* Seed (counter-based draws) = " << seed << ", GPUs = " << size << std::endl;
+        std::cout << "* Seed (counter-based draws) = " << seed << ", GPUs = " << size
+                  << (even_odd ? ", even-odd preconditioned action" : "") << std::endl;
         std::cout << "**********************************************************************" << std::endl;
     }
 
@@ -185,6 +195,7 @@ int main(int argc, char **argv) {
     p.cg_tol = tol;
     p.cg_max_iter = max_iter;
     p.seed = seed;
+    p.even_odd = even_odd;
     std::ostringstream save;
     save << "2D_U1_Ns" << Nx << "_Nt" << Nt << "_b" << format(beta) << "_m" << format(m0);
     const std::string save_prefix = save.str();

@@ -140,6 +140,13 @@ void launch_draw_momenta(hipStream_t s, const Geometry &g, uint64_t seed, double
 void launch_draw_source(hipStream_t s, const Geometry &g, uint64_t seed, double2 *chi);
 void launch_draw_gauge(hipStream_t s, const Geometry &g, uint64_t seed, double sigma, double2 *U);
 
+// ---- even-odd checkerboard (sm_eo.hip) ----
+void launch_to_cb(hipStream_t s, const Geometry &g, const double2 *full, double2 *e, double2 *o);
+void launch_from_cb(hipStream_t s, const Geometry &g, const double2 *e, const double2 *o, double2 *full);
+// out_p = a*aux_p + b*H in_q (H: the hopping bracket of D / D^dag), parity p
+void launch_eo_hop(hipStream_t s, const Geometry &g, int dagger, int p, const double2 *in, const double2 *Up,
+                   const double2 *Uq, const double2 *aux, double a, double b, double2 *out);
+
 // Pack the t = 0 and t = Wt-1 columns (both planes) into contiguous faces.
 void launch_pack_faces(hipStream_t s, const Geometry &g, const double2 *field, double2 *lo_face,
                        double2 *hi_face);

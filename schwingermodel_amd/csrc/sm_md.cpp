@@ -34,6 +34,7 @@ const double2 *ufaces(sm_ctx *c) { return c->nshard == 1 ? nullptr : face2_recv(
 
 int check_params(const sm_hmc_params *p) {
     if (!p) return fail(SM_ERR_ARG, "null params");
+    if (p->even_odd != 0 && p->even_odd != 1) return fail(SM_ERR_ARG, "even_odd must be 0 or 1");
     if (p->md_steps < 1 || p->cg_max_iter < 1 || !(p->tau > 0.0))
         return fail(SM_ERR_ARG, "bad HMC params md_steps=%d tau=%g cg_max_iter=%d", p->md_steps, p->tau,
                     p->cg_max_iter);
@@ -141,11 +142,15 @@ int sm_md_force_dev(sm_ctx *c, const sm_hmc_params *p, const double *phi, double
     TRY(check_ready(c));
     TRY(check_params(p));
     if (!phi || !F || !res) return fail(SM_ERR_ARG, "null argument");
-    // HMC::Force, src/hmc.cpp:44-60
-    double2 *psi = c->field(F_X), *T = c->field(F_RR);
-    TRY(sm_cg_dev(c, phi, (double *)psi, p->m0, p->cg_tol, p->cg_max_iter, res));  // x0 = phi
-    TRY(apply(c, psi, T, p->m0 + 2, 1, nullptr, nullptr, nullptr));                 // TEMP = D^dag psi
-    TRY(sm_force_dev(c, (const double *)psi, (const double *)T, F));                 // fermion bilinear
+    if (p->even_odd) {
+        TRY(eo_md_force(c, p, (const double2 *)phi, F, res));  // sm_eo.cpp
+    } else {
+        // HMC::Force, src/hmc.cpp:44-60
+        double2 *psi = c->field(F_X), *T = c->field(F_RR);
+        TRY(sm_cg_dev(c, phi, (double *)psi, p->m0, p->cg_tol, p->cg_max_iter, res));  // x0 = phi
+        TRY(apply(c, psi, T, p->m0 + 2, 1, nullptr, nullptr, nullptr));                 // TEMP = D^dag psi
+        TRY(sm_force_dev(c, (const double *)psi, (const double *)T, F));                 // fermion bilinear
+    }
     launch_staple_force(c->stream, c->g, c->nshard, c->U, ufaces(c), p->beta, F, nullptr);  // Force_G
     HIP_TRY(hipGetLastError());
     return SM_OK;
@@ -219,10 +224,14 @@ int sm_hamiltonian_dev(sm_ctx *c, const sm_hmc_params *p, const double *phi, con
     double sp, action;
     TRY(plaquette_sums(c, p->beta, &sp, &action, nullptr));
     sm_cg_result r;
-    double2 *x = c->field(F_X);   // the reference's TEMP
-    TRY(sm_cg_dev(c, phi, (double *)x, p->m0, p->cg_tol, p->cg_max_iter, &r));
-    double z[2];
-    TRY(sm_dot_dev(c, (const double *)x, phi, z));
+    double z[2] = {0.0, 0.0};
+    if (p->even_odd) {
+        TRY(eo_fermion_action(c, p, (const double2 *)phi, &z[0], &r));
+    } else {
+        double2 *x = c->field(F_X);   // the reference's TEMP
+        TRY(sm_cg_dev(c, phi, (double *)x, p->m0, p->cg_tol, p->cg_max_iter, &r));
+        TRY(sm_dot_dev(c, (const double *)x, phi, z));
+    }
     out->kinetic = k.x;
     out->gauge_action = action;
     out->fermion = z[0];
@@ -257,7 +266,8 @@ int sm_hmc_trajectory(sm_ctx *c, const sm_hmc_params *p, uint64_t traj, sm_hmc_r
     launch_draw_momenta(c->stream, c->g, ts, c->Pmd);   // RandomPI
     launch_draw_source(c->stream, c->g, ts, chi);       // RandomCHI
     HIP_TRY(hipGetLastError());
-    TRY(apply(c, chi, phi, p->m0 + 2, 0, nullptr, nullptr, nullptr));  // phi = D chi
+    if (p->even_odd) TRY(eo_pseudofermion(c, p, chi, phi));              // phi_e = Dhat chi_e
+    else TRY(apply(c, chi, phi, p->m0 + 2, 0, nullptr, nullptr, nullptr));  // phi = D chi
     sm_hamiltonian_terms h0, h1;
     TRY(sm_hamiltonian_dev(c, p, (const double *)phi, c->Pmd, &h0));   // H[U][Pi] (P not yet evolved)
     // leapfrog on a copy of U: the kept configuration stays in U_alt

@@ -101,6 +101,7 @@ def run_hmc(with_ref=False):
            "params": {k: c[k] for k in ("m0", "md_steps", "tau", "beta", "Ntherm", "Nmeas", "Nsteps")},
            "reference_recorded": {k: c[k] for k in ("Ep", "dEp", "acceptance", "seconds")}}
     progs = {"sm_hmc": [os.path.join(REPO, "schwingermodel_amd", "sm_hmc"), "64", "64", "1"],
+             "sm_hmc_even_odd": [os.path.join(REPO, "schwingermodel_amd", "sm_hmc"), "64", "64", "1", "--even-odd"],
              "dropin_shim": [os.path.join(REPO, "oracle", "_ref", "SM_64x64_hip")]}
     if with_ref:
         progs["reference_cpu"] = [os.path.join(REPO, "oracle", "_ref", "SM_64x64_ref")]
@@ -123,12 +124,12 @@ def run_hmc(with_ref=False):
     return out
 
 
-def run_hmc_large(N, ntraj=3):
+def run_hmc_large(N, ntraj=3, even_odd=0):
     import ctypes
     import schwingermodel_amd as sm
     L = sm.Lattice(N, N)
     sm.check(sm.lib.sm_fill_gauge_dev(L.ctx, 4321, 0.3246))
-    p = sm.HMCParams(0.10, 3.0, 0.5, 10, 1e-10, 10000, 7)
+    p = sm.HMCParams(0.10, 3.0, 0.5, 10, 1e-10, 10000, 7, even_odd)
     rows = []
     for traj in range(ntraj):
         r = sm.HMCResult()
@@ -138,7 +139,8 @@ def run_hmc_large(N, ntraj=3):
         rows.append({"traj": traj, "seconds": round(dt, 3), "cg_iterations": r.cg_iterations, "dH": r.dH,
                      "accepted": r.accepted, "ms_per_cg_it": round(1e3 * dt / max(1, r.cg_iterations), 4)})
     L.close()
-    return {"hmc_large": f"{N}x{N}", "beta": 3.0, "m0": 0.10, "tau": 0.5, "md_steps": 10, "trajectories": rows}
+    return {"hmc_large": f"{N}x{N}", "even_odd": even_odd, "beta": 3.0, "m0": 0.10, "tau": 0.5, "md_steps": 10,
+            "trajectories": rows}
 
 
 def main():
@@ -154,6 +156,7 @@ def main():
         print(json.dumps(run_hmc(a.hmc_ref)), flush=True)
     if a.hmc_large:
         print(json.dumps(run_hmc_large(a.hmc_large)), flush=True)
+        print(json.dumps(run_hmc_large(a.hmc_large, even_odd=1)), flush=True)
 
 
 if __name__ == "__main__":
