@@ -81,12 +81,6 @@ struct Raw {
     double2 d0, d1, r0, r1, ut, ux, x0, x1;
 };
 
-struct Sp {   // a 2-spinor at one site
-    double2 a, b;
-};
-
-__device__ __forceinline__ Sp shr(Sp v) { return Sp{dpp_shr1(v.a), dpp_shr1(v.b)}; }
-__device__ __forceinline__ Sp shl(Sp v) { return Sp{dpp_shl1(v.a), dpp_shl1(v.b)}; }
 
 __global__ void __launch_bounds__(256) cg_fused_kernel(CGFArgs a) {
     __shared__ double2 sh[4];

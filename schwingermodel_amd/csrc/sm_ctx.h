@@ -88,6 +88,7 @@ struct sm_ctx {
     // even-odd action (sm_eo.cpp; allocated on first use)
     double2 *eo = nullptr;          // checkerboard work vectors, V complex each
     double2 *Ucb = nullptr;         // gauge field in checkerboard layout (even, odd)
+    int eo_fused = 1;               // Dhat as one fused marching pass (0: two hop launches)
     // active CG
     double cg_mass = 0.0;
     const double2 *cg_phi = nullptr;

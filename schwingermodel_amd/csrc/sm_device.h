@@ -128,6 +128,12 @@ __device__ __forceinline__ double dpp_shl1(double v) {  // lane l <- lane l+1
 __device__ __forceinline__ double2 dpp_shr1(double2 v) { return make_double2(dpp_shr1(v.x), dpp_shr1(v.y)); }
 __device__ __forceinline__ double2 dpp_shl1(double2 v) { return make_double2(dpp_shl1(v.x), dpp_shl1(v.y)); }
 
+struct Sp {   // a 2-spinor at one site
+    double2 a, b;
+};
+__device__ __forceinline__ Sp shr(Sp v) { return Sp{dpp_shr1(v.a), dpp_shr1(v.b)}; }
+__device__ __forceinline__ Sp shl(Sp v) { return Sp{dpp_shl1(v.a), dpp_shl1(v.b)}; }
+
 // Non-temporal (streaming) 16-B loads/stores: data touched once per pass.
 // Measured on MI355X (tools/membench.hip): block-contiguous chunks with nt
 // loads+stores reach 5.7 TB/s on the 2-read/1-write BLAS-1 pattern against

@@ -37,7 +37,9 @@ static double2 *ucb(sm_ctx *c, int parity) { return c->Ucb + (size_t)parity * c-
 
 int eo_ready(sm_ctx *c) {
     if (c->nshard != 1) return fail(SM_ERR_ARG, "even-odd preconditioning needs one shard (nshard = %d)", c->nshard);
-    if (c->g.Wt % 2) return fail(SM_ERR_ARG, "even-odd preconditioning needs an even Nt (%d)", c->g.Wt);
+    // the periodic lattice is bipartite (a checkerboard) only for even Nx and Nt
+    if (c->g.Wt % 2 || c->g.Nx % 2)
+        return fail(SM_ERR_ARG, "even-odd preconditioning needs even Nx and Nt (%d x %d)", c->g.Nx, c->g.Wt);
     if (!c->eo) {
         HIP_TRY(hipMalloc(&c->eo, sizeof(double2) * (size_t)EO_N * c->g.V));
         HIP_TRY(hipMalloc(&c->Ucb, sizeof(double2) * 2 * (size_t)c->g.V));
@@ -48,18 +50,30 @@ int eo_ready(sm_ctx *c) {
     return SM_OK;
 }
 
-// out_e = Dhat v_e (dagger = 0) or Dhat^dag v_e (dagger = 1); uses EO_T.
-void eo_dhat(sm_ctx *c, int dagger, const double2 *v, double2 *out, double mass) {
+// out_e = Dhat v_e (dagger = 0) or Dhat^dag v_e (dagger = 1). Fused: both
+// hops in one marching pass (eo_dhat_fused_kernel), optionally with partials
+// of sum aux * conj(out); unfused (c->eo_fused == 0): two eo_hop launches
+// through EO_T, bitwise the same result.
+void eo_dhat(sm_ctx *c, int dagger, const double2 *v, double2 *out, double mass, const double2 *aux = nullptr,
+             double2 *partials = nullptr) {
+    if (c->eo_fused) {
+        launch_eo_dhat_fused(c->stream, c->g, eo_fused_config(c->g), dagger, v, ucb(c, 0), ucb(c, 1), mass, out, aux,
+                             partials);
+        return;
+    }
     double2 *T = eo_vec(c, EO_T);
     launch_eo_hop(c->stream, c->g, dagger, 1, v, ucb(c, 1), ucb(c, 0), nullptr, 0.0, -0.5, T);   // D_oe v
     launch_eo_hop(c->stream, c->g, dagger, 0, T, ucb(c, 0), ucb(c, 1), v, mass, 0.5 / mass, out);
+    if (aux) launch_dot_partial(c->stream, c->g.V, aux, out, partials);
 }
 
-// out = Dhat Dhat^dag v (uses EO_T, EO_W)
-static void eo_M(sm_ctx *c, const double2 *v, double2 *out, double mass) {
+// out = Dhat Dhat^dag v (uses EO_W; EO_T unfused); dot partials of <v, out>
+// into c->partials; returns their count.
+static int eo_M(sm_ctx *c, const double2 *v, double2 *out, double mass) {
     double2 *W = eo_vec(c, EO_W);
     eo_dhat(c, 1, v, W, mass);
-    eo_dhat(c, 0, W, out, mass);
+    eo_dhat(c, 0, W, out, mass, v, c->partials);
+    return c->eo_fused ? eo_fused_blocks(eo_fused_config(c->g)) : reduce_blocks(c->g.V);
 }
 
 // CG on Dhat Dhat^dag x = b (x0 = b, the reference's convention), the
@@ -69,7 +83,7 @@ int eo_cg(sm_ctx *c, const double2 *b, double2 *x, double mass, double tol, int 
     const int nparts = reduce_blocks(n);
     double2 *r = eo_vec(c, EO_R), *d = eo_vec(c, EO_D), *Ad = eo_vec(c, EO_AD);
     if (x != b) launch_copy(c->stream, n, b, x);
-    eo_M(c, x, Ad, mass);
+    eo_M(c, x, Ad, mass);                                   // (its dot partials are not used)
     double2 *prr = c->partials, *ppp = c->partials + nparts;
     launch_cg_init(c->stream, n, b, Ad, r, d, prr, ppp);
     launch_cg_finalize_init(c->stream, nparts, prr, ppp, c->sc, tol);
@@ -77,9 +91,8 @@ int eo_cg(sm_ctx *c, const double2 *b, double2 *x, double mass, double tol, int 
     while (issued < max_iter) {
         const int nb = (max_iter - issued) < chunk ? (max_iter - issued) : chunk;
         for (int i = 0; i < nb; ++i) {
-            eo_M(c, d, Ad, mass);
-            launch_dot_partial(c->stream, n, d, Ad, c->partials);
-            launch_cg_alpha(c->stream, nparts, c->partials, c->sc);
+            const int np = eo_M(c, d, Ad, mass);                     // Ad and partials of <d, Ad>
+            launch_cg_alpha(c->stream, np, c->partials, c->sc);
             launch_cg_update_xr(c->stream, n, x, r, d, Ad, c->sc, c->partials);
             launch_cg_beta(c->stream, nparts, c->partials, c->sc);
             launch_cg_update_d(c->stream, n, d, r, c->sc);

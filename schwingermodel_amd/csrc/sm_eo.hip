@@ -83,6 +83,151 @@ __global__ void __launch_bounds__(256) eo_hop_kernel(EoGeom g, int p, const doub
     }
 }
 
+// ---- fused Dhat: both hops in one marching pass ------------------------------
+// out_e = m v + (0.5/m) H_eo T,  T = -0.5 H_oe v  (Dhat v; DAG = 1: Dhat^dag v
+// with the D^dag bracket), the odd intermediate T kept in registers. Same
+// structure as the fused CG pass: a wave owns 60 k-columns (lanes k-2 .. k+61,
+// two halo lanes per side), marches x, t-neighbours by DPP. In the
+// checkerboard the t-neighbours of a site are lanes (l-1, l) or (l, l+1)
+// depending on the row's parity (row-uniform), the x-neighbours are lane l of
+// the rows x +- 1. Per-element arithmetic = two eo_hop launches (bitwise).
+// EPI_DOT: per-block partials of sum aux * conj(out) (the CG's <d, Ad>).
+constexpr int EW = 60;
+
+struct EoFArgs {
+    const double2 *v, *Ue, *Uo;
+    double2 *out;
+    const double2 *aux;
+    double2 *partials;
+    EoGeom g;
+    int xchunk, NWT, TBk, XB;
+    double mass;
+};
+
+struct ERow {                // one lane, one row: even input, even / odd links at (y, k)
+    double2 v0, v1, et, ex, ot, ox;
+};
+
+
+template <int DAG, int EPI>
+__global__ void __launch_bounds__(256) eo_dhat_fused_kernel(EoFArgs a) {
+    __shared__ double2 sh[4];
+    const int tb = blockIdx.x % a.TBk, xc = blockIdx.x / a.TBk;
+    const int lane = threadIdx.x & 63;
+    const int gw = tb * 4 + (threadIdx.x >> 6);
+    const int x0 = xc * a.xchunk, xe = min(a.g.Nx, x0 + a.xchunk);
+    double2 acc = make_double2(0.0, 0.0);
+    if (gw < a.NWT && x0 < xe) {
+        const int Wh = a.g.Wh, Nx = a.g.Nx;
+        const long Vh = a.g.Vh;
+        const int k = gw * EW - 2 + lane;
+        int kw = k % Wh;
+        if (kw < 0) kw += Wh;                                  // periodic in t (one shard)
+        const bool own = lane >= 2 && lane < EW + 2 && k < Wh;
+        const double m = a.mass, hm = 0.5 / a.mass;
+        auto wrapx = [Nx](int x) { int w = x % Nx; return w < 0 ? w + Nx : w; };
+        auto load = [&](int y, ERow &R) {
+            const long h = (long)wrapx(y) * Wh + kw;
+            R.v0 = a.v[h];
+            R.v1 = a.v[h + Vh];
+            R.et = a.Ue[h];
+            R.ex = a.Ue[h + Vh];
+            R.ot = a.Uo[h];
+            R.ox = a.Uo[h + Vh];
+        };
+        auto signs = [&](int t, double &sr0, double &sl0) {
+            const int tg = a.g.t0 + t;
+            sr0 = tg == a.g.Ntg - 1 ? -1.0 : 1.0;
+            sl0 = tg == 0 ? -1.0 : 1.0;
+        };
+        // T at odd site (y, k): neighbours v(y, k-1+s_o), v(y, k+s_o), v(y+-1, k); s_o = 1 - (y&1)
+        auto todd = [&](int y, const Sp &vc, const Sp &vxm, const Sp &vxp, const ERow &Rc, double2 ex_m) {
+            const bool ye = (wrapx(y) & 1) == 0;
+            Sp pm, pp;
+            double2 utm;
+            if (ye) {
+                pm = vc;
+                pp = shl(vc);
+                utm = Rc.et;
+            } else {
+                pm = shr(vc);
+                pp = vc;
+                utm = dpp_shr1(Rc.et);
+            }
+            double sr0, sl0;
+            signs(2 * kw + (ye ? 1 : 0), sr0, sl0);
+            double2 h0, h1;
+            dirac_bracket<DAG>(sr0, sl0, pp.a, pp.b, vxp.a, vxp.b, pm.a, pm.b, vxm.a, vxm.b, Rc.ot, Rc.ox, utm, ex_m,
+                               h0, h1);
+            return Sp{rmul(-0.5, h0), rmul(-0.5, h1)};
+        };
+        // out at even site (x, k): T(x, k-1+s_e), T(x, k+s_e), T(x+-1, k); s_e = x&1
+        auto eout = [&](int x, const Sp &Tc, const Sp &Txm, const Sp &Txp, const ERow &Rc, double2 ox_m,
+                        const Sp &vc) {
+            const bool xe_ = (wrapx(x) & 1) == 0;
+            Sp pm, pp;
+            double2 utm;
+            if (xe_) {
+                pm = shr(Tc);
+                pp = Tc;
+                utm = dpp_shr1(Rc.ot);
+            } else {
+                pm = Tc;
+                pp = shl(Tc);
+                utm = Rc.ot;
+            }
+            double sr0, sl0;
+            signs(2 * kw + (xe_ ? 0 : 1), sr0, sl0);
+            double2 h0, h1;
+            dirac_bracket<DAG>(sr0, sl0, pp.a, pp.b, Txp.a, Txp.b, pm.a, pm.b, Txm.a, Txm.b, Rc.et, Rc.ex, utm, ox_m,
+                               h0, h1);
+            return Sp{cadd(rmul(m, vc.a), rmul(hm, h0)), cadd(rmul(m, vc.b), rmul(hm, h1))};
+        };
+        ERow R, Rm1, Rc, Rn;
+        load(x0 - 2, R);
+        const Sp vm2{R.v0, R.v1};
+        const double2 exm2 = R.ex;
+        load(x0 - 1, Rm1);
+        Sp vm1{Rm1.v0, Rm1.v1};
+        load(x0, Rc);
+        Sp vc{Rc.v0, Rc.v1};
+        load(x0 + 1, Rn);
+        Sp vn{Rn.v0, Rn.v1};
+        load(x0 + 2, R);
+        Sp Tp = todd(x0 - 1, vm1, vm2, vc, Rm1, exm2);
+        Sp Tc = todd(x0, vc, vm1, vn, Rc, Rm1.ex);
+        double2 oxp = Rm1.ox;                                  // U_x(x-1) odd link
+        for (int x = x0; x < xe; ++x) {
+            const ERow R2 = R;                                 // row x+2
+            load(min(x + 3, xe + 1), R);
+            __builtin_amdgcn_sched_barrier(0);
+            const Sp v2{R2.v0, R2.v1};
+            const Sp Tn = todd(x + 1, vn, vc, v2, Rn, Rc.ex);
+            const Sp o = eout(x, Tc, Tp, Tn, Rc, oxp, vc);
+            if (own) {
+                const long h = (long)x * Wh + kw;
+                st_nt(a.out + h, o.a);
+                st_nt(a.out + h + Vh, o.b);
+                if (EPI == EPI_DOT) {
+                    acc = cadd(acc, cmul(a.aux[h], cconj(o.a)));
+                    acc = cadd(acc, cmul(a.aux[h + Vh], cconj(o.b)));
+                }
+            }
+            Tp = Tc;
+            Tc = Tn;
+            oxp = Rc.ox;
+            vc = vn;
+            vn = v2;
+            Rc = Rn;
+            Rn = R2;
+        }
+    }
+    if (EPI == EPI_DOT) {
+        const double2 bs = block_sum(acc, sh);
+        if (threadIdx.x == 0) a.partials[blockIdx.x] = bs;
+    }
+}
+
 namespace {
 unsigned eo_grid(long n) {
     long nb = (n + 255) / 256;
@@ -107,6 +252,44 @@ void launch_to_cb(hipStream_t s, const Geometry &g, const double2 *full, double2
 
 void launch_from_cb(hipStream_t s, const Geometry &g, const double2 *e, const double2 *o, double2 *full) {
     hipLaunchKernelGGL(from_cb_kernel, dim3(eo_grid(g.V)), dim3(256), 0, s, eo_geom(g), e, o, full);
+}
+
+EoFusedCfg eo_fused_config(const Geometry &g) {
+    EoFusedCfg c;
+    const int Wh = g.Wt / 2;
+    c.NWT = (Wh + EW - 1) / EW;
+    c.TBk = (c.NWT + 3) / 4;
+    int target = 4096;                                    // blocks (as the fused CG pass)
+    if (const char *e = getenv("SM_EO_BLOCKS")) target = atoi(e);
+    int nchunks = (target + c.TBk - 1) / c.TBk;
+    if (nchunks > g.Nx / 2) nchunks = g.Nx / 2;
+    if (nchunks < 1) nchunks = 1;
+    int xchunk = (g.Nx + nchunks - 1) / nchunks;
+    xchunk += xchunk & 1;                                 // even: every chunk starts on an even row
+    if (const char *e = getenv("SM_EO_XCHUNK")) xchunk = atoi(e);
+    c.xchunk = xchunk;
+    c.XB = (g.Nx + c.xchunk - 1) / c.xchunk;
+    return c;
+}
+
+int eo_fused_blocks(const EoFusedCfg &c) { return c.TBk * c.XB; }
+
+void launch_eo_dhat_fused(hipStream_t s, const Geometry &g, const EoFusedCfg &c, int dagger, const double2 *v,
+                          const double2 *Ue, const double2 *Uo, double mass, double2 *out, const double2 *aux,
+                          double2 *partials) {
+    EoFArgs a;
+    a.v = v; a.Ue = Ue; a.Uo = Uo; a.out = out; a.aux = aux; a.partials = partials;
+    a.g = eo_geom(g);
+    a.xchunk = c.xchunk; a.NWT = c.NWT; a.TBk = c.TBk; a.XB = c.XB;
+    a.mass = mass;
+    const dim3 grid(c.TBk * c.XB), block(256);
+    if (dagger) {
+        if (aux) hipLaunchKernelGGL((eo_dhat_fused_kernel<1, EPI_DOT>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((eo_dhat_fused_kernel<1, EPI_NONE>), grid, block, 0, s, a);
+    } else {
+        if (aux) hipLaunchKernelGGL((eo_dhat_fused_kernel<0, EPI_DOT>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((eo_dhat_fused_kernel<0, EPI_NONE>), grid, block, 0, s, a);
+    }
 }
 
 void launch_eo_hop(hipStream_t s, const Geometry &g, int dagger, int p, const double2 *in, const double2 *Up,

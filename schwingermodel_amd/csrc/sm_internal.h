@@ -146,6 +146,16 @@ void launch_from_cb(hipStream_t s, const Geometry &g, const double2 *e, const do
 // out_p = a*aux_p + b*H in_q (H: the hopping bracket of D / D^dag), parity p
 void launch_eo_hop(hipStream_t s, const Geometry &g, int dagger, int p, const double2 *in, const double2 *Up,
                    const double2 *Uq, const double2 *aux, double a, double b, double2 *out);
+// Fused Dhat / Dhat^dag (both hops in one marching pass); aux != null adds
+// per-block partials of sum aux * conj(out) (eo_fused_blocks of them).
+struct EoFusedCfg {
+    int NWT, TBk, xchunk, XB;
+};
+EoFusedCfg eo_fused_config(const Geometry &g);
+int eo_fused_blocks(const EoFusedCfg &c);
+void launch_eo_dhat_fused(hipStream_t s, const Geometry &g, const EoFusedCfg &c, int dagger, const double2 *v,
+                          const double2 *Ue, const double2 *Uo, double mass, double2 *out, const double2 *aux,
+                          double2 *partials);
 
 // Pack the t = 0 and t = Wt-1 columns (both planes) into contiguous faces.
 void launch_pack_faces(hipStream_t s, const Geometry &g, const double2 *field, double2 *lo_face,

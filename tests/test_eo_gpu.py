@@ -74,6 +74,30 @@ def test_dhat_matches_definition(sm, name, dag):
     assert np.linalg.norm(got - expect) <= 1e-14 * np.linalg.norm(expect)
 
 
+@pytest.mark.parametrize("name", ["l32x48_b3_m-0p10", "l64x64_b5_m-0p06", "l8x8_hot_m0p2", "l40x24_hot_m0p2"])
+@pytest.mark.parametrize("dag", [0, 1])
+def test_fused_dhat_bitwise_equals_two_hops(sm, name, dag):
+    """The fused marching Dhat kernel (one pass, odd intermediate in registers)
+    performs exactly the two eo_hop launches' arithmetic."""
+    meta, a = load_fixture(name)
+    Nx, Nt, m0 = meta["Nx"], meta["Nt"], meta["m0"]
+    S = Nx * Nt
+    v = even_only(a["psi"], Nx, Nt)
+    outs = []
+    for fused in ("1", "0"):
+        os.environ["SM_EO_FUSED"] = fused  # read when the context is created
+        try:
+            L = sm.Lattice(Nx, Nt)
+        finally:
+            os.environ.pop("SM_EO_FUSED", None)
+        sm.check(sm.lib.sm_upload_gauge(L.ctx, ptr(a["U"][:2 * S]), ptr(a["U"][2 * S:])))
+        o = np.empty(4 * S)
+        sm.check(sm.lib.sm_eo_dhat(L.ctx, dag, ptr(v[:2 * S]), ptr(v[2 * S:]), ptr(o[:2 * S]), ptr(o[2 * S:]), m0))
+        L.close()
+        outs.append(o)
+    assert np.array_equal(outs[0].view(np.uint64), outs[1].view(np.uint64))
+
+
 @pytest.mark.parametrize("name", ["l64x64_b5_m-0p06", "l32x48_b3_m-0p10"])
 def test_eo_cg_solves_and_converges_faster(sm, name):
     meta, a = load_fixture(name)

@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Per-iteration time of the even-odd CG (sm_eo_cg, tol 0) for fused-Dhat chunk heights.
+
+    python tools/tune_eo.py [--n 1024] [--xchunk 2,4,8,16] [--iters 200]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--xchunk", default="0,2,4,8,16")
+    ap.add_argument("--iters", type=int, default=200)
+    a = ap.parse_args()
+    import numpy as np
+    import schwingermodel_amd as sm
+    N = a.n
+    S = N * N
+    U, phi = np.empty(4 * S), np.empty(4 * S)
+    sm.lib.sm_fill_gauge(4321, 0.3246, N, 0, N, 0, N, U.ctypes.data, U[2 * S:].ctypes.data)
+    sm.lib.sm_fill_spinor(91011, N, 0, N, 0, N, phi.ctypes.data, phi[2 * S:].ctypes.data)
+    x = np.empty(4 * S)
+    for xc in [int(v) for v in a.xchunk.split(",")]:
+        if xc > 0:
+            os.environ["SM_EO_XCHUNK"] = str(xc)
+        L = sm.Lattice(N, N)
+        os.environ.pop("SM_EO_XCHUNK", None)
+        sm.check(sm.lib.sm_upload_gauge(L.ctx, U.ctypes.data, U[2 * S:].ctypes.data))
+        res = sm.CGResult()
+        best = None
+        for _ in range(3):
+            t = time.perf_counter()
+            sm.check(sm.lib.sm_eo_cg(L.ctx, phi.ctypes.data, phi[2 * S:].ctypes.data, x.ctypes.data,
+                                     x[2 * S:].ctypes.data, -0.10, 0.0, a.iters, ctypes.byref(res)))
+            dt = time.perf_counter() - t
+            best = dt if best is None else min(best, dt)
+        L.close()
+        print(json.dumps({"n": N, "xchunk": xc, "iters": res.iterations, "ms_per_it": round(1e3 * best / a.iters, 4)}))
+
+
+if __name__ == "__main__":
+    main()
