@@ -767,14 +767,15 @@ int sm_cg_dev(sm_ctx *c, const double *phi, double *x, double m0, double tol, in
         HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)&c->sc->max_iter, max_iter, 1, c->stream));
         passes = max_iter + 1;
     }
-    int issued = 0, chunk = 4;
+    CgChunker plan;
+    int issued = 0, chunk = plan.chunk;
     while (issued < passes) {
         const int nb = (passes - issued) < chunk ? (passes - issued) : chunk;
         TRY(sm_cg_iterate(c, nb));
         issued += nb;
         TRY(sm_cg_status(c, res));
         if (res->converged) break;
-        if (chunk < 64) chunk *= 2;
+        chunk = plan.next(res->iterations, res->residual, tol * res->phi_norm);
     }
     return sm_cg_finish(c, res);
 }

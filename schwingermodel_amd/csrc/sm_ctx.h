@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cmath>
 #include <cstddef>
 
 #include "sm_internal.h"
@@ -103,6 +104,32 @@ struct sm_ctx {
 namespace sm_host {
 
 using namespace sm;
+
+// How many CG iterations to enqueue before the next status read. Kernels are
+// no-ops once the device's `done` flag is set, so queueing past convergence
+// costs empty launches and every status read costs a host round trip: predict
+// the iterations left to the stop test from the residual's observed geometric
+// rate, and stay a few percent past it.
+struct CgChunker {
+    int chunk = 4;
+    int k_prev = -1;
+    double err_prev = 0.0;
+    int next(int k, double err, double target) {
+        int c = chunk < 64 ? 2 * chunk : 64;
+        if (k_prev >= 0 && k > k_prev && err_prev > 0.0 && err > 0.0 && err < err_prev && target > 0.0) {
+            const double rate = std::pow(err / err_prev, 1.0 / (k - k_prev));
+            if (rate < 1.0) {
+                const double left = std::log(target / err) / std::log(rate);
+                c = left <= 0.0 ? 2 : (int)std::ceil(left * 1.05) + 1;
+                c = c < 2 ? 2 : (c > 256 ? 256 : c);
+            }
+        }
+        k_prev = k;
+        err_prev = err;
+        chunk = c;
+        return c;
+    }
+};
 
 // Largest face exchanged, in doubles per x: 2 columns x 2 planes x complex.
 constexpr size_t kMaxFaceDoubles = 8;

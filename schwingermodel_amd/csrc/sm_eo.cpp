@@ -87,7 +87,8 @@ int eo_cg(sm_ctx *c, const double2 *b, double2 *x, double mass, double tol, int 
     double2 *prr = c->partials, *ppp = c->partials + nparts;
     launch_cg_init(c->stream, n, b, Ad, r, d, prr, ppp);
     launch_cg_finalize_init(c->stream, nparts, prr, ppp, c->sc, tol);
-    int issued = 0, chunk = 4;
+    CgChunker plan;
+    int issued = 0, chunk = plan.chunk;
     while (issued < max_iter) {
         const int nb = (max_iter - issued) < chunk ? (max_iter - issued) : chunk;
         for (int i = 0; i < nb; ++i) {
@@ -102,7 +103,7 @@ int eo_cg(sm_ctx *c, const double2 *b, double2 *x, double mass, double tol, int 
         HIP_TRY(hipMemcpyAsync(c->h_sc, c->sc, sizeof(CGScalars), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
         if (c->h_sc->done) break;
-        if (chunk < 64) chunk *= 2;
+        chunk = plan.next(c->h_sc->k, c->h_sc->err, tol * c->h_sc->phi_norm);
     }
     res->converged = c->h_sc->converged;
     res->iterations = c->h_sc->k;
