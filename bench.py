@@ -13,6 +13,8 @@ Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N)
 one process per GPU, the lattice sharded along t with RCCL halos; weak scaling,
 each GPU owns 4096 x 4096 sites (global lattice 4096 x 4096N). `value` is the
 whole-job rate in 4096^2-lattice CG iterations per second (= it/s x N).
+`--strong` instead splits one fixed 4096 x 4096 lattice over the N GPUs
+ and reports that lattice's it/s.
 torch.distributed (gloo) is used only for the RCCL unique id, barriers and the
 max-over-ranks timing.
 """
@@ -50,6 +52,8 @@ def parse():
                     help="multi-GPU wire: RCCL (production) or the host-staged test transport")
     ap.add_argument("--device", type=int, default=None, help="override LOCAL_RANK -> GPU mapping")
     ap.add_argument("--cg-path", choices=["onepass", "fused", "fused_inkernel", "sixkernel"], default="onepass")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling (SURVEY.md §8d config 4): a fixed nx x nt-per-gpu lattice split over the N GPUs")
     return ap.parse_args()
 
 
@@ -142,6 +146,10 @@ def main():
             dist.barrier()
 
     Nx, Wt = args.nx, args.nt_per_gpu
+    if args.strong:
+        if Wt % world:
+            raise SystemExit(f"--strong: Nt={Wt} is not divisible by {world} GPUs")
+        Wt //= world
     Nt = Wt * world
     transport = None
     if world > 1 and args.transport == "hosted":
@@ -211,7 +219,9 @@ def main():
 
     if rank == 0:
         it_per_s = args.steps / t_local
-        value = it_per_s * world  # 4096^2-lattice iterations per second, whole job
+        # weak: 4096^2-lattice iterations per second, whole job; strong: the
+        # one fixed lattice's iterations per second
+        value = it_per_s if args.strong else it_per_s * world
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, args.cpu_threads)
@@ -219,13 +229,14 @@ def main():
         line = {
             "metric": "CG iterations/sec + Dirac-apply achieved HBM GB/s, 4096^2 fp64",
             "value": round(value, 3),
-            "unit": "CG iterations/s (4096x4096 sites per GPU, whole job)",
+            "unit": ("CG iterations/s (one 4096x4096 lattice over all GPUs)" if args.strong
+                     else "CG iterations/s (4096x4096 sites per GPU, whole job)"),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * t_local / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (counter-based U(1) field theta~N(0,0.2374^2), complex-Gaussian RHS)",
