@@ -209,7 +209,8 @@ typedef struct {
                            1: the even-odd preconditioned action
                            phi_e^dag (Dhat Dhat^dag)^-1 phi_e, same gauge
                            distribution, one half-lattice CG per force
-                           (one shard, even Nt; see sm_eo_* below)          */
+                           (even Nx and shard width, shards >= 4 wide;
+                           see sm_eo_* below)                               */
 } sm_hmc_params;
 
 /* HMC::Force (src/hmc.cpp:44-60) at the current U: psi = (DD^dag)^-1 phi,
@@ -286,7 +287,9 @@ double sm_jackknife_error(const double *dat, int n, int bin);
 /* Even-odd pieces, for tests and callers of the preconditioned action:
  * Dhat = m - (1/m) D_eo D_oe on the even sites (m = m0 + 2): out = Dhat in
  * (dagger = 0) or Dhat^dag in, on the even sites of full-layout fields (odd
- * sites of out are 0); sm_eo_cg solves Dhat Dhat^dag x = phi_e the same way. */
+ * sites of out are 0); sm_eo_cg solves Dhat Dhat^dag x = phi_e the same way.
+ * t-sharded contexts exchange 2-column checkerboard faces per hop (SM_ERR_ARG
+ * for odd Nx, odd shard width or shards narrower than 4). */
 int sm_eo_dhat(sm_ctx *ctx, int dagger, const double *in0, const double *in1, double *out0, double *out1,
                double m0);
 int sm_eo_cg(sm_ctx *ctx, const double *phi0, const double *phi1, double *x0, double *x1, double m0, double tol,

@@ -239,6 +239,20 @@ int exchange_ghost_U(sm_ctx *c) {
     return SM_OK;
 }
 
+
+// alpha / beta from per-block partials (local sum, all-reduce over shards, scalar)
+int cg_scalar(sm_ctx *c, int nparts, int which) {
+    if (c->nshard == 1) {
+        if (which == 0) launch_cg_alpha(c->stream, nparts, c->partials, c->sc);
+        else launch_cg_beta(c->stream, nparts, c->partials, c->sc);
+        return SM_OK;
+    }
+    launch_sum_to_scalar(c->stream, nparts, c->partials, c->sc);
+    TRY(allreduce_dev(c, (double *)&c->sc->sum, 2));
+    if (which == 0) launch_cg_alpha_from_sum(c->stream, c->sc);
+    else launch_cg_beta_from_sum(c->stream, c->sc);
+    return SM_OK;
+}
 }  // namespace sm_host
 
 // ============================================================================
@@ -422,7 +436,7 @@ int sm_destroy(sm_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
     void *dev[] = {c->U, c->ghostU, c->fields, c->faces, c->faces2, c->partials, c->sums, c->Fbuf, c->sc,
-                   c->counters, c->U_alt, c->Pmd, c->Fmd, c->eo, c->Ucb};
+                   c->counters, c->U_alt, c->Pmd, c->Fmd, c->eo, c->Ucb, c->eo_faces};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_sc) (void)hipHostFree(c->h_sc);
@@ -582,19 +596,6 @@ int sm_cg_begin(sm_ctx *c, const double *phi, double *x, double m0, double tol) 
     return SM_OK;
 }
 
-// alpha / beta from per-block partials (local sum, all-reduce over shards, scalar)
-static int cg_scalar(sm_ctx *c, int nparts, int which) {
-    if (c->nshard == 1) {
-        if (which == 0) launch_cg_alpha(c->stream, nparts, c->partials, c->sc);
-        else launch_cg_beta(c->stream, nparts, c->partials, c->sc);
-        return SM_OK;
-    }
-    launch_sum_to_scalar(c->stream, nparts, c->partials, c->sc);
-    TRY(allreduce_dev(c, (double *)&c->sc->sum, 2));
-    if (which == 0) launch_cg_alpha_from_sum(c->stream, c->sc);
-    else launch_cg_beta_from_sum(c->stream, c->sc);
-    return SM_OK;
-}
 
 // One pass of the one-pass CG (sm_cgfused.hip: cg_onepass_kernel): pass j
 // reads the j-1 fields (d, r, Ad), writes the j fields into the other

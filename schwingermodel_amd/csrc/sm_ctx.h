@@ -89,6 +89,7 @@ struct sm_ctx {
     // even-odd action (sm_eo.cpp; allocated on first use)
     double2 *eo = nullptr;          // checkerboard work vectors, V complex each
     double2 *Ucb = nullptr;         // gauge field in checkerboard layout (even, odd)
+    double2 *eo_faces = nullptr;    // t-sharded: checkerboard face slots (sm_eo.cpp)
     int eo_fused = 1;               // Dhat as one fused marching pass (0: two hop launches)
     // active CG
     double cg_mass = 0.0;
@@ -145,6 +146,8 @@ const double2 *loU(sm_ctx *c);
 int apply(sm_ctx *c, const double2 *in, double2 *out, double mass, int dagger, const double2 *aux,
           double2 *partials, const CGScalars *skip);
 int global_sum(sm_ctx *c, int nparts, const double2 *part, int slot);
+// alpha (which = 0) / beta (1) from per-block partials: local sum, all-reduce, scalar
+int cg_scalar(sm_ctx *c, int nparts, int which);
 int check_ready(sm_ctx *c);
 int upload_plane_pair(sm_ctx *c, double2 *dst, const double *p0, const double *p1);
 int download_plane_pair(sm_ctx *c, const double2 *src, double *p0, double *p1);

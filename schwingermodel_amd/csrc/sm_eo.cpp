@@ -17,7 +17,9 @@
 // (src/dirac_operator.cpp:486-580; sm_force_dev) gives it, plus the gauge force.
 // With H the hopping bracket (D = m - 0.5 H): D_oe v = -0.5 H_oe v and
 //     Dhat v = m v + (0.5/m) H_eo (D_oe v),   l_o = (0.5/m) H'_oe X, r_o = (0.5/m) H_oe Y.
-// Kernels: sm_eo.hip. One shard only (t-sharded checkerboard faces are next).
+// Kernels: sm_eo.hip. t-sharded like the full operator: every hop exchanges
+// the 2-column checkerboard faces of its input (and, once per gauge field,
+// of both link parities) with the t +- 1 shards; dots are all-reduced.
 #include <cmath>
 
 #include "sm_ctx.h"
@@ -35,45 +37,87 @@ enum { EO_X, EO_R, EO_D, EO_AD, EO_T, EO_W, EO_PHI, EO_Y, EO_CHI, EO_LO, EO_RO, 
 static double2 *eo_vec(sm_ctx *c, int i) { return c->eo + (size_t)i * c->g.V; }
 static double2 *ucb(sm_ctx *c, int parity) { return c->Ucb + (size_t)parity * c->g.V; }
 
+// t-sharded: face slots of 8*Nx complex ([side][plane][col][x], sm_eo.hip):
+// 0 send staging, 1 / 2 received faces of the even / odd links, 3 / 4 of the
+// two vectors a hop sequence has in flight.
+enum { EOF_SEND, EOF_UE, EOF_UO, EOF_V, EOF_W, EOF_N };
+static double2 *eo_face(sm_ctx *c, int slot) { return c->eo_faces + (size_t)slot * 8 * c->g.Nx; }
+
+// Exchange the checkerboard t-faces of f into face slot `slot`; returns the
+// received faces (null on one shard: the kernels wrap periodically).
+static int eo_halo(sm_ctx *c, const double2 *f, int slot, const double2 **out) {
+    *out = nullptr;
+    if (c->nshard == 1) return SM_OK;
+    double2 *snd = eo_face(c, EOF_SEND), *rcv = eo_face(c, slot);
+    const size_t half = (size_t)4 * c->g.Nx;  // complex per side
+    launch_pack_cb_faces(c->stream, c->g, f, snd);
+    TRY(exchange_faces_on(c, c->stream, snd, snd + half, rcv, rcv + half, 2 * half));
+    *out = rcv;
+    return SM_OK;
+}
+
+static EoFaces u_faces(sm_ctx *c) {
+    EoFaces f;
+    if (c->nshard > 1) {
+        f.ue = eo_face(c, EOF_UE);
+        f.uo = eo_face(c, EOF_UO);
+    }
+    return f;
+}
+
 int eo_ready(sm_ctx *c) {
-    if (c->nshard != 1) return fail(SM_ERR_ARG, "even-odd preconditioning needs one shard (nshard = %d)", c->nshard);
-    // the periodic lattice is bipartite (a checkerboard) only for even Nx and Nt
+    // the periodic lattice is bipartite (a checkerboard) only for even Nx and
+    // Nt; t-shards of even width keep every t0 even (local parity = global)
     if (c->g.Wt % 2 || c->g.Nx % 2)
-        return fail(SM_ERR_ARG, "even-odd preconditioning needs even Nx and Nt (%d x %d)", c->g.Nx, c->g.Wt);
+        return fail(SM_ERR_ARG, "even-odd preconditioning needs even Nx and shard width (%d x %d)", c->g.Nx,
+                    c->g.Wt);
+    if (c->nshard > 1 && c->g.Wt < 4)
+        return fail(SM_ERR_ARG, "even-odd preconditioning needs t-shards at least 4 wide (Wt = %d)", c->g.Wt);
     if (!c->eo) {
         HIP_TRY(hipMalloc(&c->eo, sizeof(double2) * (size_t)EO_N * c->g.V));
         HIP_TRY(hipMalloc(&c->Ucb, sizeof(double2) * 2 * (size_t)c->g.V));
+        if (c->nshard > 1) HIP_TRY(hipMalloc(&c->eo_faces, sizeof(double2) * (size_t)EOF_N * 8 * c->g.Nx));
     }
     // checkerboard copy of the current gauge field (U changes between calls)
     launch_to_cb(c->stream, c->g, c->U, ucb(c, 0), ucb(c, 1));
     HIP_TRY(hipGetLastError());
+    const double2 *f;
+    TRY(eo_halo(c, ucb(c, 0), EOF_UE, &f));
+    TRY(eo_halo(c, ucb(c, 1), EOF_UO, &f));
     return SM_OK;
 }
 
 // out_e = Dhat v_e (dagger = 0) or Dhat^dag v_e (dagger = 1). Fused: both
 // hops in one marching pass (eo_dhat_fused_kernel), optionally with partials
 // of sum aux * conj(out); unfused (c->eo_fused == 0): two eo_hop launches
-// through EO_T, bitwise the same result.
-void eo_dhat(sm_ctx *c, int dagger, const double2 *v, double2 *out, double mass, const double2 *aux = nullptr,
-             double2 *partials = nullptr) {
+// through EO_T, bitwise the same result. t-sharded: v's faces go to slot
+// EOF_V first (and T's to EOF_W unfused). *nparts: the partial count.
+int eo_dhat(sm_ctx *c, int dagger, const double2 *v, double2 *out, double mass, const double2 *aux = nullptr,
+            double2 *partials = nullptr, int *nparts = nullptr) {
+    EoFaces f = u_faces(c);
+    TRY(eo_halo(c, v, EOF_V, &f.v));
     if (c->eo_fused) {
-        launch_eo_dhat_fused(c->stream, c->g, eo_fused_config(c->g), dagger, v, ucb(c, 0), ucb(c, 1), mass, out, aux,
-                             partials);
-        return;
+        const EoFusedCfg cfg = eo_fused_config(c->g);
+        launch_eo_dhat_fused(c->stream, c->g, cfg, dagger, v, ucb(c, 0), ucb(c, 1), mass, out, aux, partials, f);
+        if (nparts) *nparts = eo_fused_blocks(cfg);
+        return SM_OK;
     }
     double2 *T = eo_vec(c, EO_T);
-    launch_eo_hop(c->stream, c->g, dagger, 1, v, ucb(c, 1), ucb(c, 0), nullptr, 0.0, -0.5, T);   // D_oe v
-    launch_eo_hop(c->stream, c->g, dagger, 0, T, ucb(c, 0), ucb(c, 1), v, mass, 0.5 / mass, out);
+    launch_eo_hop(c->stream, c->g, dagger, 1, v, ucb(c, 1), ucb(c, 0), nullptr, 0.0, -0.5, T, f.v, f.ue);  // D_oe v
+    const double2 *tf;
+    TRY(eo_halo(c, T, EOF_W, &tf));
+    launch_eo_hop(c->stream, c->g, dagger, 0, T, ucb(c, 0), ucb(c, 1), v, mass, 0.5 / mass, out, tf, f.uo);
     if (aux) launch_dot_partial(c->stream, c->g.V, aux, out, partials);
+    if (nparts) *nparts = reduce_blocks(c->g.V);
+    return SM_OK;
 }
 
 // out = Dhat Dhat^dag v (uses EO_W; EO_T unfused); dot partials of <v, out>
 // into c->partials; returns their count.
-static int eo_M(sm_ctx *c, const double2 *v, double2 *out, double mass) {
+static int eo_M(sm_ctx *c, const double2 *v, double2 *out, double mass, int *nparts) {
     double2 *W = eo_vec(c, EO_W);
-    eo_dhat(c, 1, v, W, mass);
-    eo_dhat(c, 0, W, out, mass, v, c->partials);
-    return c->eo_fused ? eo_fused_blocks(eo_fused_config(c->g)) : reduce_blocks(c->g.V);
+    TRY(eo_dhat(c, 1, v, W, mass));
+    return eo_dhat(c, 0, W, out, mass, v, c->partials, nparts);
 }
 
 // CG on Dhat Dhat^dag x = b (x0 = b, the reference's convention), the
@@ -83,19 +127,28 @@ int eo_cg(sm_ctx *c, const double2 *b, double2 *x, double mass, double tol, int 
     const int nparts = reduce_blocks(n);
     double2 *r = eo_vec(c, EO_R), *d = eo_vec(c, EO_D), *Ad = eo_vec(c, EO_AD);
     if (x != b) launch_copy(c->stream, n, b, x);
-    eo_M(c, x, Ad, mass);                                   // (its dot partials are not used)
+    int np;
+    TRY(eo_M(c, x, Ad, mass, &np));                          // (its dot partials are not used)
     double2 *prr = c->partials, *ppp = c->partials + nparts;
     launch_cg_init(c->stream, n, b, Ad, r, d, prr, ppp);
-    launch_cg_finalize_init(c->stream, nparts, prr, ppp, c->sc, tol);
+    if (c->nshard == 1) {
+        launch_cg_finalize_init(c->stream, nparts, prr, ppp, c->sc, tol);
+    } else {
+        launch_sum_partials(c->stream, nparts, prr, c->sums);
+        launch_sum_partials(c->stream, nparts, ppp, c->sums + 1);
+        TRY(allreduce_dev(c, (double *)c->sums, 4));
+        launch_cg_init_from_sums(c->stream, c->sums, c->sc, tol);
+    }
+    // every rank takes the same decisions: the status read back is global
     CgChunker plan;
     int issued = 0, chunk = plan.chunk;
     while (issued < max_iter) {
         const int nb = (max_iter - issued) < chunk ? (max_iter - issued) : chunk;
         for (int i = 0; i < nb; ++i) {
-            const int np = eo_M(c, d, Ad, mass);                     // Ad and partials of <d, Ad>
-            launch_cg_alpha(c->stream, np, c->partials, c->sc);
+            TRY(eo_M(c, d, Ad, mass, &np));                          // Ad and partials of <d, Ad>
+            TRY(cg_scalar(c, np, 0));                                // alpha
             launch_cg_update_xr(c->stream, n, x, r, d, Ad, c->sc, c->partials);
-            launch_cg_beta(c->stream, nparts, c->partials, c->sc);
+            TRY(cg_scalar(c, nparts, 1));                            // stop test, beta
             launch_cg_update_d(c->stream, n, d, r, c->sc);
         }
         HIP_TRY(hipGetLastError());
@@ -125,9 +178,13 @@ int eo_md_force(sm_ctx *c, const sm_hmc_params *p, const double2 *phi_full, doub
     double2 *lo = eo_vec(c, EO_LO), *ro = eo_vec(c, EO_RO);
     eo_take_even(c, phi_full, phie);
     TRY(eo_cg(c, phie, X, m, p->cg_tol, p->cg_max_iter, res));
-    eo_dhat(c, 1, X, Y, m);                                                             // Y = Dhat^dag X
-    launch_eo_hop(c->stream, c->g, 1, 1, X, ucb(c, 1), ucb(c, 0), nullptr, 0.0, 0.5 / m, lo);  // l_o
-    launch_eo_hop(c->stream, c->g, 0, 1, Y, ucb(c, 1), ucb(c, 0), nullptr, 0.0, 0.5 / m, ro);  // r_o
+    TRY(eo_dhat(c, 1, X, Y, m));                                                        // Y = Dhat^dag X
+    const EoFaces f = u_faces(c);
+    const double2 *xf, *yf;
+    TRY(eo_halo(c, X, EOF_V, &xf));
+    launch_eo_hop(c->stream, c->g, 1, 1, X, ucb(c, 1), ucb(c, 0), nullptr, 0.0, 0.5 / m, lo, xf, f.ue);  // l_o
+    TRY(eo_halo(c, Y, EOF_V, &yf));
+    launch_eo_hop(c->stream, c->g, 0, 1, Y, ucb(c, 1), ucb(c, 0), nullptr, 0.0, 0.5 / m, ro, yf, f.ue);  // r_o
     double2 *L = c->field(F_L), *R = c->field(F_RR);
     launch_from_cb(c->stream, c->g, X, lo, L);
     launch_from_cb(c->stream, c->g, Y, ro, R);
@@ -157,7 +214,7 @@ int eo_pseudofermion(sm_ctx *c, const sm_hmc_params *p, const double2 *chi_full,
     TRY(eo_ready(c));
     double2 *chie = eo_vec(c, EO_CHI), *phie = eo_vec(c, EO_PHI);
     eo_take_even(c, chi_full, chie);
-    eo_dhat(c, 0, chie, phie, p->m0 + 2);
+    TRY(eo_dhat(c, 0, chie, phie, p->m0 + 2));
     launch_from_cb(c->stream, c->g, phie, nullptr, phi_full);
     HIP_TRY(hipGetLastError());
     return SM_OK;
@@ -177,7 +234,7 @@ int sm_eo_dhat(sm_ctx *c, int dagger, const double *in0, const double *in1, doub
     TRY(upload_plane_pair(c, in, in0, in1));
     double2 *ve = eo_vec(c, EO_CHI), *oe = eo_vec(c, EO_X);
     eo_take_even(c, in, ve);
-    eo_dhat(c, dagger ? 1 : 0, ve, oe, m0 + 2);
+    TRY(eo_dhat(c, dagger ? 1 : 0, ve, oe, m0 + 2));
     launch_from_cb(c->stream, c->g, oe, nullptr, out);
     HIP_TRY(hipGetLastError());
     return download_plane_pair(c, out, out0, out1);

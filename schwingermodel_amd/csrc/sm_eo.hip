@@ -15,6 +15,13 @@
 // eo_hop computes  out_p = a * aux_p + b * H_{p,q} in_q  for one parity, with
 // the reference's bracket arithmetic (a = 0, b = -0.5 reproduces D on an
 // input that vanishes on parity p bit for bit).
+//
+// t-sharded (SH = 1): a checkerboard field's t-faces are its k = 0, 1 columns
+// (sent down) and k = Wh-2, Wh-1 columns (sent up), both parities of the
+// global checkerboard agreeing with the local one because t0 is even. The
+// received faces of one field are laid out [side][plane][col][x] (side 0: the
+// down-neighbour's k = Wh-2+col, i.e. my k = col-2; side 1: the
+// up-neighbour's k = col, i.e. my k = Wh+col), 8*Nx complex.
 #include "sm_device.h"
 #include "sm_internal.h"
 
@@ -39,6 +46,21 @@ __global__ void __launch_bounds__(256) to_cb_kernel(EoGeom g, const double2 *ful
     }
 }
 
+__device__ __forceinline__ long cb_face_at(int Nx, int side, int plane, int col, int x) {
+    return (long)((side * 2 + plane) * 2 + col) * Nx + x;
+}
+
+// pack the t-faces of a checkerboard field into [side][plane][col][x]
+__global__ void __launch_bounds__(256) pack_cb_faces_kernel(EoGeom g, const double2 *f, double2 *out) {
+    const int n = 8 * g.Nx;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int x = i % g.Nx, r = i / g.Nx;
+        const int col = r & 1, plane = (r >> 1) & 1, side = r >> 2;
+        const int k = side ? g.Wh - 2 + col : col;
+        out[i] = f[plane * g.Vh + (long)x * g.Wh + k];
+    }
+}
+
 __global__ void __launch_bounds__(256) from_cb_kernel(EoGeom g, const double2 *e, const double2 *o, double2 *full) {
     for (long n = (long)blockIdx.x * blockDim.x + threadIdx.x; n < g.V; n += (long)gridDim.x * blockDim.x) {
         const int x = (int)(n / g.Wt), t = (int)(n - (long)x * g.Wt);
@@ -52,27 +74,46 @@ __global__ void __launch_bounds__(256) from_cb_kernel(EoGeom g, const double2 *e
 // out_p = a*aux_p + b*H in_q for the sites of parity p (one shard: periodic
 // x, periodic t with the antiperiodic sign on the global t boundary).
 // Up: U of parity p (plane 0 U_t, plane 1 U_x); Uq: U of parity q = 1-p.
-template <int DAG>
+// SH = 1: t-neighbours beyond the shard come from the received faces of `in`
+// (inf) and of Uq (uqf).
+template <int DAG, int SH>
 __global__ void __launch_bounds__(256) eo_hop_kernel(EoGeom g, int p, const double2 *in, const double2 *Up,
                                                      const double2 *Uq, const double2 *aux, double a, double b,
-                                                     double2 *out) {
+                                                     double2 *out, const double2 *inf, const double2 *uqf) {
     const long Vh = g.Vh;
     for (long h = (long)blockIdx.x * blockDim.x + threadIdx.x; h < Vh; h += (long)gridDim.x * blockDim.x) {
         const int x = (int)(h / g.Wh), k = (int)(h - (long)x * g.Wh);
         const int s = (p + x) & 1;
         const int t = 2 * k + s;
         int kp = k + s, km = k + s - 1;            // t+1, t-1 in the opposite parity's row
-        if (kp == g.Wh) kp = 0;
-        if (km < 0) km = g.Wh - 1;
         const int xp = x + 1 == g.Nx ? 0 : x + 1, xm = x == 0 ? g.Nx - 1 : x - 1;
         const long row = (long)x * g.Wh;
-        const long it = row + kp, im = row + km, ixp = (long)xp * g.Wh + k, ixm = (long)xm * g.Wh + k;
+        const long ixp = (long)xp * g.Wh + k, ixm = (long)xm * g.Wh + k;
+        double2 pt0, pt1, pm0, pm1, um;
+        if (SH && kp == g.Wh) {                    // up-neighbour's k = 0
+            pt0 = inf[cb_face_at(g.Nx, 1, 0, 0, x)];
+            pt1 = inf[cb_face_at(g.Nx, 1, 1, 0, x)];
+        } else {
+            if (kp == g.Wh) kp = 0;
+            pt0 = in[row + kp];
+            pt1 = in[row + kp + Vh];
+        }
+        if (SH && km < 0) {                        // down-neighbour's k = Wh-1
+            pm0 = inf[cb_face_at(g.Nx, 0, 0, 1, x)];
+            pm1 = inf[cb_face_at(g.Nx, 0, 1, 1, x)];
+            um = uqf[cb_face_at(g.Nx, 0, 0, 1, x)];
+        } else {
+            if (km < 0) km = g.Wh - 1;
+            pm0 = in[row + km];
+            pm1 = in[row + km + Vh];
+            um = Uq[row + km];
+        }
         const int tg = g.t0 + t;
         const double sr0 = tg == g.Ntg - 1 ? -1.0 : 1.0;
         const double sl0 = tg == 0 ? -1.0 : 1.0;
         double2 h0, h1;
-        dirac_bracket<DAG>(sr0, sl0, in[it], in[it + Vh], in[ixp], in[ixp + Vh], in[im], in[im + Vh], in[ixm],
-                           in[ixm + Vh], Up[h], Up[h + Vh], Uq[im], Uq[ixm + Vh], h0, h1);
+        dirac_bracket<DAG>(sr0, sl0, pt0, pt1, in[ixp], in[ixp + Vh], pm0, pm1, in[ixm], in[ixm + Vh], Up[h],
+                           Up[h + Vh], um, Uq[ixm + Vh], h0, h1);
         double2 o0 = rmul(b, h0), o1 = rmul(b, h1);
         if (aux) {
             o0 = cadd(rmul(a, aux[h]), o0);
@@ -96,6 +137,7 @@ constexpr int EW = 60;
 
 struct EoFArgs {
     const double2 *v, *Ue, *Uo;
+    const double2 *vf, *uef, *uof;   // received t-faces (SH = 1)
     double2 *out;
     const double2 *aux;
     double2 *partials;
@@ -109,7 +151,7 @@ struct ERow {                // one lane, one row: even input, even / odd links 
 };
 
 
-template <int DAG, int EPI>
+template <int DAG, int EPI, int SH>
 __global__ void __launch_bounds__(256) eo_dhat_fused_kernel(EoFArgs a) {
     __shared__ double2 sh[4];
     const int tb = blockIdx.x % a.TBk, xc = blockIdx.x / a.TBk;
@@ -124,19 +166,37 @@ __global__ void __launch_bounds__(256) eo_dhat_fused_kernel(EoFArgs a) {
         int kw = k % Wh;
         if (kw < 0) kw += Wh;                                  // periodic in t (one shard)
         const bool own = lane >= 2 && lane < EW + 2 && k < Wh;
+        // sharded: lanes outside the shard read the received faces
+        const bool inside = k >= 0 && k < Wh;
+        const int side = k < 0 ? 0 : 1;
+        const int col = k < 0 ? k + 2 : min(k - Wh, 1);
         const double m = a.mass, hm = 0.5 / a.mass;
         auto wrapx = [Nx](int x) { int w = x % Nx; return w < 0 ? w + Nx : w; };
         auto load = [&](int y, ERow &R) {
-            const long h = (long)wrapx(y) * Wh + kw;
-            R.v0 = a.v[h];
-            R.v1 = a.v[h + Vh];
-            R.et = a.Ue[h];
-            R.ex = a.Ue[h + Vh];
-            R.ot = a.Uo[h];
-            R.ox = a.Uo[h + Vh];
+            if (!SH || inside) {
+                const long h = (long)wrapx(y) * Wh + kw;
+                R.v0 = a.v[h];
+                R.v1 = a.v[h + Vh];
+                R.et = a.Ue[h];
+                R.ex = a.Ue[h + Vh];
+                R.ot = a.Uo[h];
+                R.ox = a.Uo[h + Vh];
+            } else {
+                const long f0 = cb_face_at(Nx, side, 0, col, wrapx(y)), f1 = f0 + 2 * Nx;
+                R.v0 = a.vf[f0];
+                R.v1 = a.vf[f1];
+                R.et = a.uef[f0];
+                R.ex = a.uef[f1];
+                R.ot = a.uof[f0];
+                R.ox = a.uof[f1];
+            }
         };
+        // t: local, unwrapped (halo lanes of shard 0 / the last shard wrap
+        // to the other end of the global lattice)
         auto signs = [&](int t, double &sr0, double &sl0) {
-            const int tg = a.g.t0 + t;
+            int tg = a.g.t0 + t;
+            if (tg < 0) tg += a.g.Ntg;
+            else if (tg >= a.g.Ntg) tg -= a.g.Ntg;
             sr0 = tg == a.g.Ntg - 1 ? -1.0 : 1.0;
             sl0 = tg == 0 ? -1.0 : 1.0;
         };
@@ -155,7 +215,7 @@ __global__ void __launch_bounds__(256) eo_dhat_fused_kernel(EoFArgs a) {
                 utm = dpp_shr1(Rc.et);
             }
             double sr0, sl0;
-            signs(2 * kw + (ye ? 1 : 0), sr0, sl0);
+            signs(2 * k + (ye ? 1 : 0), sr0, sl0);
             double2 h0, h1;
             dirac_bracket<DAG>(sr0, sl0, pp.a, pp.b, vxp.a, vxp.b, pm.a, pm.b, vxm.a, vxm.b, Rc.ot, Rc.ox, utm, ex_m,
                                h0, h1);
@@ -177,7 +237,7 @@ __global__ void __launch_bounds__(256) eo_dhat_fused_kernel(EoFArgs a) {
                 utm = Rc.ot;
             }
             double sr0, sl0;
-            signs(2 * kw + (xe_ ? 0 : 1), sr0, sl0);
+            signs(2 * k + (xe_ ? 0 : 1), sr0, sl0);
             double2 h0, h1;
             dirac_bracket<DAG>(sr0, sl0, pp.a, pp.b, Txp.a, Txp.b, pm.a, pm.b, Txm.a, Txm.b, Rc.et, Rc.ex, utm, ox_m,
                                h0, h1);
@@ -274,31 +334,56 @@ EoFusedCfg eo_fused_config(const Geometry &g) {
 
 int eo_fused_blocks(const EoFusedCfg &c) { return c.TBk * c.XB; }
 
+void launch_pack_cb_faces(hipStream_t s, const Geometry &g, const double2 *f, double2 *out) {
+    hipLaunchKernelGGL(pack_cb_faces_kernel, dim3((8 * g.Nx + 255) / 256), dim3(256), 0, s, eo_geom(g), f, out);
+}
+
 void launch_eo_dhat_fused(hipStream_t s, const Geometry &g, const EoFusedCfg &c, int dagger, const double2 *v,
                           const double2 *Ue, const double2 *Uo, double mass, double2 *out, const double2 *aux,
-                          double2 *partials) {
+                          double2 *partials, const EoFaces &f) {
     EoFArgs a;
     a.v = v; a.Ue = Ue; a.Uo = Uo; a.out = out; a.aux = aux; a.partials = partials;
+    a.vf = f.v; a.uef = f.ue; a.uof = f.uo;
     a.g = eo_geom(g);
     a.xchunk = c.xchunk; a.NWT = c.NWT; a.TBk = c.TBk; a.XB = c.XB;
     a.mass = mass;
     const dim3 grid(c.TBk * c.XB), block(256);
-    if (dagger) {
-        if (aux) hipLaunchKernelGGL((eo_dhat_fused_kernel<1, EPI_DOT>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((eo_dhat_fused_kernel<1, EPI_NONE>), grid, block, 0, s, a);
+#define SM_EO_LAUNCH(D, E, H) hipLaunchKernelGGL((eo_dhat_fused_kernel<D, E, H>), grid, block, 0, s, a)
+    if (f.v) {
+        if (dagger) {
+            if (aux) SM_EO_LAUNCH(1, EPI_DOT, 1);
+            else SM_EO_LAUNCH(1, EPI_NONE, 1);
+        } else {
+            if (aux) SM_EO_LAUNCH(0, EPI_DOT, 1);
+            else SM_EO_LAUNCH(0, EPI_NONE, 1);
+        }
     } else {
-        if (aux) hipLaunchKernelGGL((eo_dhat_fused_kernel<0, EPI_DOT>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((eo_dhat_fused_kernel<0, EPI_NONE>), grid, block, 0, s, a);
+        if (dagger) {
+            if (aux) SM_EO_LAUNCH(1, EPI_DOT, 0);
+            else SM_EO_LAUNCH(1, EPI_NONE, 0);
+        } else {
+            if (aux) SM_EO_LAUNCH(0, EPI_DOT, 0);
+            else SM_EO_LAUNCH(0, EPI_NONE, 0);
+        }
     }
+#undef SM_EO_LAUNCH
 }
 
 void launch_eo_hop(hipStream_t s, const Geometry &g, int dagger, int p, const double2 *in, const double2 *Up,
-                   const double2 *Uq, const double2 *aux, double a, double b, double2 *out) {
+                   const double2 *Uq, const double2 *aux, double a, double b, double2 *out, const double2 *inf,
+                   const double2 *uqf) {
     const EoGeom e = eo_geom(g);
-    if (dagger)
-        hipLaunchKernelGGL(eo_hop_kernel<1>, dim3(eo_grid(e.Vh)), dim3(256), 0, s, e, p, in, Up, Uq, aux, a, b, out);
-    else
-        hipLaunchKernelGGL(eo_hop_kernel<0>, dim3(eo_grid(e.Vh)), dim3(256), 0, s, e, p, in, Up, Uq, aux, a, b, out);
+    const dim3 grid(eo_grid(e.Vh)), block(256);
+#define SM_EO_HOP(D, H) \
+    hipLaunchKernelGGL((eo_hop_kernel<D, H>), grid, block, 0, s, e, p, in, Up, Uq, aux, a, b, out, inf, uqf)
+    if (inf) {
+        if (dagger) SM_EO_HOP(1, 1);
+        else SM_EO_HOP(0, 1);
+    } else {
+        if (dagger) SM_EO_HOP(1, 0);
+        else SM_EO_HOP(0, 0);
+    }
+#undef SM_EO_HOP
 }
 
 }  // namespace sm

@@ -143,9 +143,17 @@ void launch_draw_gauge(hipStream_t s, const Geometry &g, uint64_t seed, double s
 // ---- even-odd checkerboard (sm_eo.hip) ----
 void launch_to_cb(hipStream_t s, const Geometry &g, const double2 *full, double2 *e, double2 *o);
 void launch_from_cb(hipStream_t s, const Geometry &g, const double2 *e, const double2 *o, double2 *full);
-// out_p = a*aux_p + b*H in_q (H: the hopping bracket of D / D^dag), parity p
+// Received t-faces of checkerboard fields ([side][plane][col][x], 8*Nx
+// complex each; sm_eo.hip); all null on one shard (periodic wrap).
+struct EoFaces {
+    const double2 *v = nullptr, *ue = nullptr, *uo = nullptr;
+};
+void launch_pack_cb_faces(hipStream_t s, const Geometry &g, const double2 *f, double2 *out);
+// out_p = a*aux_p + b*H in_q (H: the hopping bracket of D / D^dag), parity p;
+// inf / uqf: faces of `in` and Uq when t-sharded (else null)
 void launch_eo_hop(hipStream_t s, const Geometry &g, int dagger, int p, const double2 *in, const double2 *Up,
-                   const double2 *Uq, const double2 *aux, double a, double b, double2 *out);
+                   const double2 *Uq, const double2 *aux, double a, double b, double2 *out,
+                   const double2 *inf = nullptr, const double2 *uqf = nullptr);
 // Fused Dhat / Dhat^dag (both hops in one marching pass); aux != null adds
 // per-block partials of sum aux * conj(out) (eo_fused_blocks of them).
 struct EoFusedCfg {
@@ -155,7 +163,7 @@ EoFusedCfg eo_fused_config(const Geometry &g);
 int eo_fused_blocks(const EoFusedCfg &c);
 void launch_eo_dhat_fused(hipStream_t s, const Geometry &g, const EoFusedCfg &c, int dagger, const double2 *v,
                           const double2 *Ue, const double2 *Uo, double mass, double2 *out, const double2 *aux,
-                          double2 *partials);
+                          double2 *partials, const EoFaces &f);
 
 // Pack the t = 0 and t = Wt-1 columns (both planes) into contiguous faces.
 void launch_pack_faces(hipStream_t s, const Geometry &g, const double2 *field, double2 *lo_face,

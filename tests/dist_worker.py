@@ -11,6 +11,9 @@ mode "oracle" (CPU, gloo): every rank applies the ORACLE's local operator to its
 mode "md" (one GPU, gloo host transport): the molecular-dynamics layer
     (plaquette, staples, gauge force, MD force, Hamiltonian, leapfrog, one HMC
     trajectory) on t-shards vs the reference's MD fixture / one shard.
+mode "eo" (one GPU, gloo host transport): the even-odd preconditioned layer
+    (Dhat, Dhat^dag, half-lattice CG, MD force, one HMC trajectory) on
+    t-shards with checkerboard faces vs one shard.
 mode "gpu" (one GPU shared by all ranks, gloo host transport): every rank runs
     the HIP kernels on its shard through sm_create_hosted (same kernels, face
     packing, ghost links, sign ownership and scalar reductions as the RCCL
@@ -187,6 +190,88 @@ def run_md(name, result_path, dist, rank, world):
     dist.destroy_process_group()
 
 
+def eo_ops(sm, ctx, V, fields, m0, prm):
+    """The even-odd layer on one context (one shard or a t-shard): Dhat and
+    Dhat^dag of psi, the half-lattice CG, the even-odd MD force and one
+    even-odd HMC trajectory (which leaves U changed). `fields` = (U, psi, phi)
+    as plane pairs of this context's block."""
+    P_ = lambda x: ctypes.c_void_p(x.ctypes.data)  # noqa: E731
+    (U0, U1), (p0, p1), (f0, f1) = fields
+    out = {}
+    for key, dag in (("dhat", 0), ("dhatdag", 1)):
+        o0, o1 = np.empty(V, complex), np.empty(V, complex)
+        sm.check(sm.lib.sm_eo_dhat(ctx, dag, P_(p0), P_(p1), P_(o0), P_(o1), m0))
+        out[key] = (o0, o1)
+    x0, x1 = np.empty(V, complex), np.empty(V, complex)
+    res = sm.CGResult()
+    sm.check(sm.lib.sm_eo_cg(ctx, P_(p0), P_(p1), P_(x0), P_(x1), m0, 1e-10, 10000, ctypes.byref(res)))
+    out["cgx"] = (x0, x1)
+    out["cg"] = (res.converged, res.iterations)
+    G0, G1 = np.empty(V), np.empty(V)
+    sm.check(sm.lib.sm_md_force(ctx, ctypes.byref(prm), P_(f0), P_(f1), P_(G0), P_(G1), ctypes.byref(res)))
+    out["force"] = (G0, G1)
+    r = sm.HMCResult()
+    sm.check(sm.lib.sm_hmc_trajectory(ctx, ctypes.byref(prm), 5, ctypes.byref(r)))
+    Ua, Ub = np.empty(V, complex), np.empty(V, complex)
+    sm.check(sm.lib.sm_download_gauge(ctx, P_(Ua), P_(Ub)))
+    out["traj"] = (r.dH, r.accepted, r.r)
+    out["traj_U"] = (Ua, Ub)
+    return out
+
+
+def run_eo(name, result_path, dist, rank, world):
+    """mode "eo": the even-odd preconditioned layer on t-shards (hosted
+    transport, checkerboard faces) vs the same calls on one shard.
+    name = gen:<Nx>x<Nt>:<sigma>:<m0> (synthetic fields)."""
+    import schwingermodel_amd as sm
+    from schwingermodel_amd import dist as smd
+    _, dims, sigma, m0s = name.split(":")
+    Nx, Nt = (int(v) for v in dims.split("x"))
+    sigma, m0 = float(sigma), float(m0s)
+    S = Nx * Nt
+    g = {k: np.empty(4 * S) for k in ("U", "psi", "phi")}
+    sm.lib.sm_fill_gauge(4321, sigma, Nt, 0, Nx, 0, Nt, g["U"].ctypes.data, g["U"][2 * S:].ctypes.data)
+    sm.lib.sm_fill_spinor(5678, Nt, 0, Nx, 0, Nt, g["psi"].ctypes.data, g["psi"][2 * S:].ctypes.data)
+    sm.lib.sm_fill_spinor(1357, Nt, 0, Nx, 0, Nt, g["phi"].ctypes.data, g["phi"][2 * S:].ctypes.data)
+    prm = sm.HMCParams(m0, 2.0, 0.5, 6, 1e-10, 10000, 77, 1)
+    t0, Wt = ctypes.c_int(), ctypes.c_int()
+    sm.check(sm.lib.sm_shard_plan(Nt, world, rank, ctypes.byref(t0), ctypes.byref(Wt)))
+    t0, Wt = t0.value, Wt.value
+    V = Nx * Wt
+    mine = [shard_field(g[k], Nx, Nt, t0, Wt) for k in ("U", "psi", "phi")]
+    dev = int(os.environ.get("SM_DEVICE", "0"))
+    ctx, tr = smd.create_hosted_context(Nx, Nt, device=dev)
+    sm.check(sm.lib.sm_upload_gauge(ctx, ctypes.c_void_p(mine[0][0].ctypes.data),
+                                    ctypes.c_void_p(mine[0][1].ctypes.data)))
+    local = eo_ops(sm, ctx, V, mine, m0, prm)
+    sm.lib.sm_destroy(ctx)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, local)
+    if rank == 0:
+        L = sm.Lattice(Nx, Nt, device=dev)
+        full = [shard_field(g[k], Nx, Nt, 0, Nt) for k in ("U", "psi", "phi")]
+        sm.check(sm.lib.sm_upload_gauge(L.ctx, ctypes.c_void_p(full[0][0].ctypes.data),
+                                        ctypes.c_void_p(full[0][1].ctypes.data)))
+        one = eo_ops(sm, L.ctx, S, full, m0, prm)
+        L.close()
+        from conftest import bits_equal
+        rep = {"world": world, "Wt": Wt, "checks": {}}
+        for key in ("dhat", "dhatdag", "cgx", "force", "traj_U"):
+            dtype = float if key == "force" else complex
+            gsh = unshard([d[key] for d in gathered], Nx, Nt, Wt, dtype)
+            ref = unshard([one[key]], Nx, Nt, Nt, dtype)
+            rep["checks"][key] = (bool(bits_equal(gsh, ref)) if key.startswith("dhat")
+                                  else float(np.linalg.norm(gsh - ref) / np.linalg.norm(ref)))
+        rep["cg"] = [list(d["cg"]) for d in gathered]
+        rep["cg_one"] = list(one["cg"])
+        rep["traj"] = [list(d["traj"]) for d in gathered]
+        rep["traj_one"] = list(one["traj"])
+        with open(result_path, "w") as f:
+            json.dump(rep, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     mode, name, result_path = sys.argv[1], sys.argv[2], sys.argv[3]
     import torch.distributed as dist
@@ -194,6 +279,8 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     if mode == "md":
         return run_md(name, result_path, dist, rank, world)
+    if mode == "eo":
+        return run_eo(name, result_path, dist, rank, world)
     from conftest import bits_equal, load_fixture
     import schwingermodel_amd as sm
     from schwingermodel_amd import dist as smd

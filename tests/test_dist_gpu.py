@@ -57,3 +57,33 @@ def test_sharded_md_matches_reference(tmp_path, fixture, world):
     assert abs(dH - t["single"][0]) <= 1e-6 * max(1.0, abs(t["single"][0]))
     assert acc == t["single"][1] and r == t["single"][2]
     assert t["U_rel"] <= 1e-8
+
+
+@pytest.mark.parametrize("fixture,world,fused", [("gen:32x48:0.4242:0.0", 2, "1"), ("gen:32x48:0.3:-0.1", 4, "1"),
+                                                 # the two-launch Dhat (eo_hop with faces)
+                                                 ("gen:32x48:0.3:-0.1", 4, "0"),
+                                                 # Wh = 128: three waves per strip, interior
+                                                 # waves without halo lanes
+                                                 ("gen:24x512:0.3246:-0.05", 2, "1")])
+def test_sharded_even_odd_matches_one_shard(tmp_path, fixture, world, fused):
+    """Even-odd layer on t-shards (checkerboard faces over the host transport)
+    vs one shard: Dhat / Dhat^dag bitwise (same per-element arithmetic), the
+    half-lattice CG to 1e-10 in the same iteration count (+-1 %), the MD force
+    to 1e-10, and an HMC trajectory with the same accept decision."""
+    rep = run_world("eo", fixture, world, tmp_path, timeout=600, extra_env={"SM_EO_FUSED": fused})
+    c = rep["checks"]
+    assert c["dhat"] is True and c["dhatdag"] is True, c
+    # the sharded dots sum per-shard partials: a different rounding order
+    # than one shard, amplified by the condition number along the solve
+    # (3e-12 measured at 32x48, m0 = -0.1); both solves reach |r| < 1e-10 |b|
+    assert c["cgx"] <= 1e-10, c
+    its = {it for conv, it in rep["cg"]}
+    assert len(its) == 1 and all(conv for conv, it in rep["cg"])
+    one = rep["cg_one"][1]
+    assert abs(its.pop() - one) <= max(1, one // 100)
+    assert c["force"] <= 1e-10, c
+    assert len({tuple(t) for t in rep["traj"]}) == 1
+    dH, acc, r = rep["traj"][0]
+    assert abs(dH - rep["traj_one"][0]) <= 1e-6 * max(1.0, abs(rep["traj_one"][0]))
+    assert acc == rep["traj_one"][1] and r == rep["traj_one"][2]
+    assert c["traj_U"] <= 1e-8, c
