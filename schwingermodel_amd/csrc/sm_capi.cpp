@@ -373,6 +373,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     if (const char *e = getenv("SM_CG_FUSED")) c->cg_fused = atoi(e);
     if (const char *e = getenv("SM_CG_INKERNEL_MAX_BLOCKS")) c->cg_inkernel_max_blocks = atoi(e);
     if (const char *e = getenv("SM_EO_FUSED")) c->eo_fused = atoi(e);
+    if (const char *e = getenv("SM_EO_CG_FOLDED")) c->eo_cg_folded = atoi(e);
     const int np = kMaxPartials;
     const size_t fb = sizeof(double2) * 2 * (size_t)c->g.V;
     hipError_t e = hipSuccess;

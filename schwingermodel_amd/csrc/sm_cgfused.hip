@@ -590,6 +590,15 @@ CGFusedCfg cg_fused_config(const Geometry &g) {
     if (nchunks > g.Nx) nchunks = g.Nx;
     if (nchunks < 1) nchunks = 1;
     c.xchunk = (g.Nx + nchunks - 1) / nchunks;
+    // mid-size lattices: at least min(12, Nx/64) rows per chunk, so the 4
+    // halo rows a chunk re-reads stay a small fraction (tools/tune_cg.py,
+    // one-pass ms per iteration: 512^2 8 rows 0.030 vs 1 row 0.039; 1024^2
+    // 12 rows 0.076 vs 2 rows 0.087; 2048^2 8-12 rows 0.27 vs 0.28). Small
+    // lattices keep one row per block (latency-bound: parallelism first).
+    if (g.Nx >= 512) {
+        const int xmin = g.Nx / 64 < 12 ? g.Nx / 64 : 12;
+        if (c.xchunk < xmin) c.xchunk = xmin;
+    }
     if (const char *e = getenv("SM_CGF_XCHUNK")) c.xchunk = atoi(e);
     c.XB = (g.Nx + c.xchunk - 1) / c.xchunk;
     c.remap = 1;

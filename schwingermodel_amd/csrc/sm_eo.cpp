@@ -32,15 +32,15 @@ using namespace sm_host;
 namespace sm_host {
 
 // eo work vectors (each one parity: 2 planes x V/2 = V complex)
-enum { EO_X, EO_R, EO_D, EO_AD, EO_T, EO_W, EO_PHI, EO_Y, EO_CHI, EO_LO, EO_RO, EO_N };
+enum { EO_X, EO_R, EO_D, EO_AD, EO_T, EO_W, EO_PHI, EO_Y, EO_CHI, EO_LO, EO_RO, EO_R2, EO_D2, EO_N };
 
 static double2 *eo_vec(sm_ctx *c, int i) { return c->eo + (size_t)i * c->g.V; }
 static double2 *ucb(sm_ctx *c, int parity) { return c->Ucb + (size_t)parity * c->g.V; }
 
 // t-sharded: face slots of 8*Nx complex ([side][plane][col][x], sm_eo.hip):
 // 0 send staging, 1 / 2 received faces of the even / odd links, 3 / 4 of the
-// two vectors a hop sequence has in flight.
-enum { EOF_SEND, EOF_UE, EOF_UO, EOF_V, EOF_W, EOF_N };
+// two vectors a hop sequence has in flight, 5 / 6 of r and Ad (folded CG).
+enum { EOF_SEND, EOF_UE, EOF_UO, EOF_V, EOF_W, EOF_R, EOF_A, EOF_N };
 static double2 *eo_face(sm_ctx *c, int slot) { return c->eo_faces + (size_t)slot * 8 * c->g.Nx; }
 
 // Exchange the checkerboard t-faces of f into face slot `slot`; returns the
@@ -120,9 +120,90 @@ static int eo_M(sm_ctx *c, const double2 *v, double2 *out, double mass, int *npa
     return eo_dhat(c, 0, W, out, mass, v, c->partials, nparts);
 }
 
+// Folded CG on Dhat Dhat^dag (c->eo_cg_folded, needs the fused Dhat): the
+// one-pass recurrence of the full CG (cg_onepass_kernel / cg1_scalars) on
+// half-lattice vectors. Iteration j = pass A (r_j, d_j, x; W = Dhat^dag d_j)
+// + pass B (Ad_j = Dhat W, <d_j,Ad_j>, <r_j,Ad_j>, |Ad_j|^2) + the scalar
+// kernel (stop test on the direct |r_j|^2, alpha_j, beta_j by the expansion).
+// 3 launches instead of 6, and r, Ad, d, x are not re-streamed by separate
+// BLAS-1 kernels: ~512 instead of 576 B per even site. r and d ping-pong.
+static int eo_cg_folded(sm_ctx *c, const double2 *b, double2 *x, double mass, double tol, int max_iter,
+                        sm_cg_result *res) {
+    const long n = c->g.V;
+    const int nred = reduce_blocks(n);
+    double2 *Ad = eo_vec(c, EO_AD), *W = eo_vec(c, EO_W);
+    double2 *rb[2] = {eo_vec(c, EO_R), eo_vec(c, EO_R2)}, *db[2] = {eo_vec(c, EO_D), eo_vec(c, EO_D2)};
+    if (x != b) launch_copy(c->stream, n, b, x);
+    int np;
+    TRY(eo_M(c, x, Ad, mass, &np));
+    double2 *prr = c->partials, *ppp = c->partials + nred;
+    launch_cg_init(c->stream, n, b, Ad, rb[0], db[0], prr, ppp);                // r_0 = b - M x_0; d_0 = r_0
+    if (c->nshard == 1) {
+        launch_cg_finalize_init(c->stream, nred, prr, ppp, c->sc, tol);
+    } else {
+        launch_sum_partials(c->stream, nred, prr, c->sums);
+        launch_sum_partials(c->stream, nred, ppp, c->sums + 1);
+        TRY(allreduce_dev(c, (double *)c->sums, 4));
+        launch_cg_init_from_sums(c->stream, c->sums, c->sc, tol);
+    }
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)&c->sc->max_iter, max_iter, 1, c->stream));
+    const EoFusedCfg cfg = eo_fused_config(c->g);
+    const int nparts = eo_fused_blocks(cfg);
+    const EoFaces uf = u_faces(c);
+    long j = 0;
+    auto pass = [&]() -> int {
+        const int o = j & 1;
+        EoCgPass q;
+        q.dold = db[o];
+        q.rold = rb[o];
+        q.dnew = db[1 - o];
+        q.rnew = rb[1 - o];
+        q.x = x;
+        q.W = W;
+        q.ad = Ad;
+        q.first = j == 0;
+        EoFaces f = uf;
+        TRY(eo_halo(c, q.dold, EOF_V, &f.v));
+        TRY(eo_halo(c, q.rold, EOF_R, &q.rf));
+        TRY(eo_halo(c, Ad, EOF_A, &q.af));
+        launch_eo_cg_pass(c->stream, c->g, cfg, 0, q, ucb(c, 0), ucb(c, 1), mass, f, c->sc, c->partials);
+        TRY(eo_halo(c, W, EOF_W, &q.wf));
+        launch_eo_cg_pass(c->stream, c->g, cfg, 1, q, ucb(c, 0), ucb(c, 1), mass, f, c->sc, c->partials);
+        if (c->nshard == 1) {
+            launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, q.first);
+        } else {
+            launch_cg1_local_sum(c->stream, nparts, c->partials, c->sc);
+            TRY(allreduce_dev(c, (double *)c->sc->sum3, 6));
+            launch_cg1_from_sums(c->stream, c->sc, q.first);
+        }
+        ++j;
+        return SM_OK;
+    };
+    // pass 0 forms Ad_0; pass j >= 1 completes iteration j (the device stops
+    // itself at convergence or k = max_iter); all ranks read the same status
+    const long passes = (long)max_iter + 1;
+    CgChunker plan;
+    int chunk = plan.chunk;
+    while (j < passes) {
+        const long nb = (passes - j) < chunk ? (passes - j) : chunk;
+        for (long i = 0; i < nb; ++i) TRY(pass());
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(c->h_sc, c->sc, sizeof(CGScalars), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (c->h_sc->done) break;
+        chunk = plan.next(c->h_sc->k, c->h_sc->err, tol * c->h_sc->phi_norm);
+    }
+    res->converged = c->h_sc->converged;
+    res->iterations = c->h_sc->k;
+    res->residual = c->h_sc->err;
+    res->phi_norm = c->h_sc->phi_norm;
+    return SM_OK;
+}
+
 // CG on Dhat Dhat^dag x = b (x0 = b, the reference's convention), the
 // reference's recurrence and stop test on half-lattice vectors.
 int eo_cg(sm_ctx *c, const double2 *b, double2 *x, double mass, double tol, int max_iter, sm_cg_result *res) {
+    if (c->eo_cg_folded && c->eo_fused) return eo_cg_folded(c, b, x, mass, tol, max_iter, res);
     const long n = c->g.V;  // complex entries of an even vector
     const int nparts = reduce_blocks(n);
     double2 *r = eo_vec(c, EO_R), *d = eo_vec(c, EO_D), *Ad = eo_vec(c, EO_AD);

@@ -138,6 +138,12 @@ constexpr int EW = 60;
 struct EoFArgs {
     const double2 *v, *Ue, *Uo;
     const double2 *vf, *uef, *uof;   // received t-faces (SH = 1)
+    // folded CG (MODE 1 / 2, see eo_dhat_fused_kernel)
+    const double2 *rold, *aold, *rf, *af;
+    double2 *dnew, *rnew, *x;
+    const double2 *aux2;
+    CGScalars *sc;
+    int first;
     double2 *out;
     const double2 *aux;
     double2 *partials;
@@ -151,14 +157,31 @@ struct ERow {                // one lane, one row: even input, even / odd links 
 };
 
 
-template <int DAG, int EPI, int SH>
+//
+// MODE 1 / 2: the two passes of the folded even-odd CG iteration j (the
+// one-pass recurrence of cg_onepass_kernel on half-lattice vectors):
+//   MODE 1 (DAG = 1): every loaded element forms r_j = r_{j-1} - alpha Ad_{j-1}
+//     and d_j = d_{j-1} beta + r_j (v = d_{j-1}, rold, aold; first: d_j = r_j =
+//     r_0); owned sites store r_j, d_j and x += alpha d_{j-1} and sum |r_j|^2;
+//     out = Dhat^dag d_j. Partial: p[3b+2].x = |r_j|^2.
+//   MODE 2 (DAG = 0, EPI_DOT): out = Ad_j = Dhat W; partials p[3b] = <d_j,Ad_j>
+//     (aux = d_j), p[3b+1] = <r_j,Ad_j> (aux2 = r_j), p[3b+2].y = |Ad_j|^2.
+// alpha, beta: sc (cg1_scalars after the previous pass B).
+template <int DAG, int EPI, int SH, int MODE>
 __global__ void __launch_bounds__(256) eo_dhat_fused_kernel(EoFArgs a) {
     __shared__ double2 sh[4];
+    if (MODE != 0 && a.sc->done) return;                   // grid-uniform
     const int tb = blockIdx.x % a.TBk, xc = blockIdx.x / a.TBk;
     const int lane = threadIdx.x & 63;
     const int gw = tb * 4 + (threadIdx.x >> 6);
     const int x0 = xc * a.xchunk, xe = min(a.g.Nx, x0 + a.xchunk);
-    double2 acc = make_double2(0.0, 0.0);
+    double2 acc = make_double2(0.0, 0.0), acc_rA = make_double2(0.0, 0.0);
+    double acc_nn = 0.0;                                   // MODE 1: |r|^2, MODE 2: |Ad|^2
+    double2 alpha = make_double2(0.0, 0.0), beta = make_double2(0.0, 0.0);
+    if (MODE == 1) {
+        alpha = a.sc->alpha;
+        beta = a.sc->beta;
+    }
     if (gw < a.NWT && x0 < xe) {
         const int Wh = a.g.Wh, Nx = a.g.Nx;
         const long Vh = a.g.Vh;
@@ -173,10 +196,17 @@ __global__ void __launch_bounds__(256) eo_dhat_fused_kernel(EoFArgs a) {
         const double m = a.mass, hm = 0.5 / a.mass;
         auto wrapx = [Nx](int x) { int w = x % Nx; return w < 0 ? w + Nx : w; };
         auto load = [&](int y, ERow &R) {
+            double2 r0, r1, A0, A1;
             if (!SH || inside) {
                 const long h = (long)wrapx(y) * Wh + kw;
                 R.v0 = a.v[h];
                 R.v1 = a.v[h + Vh];
+                if (MODE == 1) {
+                    r0 = a.rold[h];
+                    r1 = a.rold[h + Vh];
+                    A0 = a.aold[h];
+                    A1 = a.aold[h + Vh];
+                }
                 R.et = a.Ue[h];
                 R.ex = a.Ue[h + Vh];
                 R.ot = a.Uo[h];
@@ -185,10 +215,38 @@ __global__ void __launch_bounds__(256) eo_dhat_fused_kernel(EoFArgs a) {
                 const long f0 = cb_face_at(Nx, side, 0, col, wrapx(y)), f1 = f0 + 2 * Nx;
                 R.v0 = a.vf[f0];
                 R.v1 = a.vf[f1];
+                if (MODE == 1) {
+                    r0 = a.rf[f0];
+                    r1 = a.rf[f1];
+                    A0 = a.af[f0];
+                    A1 = a.af[f1];
+                }
                 R.et = a.uef[f0];
                 R.ex = a.uef[f1];
                 R.ot = a.uof[f0];
                 R.ox = a.uof[f1];
+            }
+            if (MODE == 1) {
+                // the reference's per-element updates (src/conjugate_gradient.cpp:36-39, 55-58)
+                const double2 rj0 = a.first ? r0 : csub(r0, cmul(alpha, A0));
+                const double2 rj1 = a.first ? r1 : csub(r1, cmul(alpha, A1));
+                const double2 dj0 = a.first ? r0 : cadd(cmul(R.v0, beta), rj0);
+                const double2 dj1 = a.first ? r1 : cadd(cmul(R.v1, beta), rj1);
+                if (own && y >= x0 && y < xe) {
+                    const long h = (long)y * Wh + kw;
+                    st_nt(a.rnew + h, rj0);
+                    st_nt(a.rnew + h + Vh, rj1);
+                    st_nt(a.dnew + h, dj0);
+                    st_nt(a.dnew + h + Vh, dj1);
+                    if (!a.first) {
+                        st_nt(a.x + h, cadd(a.x[h], cmul(alpha, R.v0)));
+                        st_nt(a.x + h + Vh, cadd(a.x[h + Vh], cmul(alpha, R.v1)));
+                    }
+                    acc_nn += cmul(rj0, cconj(rj0)).x;  // Re dot(r, r)
+                    acc_nn += cmul(rj1, cconj(rj1)).x;
+                }
+                R.v0 = dj0;
+                R.v1 = dj1;
             }
         };
         // t: local, unwrapped (halo lanes of shard 0 / the last shard wrap
@@ -272,6 +330,12 @@ __global__ void __launch_bounds__(256) eo_dhat_fused_kernel(EoFArgs a) {
                     acc = cadd(acc, cmul(a.aux[h], cconj(o.a)));
                     acc = cadd(acc, cmul(a.aux[h + Vh], cconj(o.b)));
                 }
+                if (MODE == 2) {
+                    acc_rA = cadd(acc_rA, cmul(a.aux2[h], cconj(o.a)));
+                    acc_rA = cadd(acc_rA, cmul(a.aux2[h + Vh], cconj(o.b)));
+                    acc_nn += cmul(o.a, cconj(o.a)).x;
+                    acc_nn += cmul(o.b, cconj(o.b)).x;
+                }
             }
             Tp = Tc;
             Tc = Tn;
@@ -282,7 +346,22 @@ __global__ void __launch_bounds__(256) eo_dhat_fused_kernel(EoFArgs a) {
             Rn = R2;
         }
     }
-    if (EPI == EPI_DOT) {
+    if (MODE == 1) {
+        const double2 bs = block_sum(make_double2(acc_nn, 0.0), sh);
+        if (threadIdx.x == 0) a.partials[3 * (long)blockIdx.x + 2].x = bs.x;
+    } else if (MODE == 2) {
+        const double2 s0 = block_sum(acc, sh);
+        __syncthreads();
+        const double2 s1 = block_sum(acc_rA, sh);
+        __syncthreads();
+        const double2 s2 = block_sum(make_double2(acc_nn, 0.0), sh);
+        if (threadIdx.x == 0) {
+            double2 *p = a.partials + 3 * (long)blockIdx.x;
+            p[0] = s0;
+            p[1] = s1;
+            p[2].y = s2.x;
+        }
+    } else if (EPI == EPI_DOT) {
         const double2 bs = block_sum(acc, sh);
         if (threadIdx.x == 0) a.partials[blockIdx.x] = bs;
     }
@@ -325,6 +404,13 @@ EoFusedCfg eo_fused_config(const Geometry &g) {
     if (nchunks > g.Nx / 2) nchunks = g.Nx / 2;
     if (nchunks < 1) nchunks = 1;
     int xchunk = (g.Nx + nchunks - 1) / nchunks;
+    // but at least min(8, Nx/128) rows: short chunks re-read their 4 halo rows
+    // too often (tools/tune_eo.py, one MI355X, ms per CG iteration, best
+    // chunk: 512^2 4 rows 0.039 vs 0.043; 1024^2 8 rows 0.079 vs 0.096;
+    // 2048^2 8 rows 0.243 vs 0.262; 4096^2 the 4096-block rule's 10 rows)
+    int xmin = g.Nx / 128;
+    xmin = xmin < 2 ? 2 : (xmin > 8 ? 8 : xmin);
+    if (xchunk < xmin) xchunk = xmin;
     xchunk += xchunk & 1;                                 // even: every chunk starts on an even row
     if (const char *e = getenv("SM_EO_XCHUNK")) xchunk = atoi(e);
     c.xchunk = xchunk;
@@ -348,7 +434,7 @@ void launch_eo_dhat_fused(hipStream_t s, const Geometry &g, const EoFusedCfg &c,
     a.xchunk = c.xchunk; a.NWT = c.NWT; a.TBk = c.TBk; a.XB = c.XB;
     a.mass = mass;
     const dim3 grid(c.TBk * c.XB), block(256);
-#define SM_EO_LAUNCH(D, E, H) hipLaunchKernelGGL((eo_dhat_fused_kernel<D, E, H>), grid, block, 0, s, a)
+#define SM_EO_LAUNCH(D, E, H) hipLaunchKernelGGL((eo_dhat_fused_kernel<D, E, H, 0>), grid, block, 0, s, a)
     if (f.v) {
         if (dagger) {
             if (aux) SM_EO_LAUNCH(1, EPI_DOT, 1);
@@ -367,6 +453,34 @@ void launch_eo_dhat_fused(hipStream_t s, const Geometry &g, const EoFusedCfg &c,
         }
     }
 #undef SM_EO_LAUNCH
+}
+
+void launch_eo_cg_pass(hipStream_t s, const Geometry &g, const EoFusedCfg &c, int which, const EoCgPass &q,
+                       const double2 *Ue, const double2 *Uo, double mass, const EoFaces &f, CGScalars *sc,
+                       double2 *partials) {
+    EoFArgs a = {};
+    a.Ue = Ue; a.Uo = Uo; a.uef = f.ue; a.uof = f.uo;
+    a.g = eo_geom(g);
+    a.xchunk = c.xchunk; a.NWT = c.NWT; a.TBk = c.TBk; a.XB = c.XB;
+    a.mass = mass;
+    a.sc = sc;
+    a.partials = partials;
+    a.first = q.first;
+    const dim3 grid(c.TBk * c.XB), block(256);
+    if (which == 0) {  // pass A: d_j, r_j, x; W = Dhat^dag d_j
+        a.v = q.dold; a.rold = q.rold; a.aold = q.ad;
+        a.vf = f.v; a.rf = q.rf; a.af = q.af;
+        a.dnew = q.dnew; a.rnew = q.rnew; a.x = q.x;
+        a.out = q.W;
+        if (f.v) hipLaunchKernelGGL((eo_dhat_fused_kernel<1, EPI_NONE, 1, 1>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((eo_dhat_fused_kernel<1, EPI_NONE, 0, 1>), grid, block, 0, s, a);
+    } else {           // pass B: Ad_j = Dhat W and the three dots
+        a.v = q.W; a.vf = q.wf;
+        a.aux = q.dnew; a.aux2 = q.rnew;
+        a.out = q.ad;
+        if (q.wf) hipLaunchKernelGGL((eo_dhat_fused_kernel<0, EPI_DOT, 1, 2>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((eo_dhat_fused_kernel<0, EPI_DOT, 0, 2>), grid, block, 0, s, a);
+    }
 }
 
 void launch_eo_hop(hipStream_t s, const Geometry &g, int dagger, int p, const double2 *in, const double2 *Up,

@@ -165,6 +165,20 @@ void launch_eo_dhat_fused(hipStream_t s, const Geometry &g, const EoFusedCfg &c,
                           const double2 *Ue, const double2 *Uo, double mass, double2 *out, const double2 *aux,
                           double2 *partials, const EoFaces &f);
 
+// Folded even-odd CG iteration j (sm_eo.hip, eo_dhat_fused_kernel MODE 1/2):
+// which = 0: pass A (r_j, d_j, x update; W = Dhat^dag d_j; partial |r_j|^2),
+// which = 1: pass B (Ad_j = Dhat W; <d_j,Ad_j>, <r_j,Ad_j>, |Ad_j|^2). The 3
+// partials per block feed launch_cg1_scalars (sm_cgfused.hip).
+struct EoCgPass {
+    const double2 *dold, *rold;
+    double2 *dnew, *rnew, *x, *W, *ad;
+    const double2 *rf = nullptr, *af = nullptr, *wf = nullptr;  // t-sharded faces of rold, ad, W
+    int first;
+};
+void launch_eo_cg_pass(hipStream_t s, const Geometry &g, const EoFusedCfg &c, int which, const EoCgPass &q,
+                       const double2 *Ue, const double2 *Uo, double mass, const EoFaces &f, CGScalars *sc,
+                       double2 *partials);
+
 // Pack the t = 0 and t = Wt-1 columns (both planes) into contiguous faces.
 void launch_pack_faces(hipStream_t s, const Geometry &g, const double2 *field, double2 *lo_face,
                        double2 *hi_face);

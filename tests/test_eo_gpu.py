@@ -120,6 +120,37 @@ def test_eo_cg_solves_and_converges_faster(sm, name):
     assert res.iterations < 0.6 * meta["cg_iters"], (res.iterations, meta["cg_iters"])
 
 
+@pytest.mark.parametrize("name", ["l64x64_b5_m-0p06", "l32x48_b3_m-0p10", "l16x16_b2_m-0p19"])
+def test_folded_eo_cg_matches_six_kernel_eo_cg(sm, name):
+    """The folded even-odd CG (2 passes + scalars per iteration, the one-pass
+    recurrence) against the six-launch even-odd CG with the reference's
+    recurrence: same stop rule, iterations +-1 %, solution to 1e-10 (the
+    one-pass beta differs from the reference's by rounding only)."""
+    meta, a = load_fixture(name)
+    Nx, Nt, m0 = meta["Nx"], meta["Nt"], meta["m0"]
+    S = Nx * Nt
+    phi = even_only(a["psi"], Nx, Nt)
+    out = {}
+    for folded in ("1", "0"):
+        os.environ["SM_EO_CG_FOLDED"] = folded  # read when the context is created
+        try:
+            L = sm.Lattice(Nx, Nt)
+        finally:
+            os.environ.pop("SM_EO_CG_FOLDED", None)
+        sm.check(sm.lib.sm_upload_gauge(L.ctx, ptr(a["U"][:2 * S]), ptr(a["U"][2 * S:])))
+        x = np.empty(4 * S)
+        res = sm.CGResult()
+        sm.check(sm.lib.sm_eo_cg(L.ctx, ptr(phi[:2 * S]), ptr(phi[2 * S:]), ptr(x[:2 * S]), ptr(x[2 * S:]), m0,
+                                 1e-10, MAXIT, ctypes.byref(res)))
+        L.close()
+        assert res.converged == 1
+        out[folded] = (x, res.iterations)
+    (xf, itf), (xs, its) = out["1"], out["0"]
+    assert abs(itf - its) <= max(1, its // 100), (itf, its)
+    assert np.linalg.norm(xf - xs) <= 1e-10 * np.linalg.norm(xs)
+    assert np.all(xf - even_only(xf, Nx, Nt) == 0.0)
+
+
 def fd_force_check(sm, even_odd, N=12, links=((5, 0), (17, 1), (70, 0), (101, 1))):
     """F(n, mu) = -dH/domega for U_mu(n) -> U_mu(n) e^{i omega} (P = 0, fixed phi)."""
     S = N * N

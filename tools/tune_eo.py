@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Per-iteration time of the even-odd CG (sm_eo_cg, tol 0) for fused-Dhat chunk heights.
 
-    python tools/tune_eo.py [--n 1024] [--xchunk 2,4,8,16] [--iters 200]
+    python tools/tune_eo.py [--n 1024] [--xchunk 2,4,8,16] [--iters 200] [--folded 1,0]
+
+Host-pointer API: the timing includes the upload of phi and the download of
+x (subtract, or compare variants at equal --iters).
 """
 import argparse
 import ctypes
@@ -19,6 +22,7 @@ def main():
     ap.add_argument("--n", type=int, default=1024)
     ap.add_argument("--xchunk", default="0,2,4,8,16")
     ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--folded", default="1", help="comma list: 1 folded CG (2 passes), 0 six-launch CG")
     a = ap.parse_args()
     import numpy as np
     import schwingermodel_amd as sm
@@ -28,11 +32,12 @@ def main():
     sm.lib.sm_fill_gauge(4321, 0.3246, N, 0, N, 0, N, U.ctypes.data, U[2 * S:].ctypes.data)
     sm.lib.sm_fill_spinor(91011, N, 0, N, 0, N, phi.ctypes.data, phi[2 * S:].ctypes.data)
     x = np.empty(4 * S)
-    for xc in [int(v) for v in a.xchunk.split(",")]:
+    for xc, folded in [(int(v), f) for v in a.xchunk.split(",") for f in a.folded.split(",")]:
         if xc > 0:
             os.environ["SM_EO_XCHUNK"] = str(xc)
-        L = sm.Lattice(N, N)
-        os.environ.pop("SM_EO_XCHUNK", None)
+        os.environ["SM_EO_CG_FOLDED"] = folded
+        L = sm.Lattice(N, N)   # (SM_EO_XCHUNK is read per launch: keep it set for the solves)
+        os.environ.pop("SM_EO_CG_FOLDED", None)
         sm.check(sm.lib.sm_upload_gauge(L.ctx, U.ctypes.data, U[2 * S:].ctypes.data))
         res = sm.CGResult()
         best = None
@@ -43,7 +48,9 @@ def main():
             dt = time.perf_counter() - t
             best = dt if best is None else min(best, dt)
         L.close()
-        print(json.dumps({"n": N, "xchunk": xc, "iters": res.iterations, "ms_per_it": round(1e3 * best / a.iters, 4)}))
+        os.environ.pop("SM_EO_XCHUNK", None)
+        print(json.dumps({"n": N, "xchunk": xc, "folded": int(folded), "iters": res.iterations,
+                          "ms_per_it": round(1e3 * best / a.iters, 4)}), flush=True)
 
 
 if __name__ == "__main__":
