@@ -372,6 +372,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     c->fcfg = cg_fused_config(c->g);
     if (const char *e = getenv("SM_CG_FUSED")) c->cg_fused = atoi(e);
     if (const char *e = getenv("SM_CG_INKERNEL_MAX_BLOCKS")) c->cg_inkernel_max_blocks = atoi(e);
+    if (const char *e = getenv("SM_CG_REDUNDANT")) c->cg_redundant = atoi(e);
     if (const char *e = getenv("SM_EO_FUSED")) c->eo_fused = atoi(e);
     if (const char *e = getenv("SM_EO_CG_FOLDED")) c->eo_cg_folded = atoi(e);
     const int np = kMaxPartials;
@@ -593,6 +594,7 @@ int sm_cg_begin(sm_ctx *c, const double *phi, double *x, double m0, double tol) 
     HIP_TRY(hipGetLastError());
     c->cg_active = 1;
     c->cg_issued = 0;
+    c->cg_flush_pass = -1;
     c->cg_pending_x = 0;
     return SM_OK;
 }
@@ -613,14 +615,20 @@ static int cg_onepass(sm_ctx *c) {
     // small one-shard grids: the pass's last block forms the scalars (saves a
     // latency-bound launch per iteration); large grids contend on the ticket
     const bool inkernel = c->nshard == 1 && nparts <= c->cg_inkernel_max_blocks;
+    // redundant scalars (default for those grids): partials by pass parity,
+    // evaluated by every block of the next pass; sm_cg_iterate flushes the last
+    const bool redundant = inkernel && c->cg_redundant;
+    double2 *part = redundant ? c->partials + (j & 1) * 3 * (size_t)nparts : c->partials;
+    const double2 *prev = redundant ? c->partials + ((j + 1) & 1) * 3 * (size_t)nparts : nullptr;
     auto pass = [&](int tb0, int tbn) {
         launch_cg_onepass(c->stream, c->g, fc, c->nshard, dold, rold, aold, dnew, rnew, anew, c->cg_x, c->U,
                           face2_recv(c, 0), face2_recv(c, 1), face2_recv(c, 3), face2_recv(c, 2), c->cg_mass,
-                          first, c->sc, c->partials, tb0, tbn, inkernel ? c->counters : nullptr);
+                          first, c->sc, part, tb0, tbn, inkernel && !redundant ? c->counters : nullptr, prev, j);
     };
     if (c->nshard == 1) {
         pass(0, fc.TBk);
         if (!inkernel) launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
+        c->cg_flush_pass = redundant ? j : -1;
         return SM_OK;
     }
     // interior t-blocks while the 2-deep faces of d, r, Ad travel (one round)
@@ -729,6 +737,12 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
             launch_cg_update_d(c->stream, n, d, r, c->sc);
         }
         c->cg_issued++;
+    }
+    if (c->cg_fused == 3 && c->cg_flush_pass >= 0) {  // redundant scalars: evaluate the last pass for the host
+        const long J = c->cg_flush_pass;
+        const int nparts = cg_fused_blocks(c->fcfg);
+        launch_cg1_flush(c->stream, nparts, c->partials + (J & 1) * 3 * (size_t)nparts, c->sc, J);
+        c->cg_flush_pass = -1;
     }
     HIP_TRY(hipGetLastError());
     return SM_OK;

@@ -249,6 +249,8 @@ struct CG1Args {
     CGScalars *sc;
     double2 *partials;                 // 3 per block: <d,Ad>, <r,Ad>, (|r|^2, |Ad|^2)
     unsigned *counter;                 // small one-shard grids: the last block forms the scalars
+    const double2 *prev;               // != null: redundant scalars from pass j-1's partials
+    long pass;                         // j (redundant scalars)
     long V;
     int Nx, Wt, t0, Ntg, nshard;
     int xchunk, NWT, TBk, XB, remap, first;
@@ -257,6 +259,32 @@ struct CG1Args {
 };
 
 __device__ void cg1_scalars(CGScalars *sc, int first, double2 dA, double2 rA, double2 nn);
+__device__ __forceinline__ CGRed cg1_eval(CGRed s, double tol, double phi_norm, int max_iter, int first, double2 dA,
+                                          double2 rA, double2 nn);
+
+// Redundant scalars: S_{j-1} from S_{j-2} (red[j & 1]) and pass j-1's partials,
+// evaluated by every block (all threads: block sums in a fixed order); block 0
+// stores it to red[(j-1) & 1]. Returns S_{j-1} (valid in thread 0).
+__device__ __forceinline__ CGRed cg1_redundant(CGScalars *sc, const double2 *prev, int nparts, long j, double2 *sh) {
+    CGRed s = sc->red[j & 1];
+    if (!s.done) {
+        double2 acc[3] = {make_double2(0.0, 0.0), make_double2(0.0, 0.0), make_double2(0.0, 0.0)};
+        for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
+            acc[0] = cadd(acc[0], prev[3 * i]);
+            acc[1] = cadd(acc[1], prev[3 * i + 1]);
+            acc[2] = cadd(acc[2], prev[3 * i + 2]);
+        }
+        double2 t[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            t[q] = block_sum(acc[q], sh);
+            __syncthreads();
+        }
+        s = cg1_eval(s, sc->tol, sc->phi_norm, sc->max_iter, j - 1 == 0, t[0], t[1], t[2]);
+    }
+    if (threadIdx.x == 0 && blockIdx.x == 0) sc->red[(j - 1) & 1] = s;
+    return s;
+}
 
 struct Raw3 {
     double2 d0, d1, r0, r1, a0, a1, ut, ux, x0, x1;
@@ -284,11 +312,33 @@ __device__ __forceinline__ CSrc csrc1(const double2 *base, const double2 *face, 
     return s;
 }
 
+template <int RED>  // RED: redundant scalars (a.prev != null); its own instance keeps the call out of the large-grid kernel
 __global__ void __launch_bounds__(256) cg_onepass_kernel(CG1Args a) {
     __shared__ double2 sh[4];
     CGScalars *sc = a.sc;
-    if (sc->done) return;  // grid-uniform: converged (or max_iter) in an earlier pass
-    const double2 alpha = sc->alpha, beta = sc->beta;  // alpha_{j-1}, beta_{j-1}
+    double2 alpha, beta;                               // alpha_{j-1}, beta_{j-1}
+    if (RED) {
+        __shared__ double2 s_ab[2];
+        __shared__ int s_stop;
+        if (!a.first) {
+            const CGRed s = cg1_redundant(sc, a.prev, (int)gridDim.x, a.pass, sh);
+            if (threadIdx.x == 0) {
+                s_ab[0] = s.alpha;
+                s_ab[1] = s.beta;
+                s_stop = s.done;
+            }
+        } else if (threadIdx.x == 0) {
+            s_stop = 0;
+        }
+        __syncthreads();
+        if (s_stop) return;                            // block-uniform
+        alpha = s_ab[0];
+        beta = s_ab[1];
+    } else {
+        if (sc->done) return;  // grid-uniform: converged (or max_iter) in an earlier pass
+        alpha = sc->alpha;
+        beta = sc->beta;
+    }
     int tb, xc;
     {
         int w = blockIdx.x;
@@ -430,7 +480,7 @@ __global__ void __launch_bounds__(256) cg_onepass_kernel(CG1Args a) {
     __syncthreads();
     const double2 s2 = block_sum(acc_n, sh);
     double2 *p = a.partials + 3 * (long)(a.part0 + blockIdx.x);
-    if (!a.counter) {
+    if (!a.counter) {  // (also the redundant-scalar path: plain stores, read by the next launch)
         if (threadIdx.x == 0) {
             p[0] = s0;
             p[1] = s1;
@@ -499,26 +549,63 @@ __device__ void sum3_partials(int nparts, const double2 *part, double2 out[3]) {
 
 // From the three global sums: stop test on the direct |r_j|^2 (j >= 1), then
 // alpha_j and beta_j (src/conjugate_gradient.cpp:33, 43-61).
-__device__ __attribute__((noinline)) void cg1_scalars(CGScalars *sc, int first, double2 dA, double2 rA, double2 nn) {
+__device__ __forceinline__ CGRed cg1_eval(CGRed s, double tol, double phi_norm, int max_iter, int first, double2 dA,
+                                          double2 rA, double2 nn) {
     const double rr = nn.x, AA = nn.y;
     if (!first) {
-        sc->err = sqrt(rr);
-        sc->k += 1;
-        if (sc->err < sc->tol * sc->phi_norm) {
-            sc->done = 1;
-            sc->converged = 1;
-            return;
+        s.err = sqrt(rr);
+        s.k += 1;
+        if (s.err < tol * phi_norm) {
+            s.done = 1;
+            s.converged = 1;
+            return s;
         }
-        if (sc->k >= sc->max_iter) {
-            sc->done = 1;
-            return;
+        if (s.k >= max_iter) {
+            s.done = 1;
+            return s;
         }
     }
-    sc->rn = make_double2(rr, 0.0);
+    s.rn = make_double2(rr, 0.0);
     const double2 al = cdiv(rr, 0.0, dA.x, dA.y);   // r_norm2 / dot(d, Ad)
-    sc->alpha = al;
+    s.alpha = al;
     const double est = rr - 2.0 * (al.x * rA.x + al.y * rA.y) + (al.x * al.x + al.y * al.y) * AA;
-    sc->beta = cdiv(est, 0.0, rr, 0.0);             // err^2 / r_norm2
+    s.beta = cdiv(est, 0.0, rr, 0.0);               // err^2 / r_norm2
+    return s;
+}
+
+__device__ __forceinline__ void store_state(CGScalars *sc, const CGRed &s) {
+    sc->rn = s.rn;
+    sc->alpha = s.alpha;
+    sc->beta = s.beta;
+    sc->err = s.err;
+    sc->k = s.k;
+    sc->done = s.done;
+    sc->converged = s.converged;
+}
+
+__device__ __attribute__((noinline)) void cg1_scalars(CGScalars *sc, int first, double2 dA, double2 rA, double2 nn) {
+    CGRed s;
+    s.rn = sc->rn;
+    s.alpha = sc->alpha;
+    s.beta = sc->beta;
+    s.err = sc->err;
+    s.k = sc->k;
+    s.done = sc->done;
+    s.converged = sc->converged;
+    s.pad = 0;
+    store_state(sc, cg1_eval(s, sc->tol, sc->phi_norm, sc->max_iter, first, dA, rA, nn));
+}
+
+// Redundant-scalar path: S_J of the last issued pass J into red[J & 1] and the
+// host-visible fields (the next pass recomputes exactly the same S_J).
+__global__ void __launch_bounds__(256) cg1_flush_kernel(int nparts, const double2 *part, CGScalars *sc, long J) {
+    __shared__ double2 sh[4];
+    const CGRed s = cg1_redundant(sc, part, nparts, J + 1, sh);  // S_J from S_{J-1} and pass J's partials
+    if (threadIdx.x == 0) store_state(sc, s);
+}
+
+void launch_cg1_flush(hipStream_t s, int nparts, const double2 *partials, CGScalars *sc, long pass) {
+    hipLaunchKernelGGL(cg1_flush_kernel, dim3(1), dim3(256), 0, s, nparts, partials, sc, pass);
 }
 
 __global__ void __launch_bounds__(SB) cg1_scalar_kernel(int nparts, const double2 *part, CGScalars *sc, int first) {
@@ -549,7 +636,8 @@ void launch_cg_onepass(hipStream_t s, const Geometry &g, const CGFusedCfg &c, in
                        const double2 *dold, const double2 *rold, const double2 *aold, double2 *dnew,
                        double2 *rnew, double2 *anew, double2 *x, const double2 *U, const double2 *fd,
                        const double2 *fr, const double2 *fa, const double2 *fU, double mass, int first,
-                       CGScalars *sc, double2 *partials, int tb0, int tbn, unsigned *counter) {
+                       CGScalars *sc, double2 *partials, int tb0, int tbn, unsigned *counter,
+                       const double2 *prev_partials, long pass) {
     if (tbn <= 0) return;
     CG1Args a;
     a.dold = dold; a.rold = rold; a.aold = aold;
@@ -565,7 +653,10 @@ void launch_cg_onepass(hipStream_t s, const Geometry &g, const CGFusedCfg &c, in
     a.tbn = tbn;
     a.part0 = tb0 * c.XB;
     a.counter = counter;
-    hipLaunchKernelGGL(cg_onepass_kernel, dim3(tbn * c.XB), dim3(256), 0, s, a);
+    a.prev = prev_partials;
+    a.pass = pass;
+    if (prev_partials) hipLaunchKernelGGL(cg_onepass_kernel<1>, dim3(tbn * c.XB), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(cg_onepass_kernel<0>, dim3(tbn * c.XB), dim3(256), 0, s, a);
 }
 
 void launch_cg1_scalars(hipStream_t s, int nparts, const double2 *partials, CGScalars *sc, int first) {

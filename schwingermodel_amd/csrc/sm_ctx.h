@@ -60,6 +60,8 @@ struct sm_ctx {
     // (every block of a one-wave grid hits the ticket at once), so off by default.
     int cg_inkernel = 0;
     int cg_inkernel_max_blocks = sm::kInKernelScalarMaxBlocks;  // one-pass path (sm_cgfused.hip)
+    int cg_redundant = 1;           // those grids: every block evaluates the previous pass's scalars
+    long cg_flush_pass = -1;        // last one-pass pass whose scalars still await evaluation
     hipStream_t own_stream = nullptr, stream = nullptr;
     hipStream_t comm_stream = nullptr;  // halo exchange overlapped with interior compute
     hipEvent_t ev_ready = nullptr, ev_halo = nullptr;

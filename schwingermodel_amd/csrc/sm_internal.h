@@ -27,6 +27,14 @@ struct Geometry {
     long V;              // Nx*Wt
 };
 
+// One-pass CG scalar state after evaluating one pass's partials (the
+// redundant-scalar path of small grids keeps it per pass parity, sm_cgfused.hip).
+struct CGRed {
+    double2 rn, alpha, beta;
+    double err;
+    int k, done, converged, pad;
+};
+
 // Scalars of one CG solve, resident on the device (no host round trip per
 // iteration). Mirrors the locals of conjugate_gradient(),
 // src/conjugate_gradient.cpp:6-14.
@@ -42,6 +50,7 @@ struct CGScalars {
     int converged;
     int max_iter;        // one-pass path: the device stops itself at k == max_iter
     double2 sum3[3];     // one-pass path, multi-shard: all-reduced <d,Ad>, <r,Ad>, (|r|^2,|Ad|^2)
+    CGRed red[2];        // one-pass path, redundant scalars: state S_i in red[i & 1]; red[1] = S_-1
 };
 
 enum Epilogue { EPI_NONE = 0, EPI_DOT = 1 };
@@ -109,7 +118,15 @@ void launch_cg_onepass(hipStream_t s, const Geometry &g, const CGFusedCfg &c, in
                        double2 *rnew, double2 *anew, double2 *x, const double2 *U, const double2 *fd,
                        const double2 *fr, const double2 *fa, const double2 *fU, double mass, int first,
                        CGScalars *sc, double2 *partials, int tb0, int tbn,
-                       unsigned *counter);  // counter != null: the last block forms the scalars
+                       unsigned *counter,   // counter != null: the last block forms the scalars
+                       const double2 *prev_partials = nullptr,  // != null: redundant scalars (see below)
+                       long pass = 0);
+// Redundant scalars (small one-shard grids): pass j writes its partials (by
+// pass parity) and every block of pass j + 1 evaluates them itself (fixed
+// order, bitwise the same in every block) -- no ticket, no scalar launch.
+// launch_cg1_flush evaluates the last issued pass's partials into sc for the
+// host (idempotent: the next pass recomputes the same state).
+void launch_cg1_flush(hipStream_t s, int nparts, const double2 *partials, CGScalars *sc, long pass);
 // one-pass: in-kernel scalars up to this grid size (64^2: 64 blocks, 12.2 vs 14.2 us per
 // iteration; 256^2: 512 blocks, 18.9 vs 17.0 us -- the ticket contends; tools/tune_cg.py)
 constexpr int kInKernelScalarMaxBlocks = 128;
