@@ -114,9 +114,12 @@ int sm_synchronize(sm_ctx *ctx);
  * variant selects the stencil code variant. Values <= 0 (< 0 for xcd_remap
  * and variant) keep the current setting. */
 int sm_tune(sm_ctx *ctx, int bt, int xchunk, int xcd_remap, int variant);
-/* CG path: fused = 3 (the default) runs an iteration in ONE HBM pass: the
+/* CG path: fused = 4 (the default) is the two-direction one-pass iteration:
+ * no r vector (r_{j-1} = d_{j-1} - beta_{j-2} d_{j-2} is rebuilt from the two
+ * stored directions) and x updated on even passes only, 224 B/site.
+ * fused = 3 runs an iteration in ONE HBM pass with an r vector: the
  * residual update r -= alpha Ad is folded into the next pass, beta comes from
- * that pass's direct dots (sm_cgfused.hip). 1 runs two passes each followed
+ * that pass's direct dots (sm_cgfused.hip), 288 B/site. 1 runs two passes each followed
  * by a one-block scalar kernel (alpha, beta), 2 the same two passes with
  * alpha and beta reduced in-kernel by the last block of each pass (one shard
  * only), 0 the six-kernel

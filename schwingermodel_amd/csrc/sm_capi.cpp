@@ -456,9 +456,9 @@ int sm_destroy(sm_ctx *c) {
 
 int sm_tune_cg(sm_ctx *c, int fused, int xchunk) {
     if (!c) return fail(SM_ERR_ARG, "null context");
-    if (fused > 3) return fail(SM_ERR_ARG, "fused must be 0, 1, 2 or 3");
+    if (fused > 4) return fail(SM_ERR_ARG, "fused must be 0, 1, 2, 3 or 4");
     if (fused >= 0) {
-        c->cg_fused = fused == 3 ? 3 : (fused != 0);
+        c->cg_fused = fused >= 3 ? fused : (fused != 0);
         c->cg_inkernel = fused == 2;
     }
     if (xchunk > 0) {
@@ -604,12 +604,30 @@ int sm_cg_begin(sm_ctx *c, const double *phi, double *x, double m0, double tol) 
 // reads the j-1 fields (d, r, Ad), writes the j fields into the other
 // buffers, updates x in place, then the scalar kernel forms err / stop,
 // alpha_j and beta_j.
+//
+// Two-direction form (cg_fused == 4): no r vector. d rotates through three
+// buffers (pass j reads d_{j-1} and d_{j-2}, writes d_j); the `rold` operand
+// is d_{j-2}, and x is updated on even passes only, so after an odd final
+// pass sm_cg_finish adds the pending alpha_{j-1} d_{j-1}.
+static double2 *cg_dbuf(sm_ctx *c, long i) {  // d_i of the two-direction form (d_0 from cg_init in F_D)
+    static const int slot[3] = {F_D2, F_R, F_D};
+    return c->field(slot[((i % 3) + 3) % 3]);
+}
+
 static int cg_onepass(sm_ctx *c) {
     const long j = c->cg_issued;
     const bool odd = j & 1, first = j == 0;
+    const bool td = c->cg_fused == 4;
     double2 *dold = c->field(odd ? F_D2 : F_D), *dnew = c->field(odd ? F_D : F_D2);
     double2 *rold = c->field(odd ? F_R2 : F_R), *rnew = c->field(odd ? F_R : F_R2);
     double2 *aold = c->field(odd ? F_AD2 : F_AD), *anew = c->field(odd ? F_AD : F_AD2);
+    if (td) {
+        // pass 0 reads d_0 from F_D and stores it to cg_dbuf(0); rold = d_{j-2}
+        dold = first ? c->field(F_D) : cg_dbuf(c, j - 1);
+        rold = cg_dbuf(c, j - 2);
+        dnew = cg_dbuf(c, j);
+        rnew = nullptr;
+    }
     const CGFusedCfg &fc = c->fcfg;
     const int nparts = cg_fused_blocks(fc);
     // small one-shard grids: the pass's last block forms the scalars (saves a
@@ -623,8 +641,10 @@ static int cg_onepass(sm_ctx *c) {
     auto pass = [&](int tb0, int tbn) {
         launch_cg_onepass(c->stream, c->g, fc, c->nshard, dold, rold, aold, dnew, rnew, anew, c->cg_x, c->U,
                           face2_recv(c, 0), face2_recv(c, 1), face2_recv(c, 3), face2_recv(c, 2), c->cg_mass,
-                          first, c->sc, part, tb0, tbn, inkernel && !redundant ? c->counters : nullptr, prev, j);
+                          first, c->sc, part, tb0, tbn, inkernel && !redundant ? c->counters : nullptr, prev, j,
+                          td);
     };
+    if (td) c->cg_pending_x = 1;  // sm_cg_finish checks the device's final pass parity
     if (c->nshard == 1) {
         pass(0, fc.TBk);
         if (!inkernel) launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
@@ -670,7 +690,7 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
     double2 *r = c->field(F_R), *Ad = c->field(F_AD), *t = c->field(F_T);
     double2 *x = c->cg_x;
     for (int i = 0; i < niter; ++i) {
-        if (c->cg_fused == 3) {
+        if (c->cg_fused >= 3) {
             TRY(cg_onepass(c));
         } else if (c->cg_fused) {
             // pass 1: d_k, deferred x update, Ad = D D^dag d_k, <d_k, Ad>
@@ -738,7 +758,7 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
         }
         c->cg_issued++;
     }
-    if (c->cg_fused == 3 && c->cg_flush_pass >= 0) {  // redundant scalars: evaluate the last pass for the host
+    if (c->cg_fused >= 3 && c->cg_flush_pass >= 0) {  // redundant scalars: evaluate the last pass for the host
         const long J = c->cg_flush_pass;
         const int nparts = cg_fused_blocks(c->fcfg);
         launch_cg1_flush(c->stream, nparts, c->partials + (J & 1) * 3 * (size_t)nparts, c->sc, J);
@@ -750,7 +770,11 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
 
 int sm_cg_finish(sm_ctx *c, sm_cg_result *res) {
     if (!c || !res) return fail(SM_ERR_ARG, "null argument");
-    if (c->cg_active && c->cg_pending_x) {
+    if (c->cg_active && c->cg_pending_x && c->cg_fused == 4) {
+        launch_cg_td_finish_x(c->stream, 2 * c->g.V, c->cg_x, cg_dbuf(c, 0), cg_dbuf(c, 1), cg_dbuf(c, 2), c->sc);
+        HIP_TRY(hipGetLastError());
+        c->cg_pending_x = 0;
+    } else if (c->cg_active && c->cg_pending_x) {
         launch_cg_finish_x(c->stream, 2 * c->g.V, c->cg_x, c->field(F_D), c->field(F_D2), c->sc);
         HIP_TRY(hipGetLastError());
         c->cg_pending_x = 0;
@@ -779,7 +803,7 @@ int sm_cg_dev(sm_ctx *c, const double *phi, double *x, double m0, double tol, in
     // The one-pass path runs max_iter + 1 passes (pass 0 forms Ad_0) and stops
     // itself at k == max_iter.
     int passes = max_iter;
-    if (c->cg_fused == 3) {
+    if (c->cg_fused >= 3) {
         HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)&c->sc->max_iter, max_iter, 1, c->stream));
         passes = max_iter + 1;
     }

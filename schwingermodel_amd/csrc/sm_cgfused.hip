@@ -312,19 +312,26 @@ __device__ __forceinline__ CSrc csrc1(const double2 *base, const double2 *face, 
     return s;
 }
 
-template <int RED>  // RED: redundant scalars (a.prev != null); its own instance keeps the call out of the large-grid kernel
+// RED: redundant scalars (a.prev != null); its own instance keeps the call out of the large-grid kernel.
+// TD: two-direction recurrence (no r vector): the `rold` fields hold d_{j-2},
+// r_{j-1} is rebuilt as d_{j-1} - d_{j-2} beta_{j-2}, and x takes the updates of
+// passes j-1 and j together on even passes (XP = 1); 224 instead of 288 B/site.
+template <int RED, int TD, int XP>
 __global__ void __launch_bounds__(256) cg_onepass_kernel(CG1Args a) {
     __shared__ double2 sh[4];
     CGScalars *sc = a.sc;
     double2 alpha, beta;                               // alpha_{j-1}, beta_{j-1}
+    double2 alpha2, beta2;                             // alpha_{j-2}, beta_{j-2} (TD)
     if (RED) {
-        __shared__ double2 s_ab[2];
+        __shared__ double2 s_ab[4];
         __shared__ int s_stop;
         if (!a.first) {
             const CGRed s = cg1_redundant(sc, a.prev, (int)gridDim.x, a.pass, sh);
             if (threadIdx.x == 0) {
                 s_ab[0] = s.alpha;
                 s_ab[1] = s.beta;
+                s_ab[2] = s.alpha2;
+                s_ab[3] = s.beta2;
                 s_stop = s.done;
             }
         } else if (threadIdx.x == 0) {
@@ -334,10 +341,14 @@ __global__ void __launch_bounds__(256) cg_onepass_kernel(CG1Args a) {
         if (s_stop) return;                            // block-uniform
         alpha = s_ab[0];
         beta = s_ab[1];
+        alpha2 = s_ab[2];
+        beta2 = s_ab[3];
     } else {
         if (sc->done) return;  // grid-uniform: converged (or max_iter) in an earlier pass
         alpha = sc->alpha;
         beta = sc->beta;
+        alpha2 = sc->alpha2;
+        beta2 = sc->beta2;
     }
     int tb, xc;
     {
@@ -380,26 +391,44 @@ __global__ void __launch_bounds__(256) cg_onepass_kernel(CG1Args a) {
             const double2 *pu = Su.p + (long)wrap(min(xr, xe)) * Su.xs;
             R.ut = pu[0];
             R.ux = pu[Su.ps];
-            const long nx = (long)wrap(min(max(xr, x0), xe - 1)) * Wt + cx;
-            R.x0 = a.x[nx];
-            R.x1 = a.x[nx + a.V];
+            if (!TD || XP) {
+                const long nx = (long)wrap(min(max(xr, x0), xe - 1)) * Wt + cx;
+                R.x0 = a.x[nx];
+                R.x1 = a.x[nx + a.V];
+            }
         };
-        // r_j and d_j of row xr; on owned rows store r_j, d_j, x_j, add |r_j|^2
+        const bool rebuild = TD && a.pass >= 2;  // pass 1 has r_0 = d_0 (no d_{-1})
+        // r_j and d_j of row xr; on owned rows store r_j (not TD), d_j, x_j, add |r_j|^2
         auto form = [&](int xr, const Raw3 &R, Sp &rj) {
-            rj.a = first ? R.r0 : csub(R.r0, cmul(alpha, R.a0));
-            rj.b = first ? R.r1 : csub(R.r1, cmul(alpha, R.a1));
+            Sp rp;  // r_{j-1}
+            if (TD) {
+                // d_{j-1} = d_{j-2} beta_{j-2} + r_{j-1} (the reference's d *= beta; d += r)
+                rp.a = rebuild ? csub(R.d0, cmul(R.r0, beta2)) : R.d0;
+                rp.b = rebuild ? csub(R.d1, cmul(R.r1, beta2)) : R.d1;
+            } else {
+                rp.a = R.r0;
+                rp.b = R.r1;
+            }
+            rj.a = first ? rp.a : csub(rp.a, cmul(alpha, R.a0));
+            rj.b = first ? rp.b : csub(rp.b, cmul(alpha, R.a1));
             Sp d;
             d.a = first ? R.d0 : cadd(cmul(R.d0, beta), rj.a);
             d.b = first ? R.d1 : cadd(cmul(R.d1, beta), rj.b);
             if (xr >= x0 && xr < xe && own) {
                 const long n = (long)xr * Wt + c;
-                st_nt(a.rnew + n, rj.a);
-                st_nt(a.rnew + n + a.V, rj.b);
+                if (!TD) {
+                    st_nt(a.rnew + n, rj.a);
+                    st_nt(a.rnew + n + a.V, rj.b);
+                }
                 st_nt(a.dnew + n, d.a);
                 st_nt(a.dnew + n + a.V, d.b);
-                if (!first) {
+                if (!TD && !first) {
                     st_nt(a.x + n, cadd(R.x0, cmul(alpha, R.d0)));
                     st_nt(a.x + n + a.V, cadd(R.x1, cmul(alpha, R.d1)));
+                }
+                if (TD && XP) {  // x_j = (x_{j-2} + alpha_{j-2} d_{j-2}) + alpha_{j-1} d_{j-1}
+                    st_nt(a.x + n, cadd(cadd(R.x0, cmul(alpha2, R.r0)), cmul(alpha, R.d0)));
+                    st_nt(a.x + n + a.V, cadd(cadd(R.x1, cmul(alpha2, R.r1)), cmul(alpha, R.d1)));
                 }
                 acc_n.x += cmul(rj.a, cconj(rj.a)).x;  // Re dot(r, r), include/variables.h:185-188
                 acc_n.x += cmul(rj.b, cconj(rj.b)).x;
@@ -567,6 +596,8 @@ __device__ __forceinline__ CGRed cg1_eval(CGRed s, double tol, double phi_norm, 
     }
     s.rn = make_double2(rr, 0.0);
     const double2 al = cdiv(rr, 0.0, dA.x, dA.y);   // r_norm2 / dot(d, Ad)
+    s.alpha2 = s.alpha;                             // two-direction CG keeps one pass of history
+    s.beta2 = s.beta;
     s.alpha = al;
     const double est = rr - 2.0 * (al.x * rA.x + al.y * rA.y) + (al.x * al.x + al.y * al.y) * AA;
     s.beta = cdiv(est, 0.0, rr, 0.0);               // err^2 / r_norm2
@@ -577,6 +608,8 @@ __device__ __forceinline__ void store_state(CGScalars *sc, const CGRed &s) {
     sc->rn = s.rn;
     sc->alpha = s.alpha;
     sc->beta = s.beta;
+    sc->alpha2 = s.alpha2;
+    sc->beta2 = s.beta2;
     sc->err = s.err;
     sc->k = s.k;
     sc->done = s.done;
@@ -588,6 +621,8 @@ __device__ __attribute__((noinline)) void cg1_scalars(CGScalars *sc, int first, 
     s.rn = sc->rn;
     s.alpha = sc->alpha;
     s.beta = sc->beta;
+    s.alpha2 = sc->alpha2;
+    s.beta2 = sc->beta2;
     s.err = sc->err;
     s.k = sc->k;
     s.done = sc->done;
@@ -637,7 +672,7 @@ void launch_cg_onepass(hipStream_t s, const Geometry &g, const CGFusedCfg &c, in
                        double2 *rnew, double2 *anew, double2 *x, const double2 *U, const double2 *fd,
                        const double2 *fr, const double2 *fa, const double2 *fU, double mass, int first,
                        CGScalars *sc, double2 *partials, int tb0, int tbn, unsigned *counter,
-                       const double2 *prev_partials, long pass) {
+                       const double2 *prev_partials, long pass, int twodir) {
     if (tbn <= 0) return;
     CG1Args a;
     a.dold = dold; a.rold = rold; a.aold = aold;
@@ -655,8 +690,20 @@ void launch_cg_onepass(hipStream_t s, const Geometry &g, const CGFusedCfg &c, in
     a.counter = counter;
     a.prev = prev_partials;
     a.pass = pass;
-    if (prev_partials) hipLaunchKernelGGL(cg_onepass_kernel<1>, dim3(tbn * c.XB), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(cg_onepass_kernel<0>, dim3(tbn * c.XB), dim3(256), 0, s, a);
+    const dim3 grid(tbn * c.XB), block(256);
+    if (!twodir) {
+        if (prev_partials) hipLaunchKernelGGL((cg_onepass_kernel<1, 0, 0>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((cg_onepass_kernel<0, 0, 0>), grid, block, 0, s, a);
+        return;
+    }
+    const bool xp = pass >= 2 && (pass & 1) == 0;  // x takes passes j-1 and j together
+    if (prev_partials) {
+        if (xp) hipLaunchKernelGGL((cg_onepass_kernel<1, 1, 1>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((cg_onepass_kernel<1, 1, 0>), grid, block, 0, s, a);
+    } else {
+        if (xp) hipLaunchKernelGGL((cg_onepass_kernel<0, 1, 1>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((cg_onepass_kernel<0, 1, 0>), grid, block, 0, s, a);
+    }
 }
 
 void launch_cg1_scalars(hipStream_t s, int nparts, const double2 *partials, CGScalars *sc, int first) {
@@ -776,6 +823,26 @@ __global__ void __launch_bounds__(RB2) cg_finish_x_kernel(long n, double2 *x, co
 void launch_cg_finish_x(hipStream_t s, long n, double2 *x, const double2 *d0, const double2 *d1,
                         const CGScalars *sc) {
     hipLaunchKernelGGL(cg_finish_x_kernel, dim3(reduce_blocks(n)), dim3(RB2), 0, s, n, x, d0, d1, sc);
+}
+
+// Two-direction form: after the last pass J = k (pass J evaluated into sc), an
+// odd J left alpha_{J-1} d_{J-1} out of x. A stopping evaluation keeps alpha =
+// alpha_{J-1}; a non-final one has already moved it to alpha2.
+__global__ void __launch_bounds__(RB2) cg_td_finish_x_kernel(long n, double2 *x, const double2 *d0,
+                                                             const double2 *d1, const double2 *d2,
+                                                             const CGScalars *sc) {
+    const int k = sc->k;
+    if (k < 1 || !(k & 1)) return;
+    const double2 alpha = sc->done ? sc->alpha : sc->alpha2;
+    const int i3 = (k - 1) % 3;
+    const double2 *d = i3 == 0 ? d0 : (i3 == 1 ? d1 : d2);
+    const Chunk ch = block_chunk(n);
+    for (long i = ch.beg + threadIdx.x; i < ch.end; i += RB2) x[i] = cadd(x[i], cmul(alpha, d[i]));
+}
+
+void launch_cg_td_finish_x(hipStream_t s, long n, double2 *x, const double2 *d0, const double2 *d1,
+                           const double2 *d2, const CGScalars *sc) {
+    hipLaunchKernelGGL(cg_td_finish_x_kernel, dim3(reduce_blocks(n)), dim3(RB2), 0, s, n, x, d0, d1, d2, sc);
 }
 
 // ---- 2-deep t-faces: columns {Wt-2, Wt-1} go up (arrive as -2, -1), {0, 1} go

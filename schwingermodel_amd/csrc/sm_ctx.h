@@ -52,9 +52,11 @@ struct sm_ctx {
     sm::LaunchCfg cfg{};
     sm::CGFusedCfg fcfg{};
     // CG iteration: 0 six kernels, 1 two-pass fused (scalar kernels), 2 two-pass
-    // fused with in-kernel scalars, 3 one-pass (sm_cgfused.hip; the default:
-    // 288 B/site, 0.979 vs 1.040 ms per iteration at 4096^2, tools/tune_cg.py)
-    int cg_fused = 3;
+    // fused with in-kernel scalars, 3 one-pass (sm_cgfused.hip: 288 B/site,
+    // 0.979 vs 1.040 ms per iteration at 4096^2, tools/tune_cg.py), 4 the
+    // two-direction one-pass form (the default: no r vector, x every other
+    // pass, 224 B/site; 0.776 vs 1.013 ms per iteration at 4096^2)
+    int cg_fused = 4;
     // one shard: alpha/beta by the last block of each pass instead of two
     // one-block kernels. Measured equal at 4096^2 and 19 % slower at 1024^2
     // (every block of a one-wave grid hits the ticket at once), so off by default.

@@ -31,6 +31,7 @@ struct Geometry {
 // redundant-scalar path of small grids keeps it per pass parity, sm_cgfused.hip).
 struct CGRed {
     double2 rn, alpha, beta;
+    double2 alpha2, beta2;   // alpha, beta of the pass before (two-direction CG)
     double err;
     int k, done, converged, pad;
 };
@@ -41,6 +42,7 @@ struct CGRed {
 struct CGScalars {
     double2 rn;          // r_norm2 (complex, as the reference keeps it)
     double2 alpha, beta;
+    double2 alpha2, beta2;  // two-direction CG: alpha_{j-1}, beta_{j-1} while alpha, beta are alpha_j, beta_j
     double2 sum;         // last globally reduced dot
     double phi_norm;     // sqrt(Re <phi,phi>)
     double tol;
@@ -120,7 +122,12 @@ void launch_cg_onepass(hipStream_t s, const Geometry &g, const CGFusedCfg &c, in
                        CGScalars *sc, double2 *partials, int tb0, int tbn,
                        unsigned *counter,   // counter != null: the last block forms the scalars
                        const double2 *prev_partials = nullptr,  // != null: redundant scalars (see below)
-                       long pass = 0);
+                       long pass = 0,
+                       int twodir = 0);  // two-direction form: rold/fr = d_{j-2}, rnew unused
+// Two-direction form, after the last pass J = sc->k: if J is odd, x += alpha_{J-1} d_{J-1}
+// (d_i lives in d[i % 3]).
+void launch_cg_td_finish_x(hipStream_t s, long n, double2 *x, const double2 *d0, const double2 *d1,
+                           const double2 *d2, const CGScalars *sc);
 // Redundant scalars (small one-shard grids): pass j writes its partials (by
 // pass parity) and every block of pass j + 1 evaluates them itself (fixed
 // order, bitwise the same in every block) -- no ticket, no scalar launch.

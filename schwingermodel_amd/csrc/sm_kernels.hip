@@ -427,9 +427,11 @@ __device__ __forceinline__ void cg_init_scalars(CGScalars *sc, double2 rr, doubl
     sc->done = 0;
     sc->converged = 0;
     sc->max_iter = 0x7fffffff;  // sm_cg_dev sets the caller's limit (one-pass path)
+    sc->alpha = sc->beta = sc->alpha2 = sc->beta2 = make_double2(0.0, 0.0);
     CGRed s0;                   // S_-1 of the redundant-scalar path
     s0.rn = rr;
     s0.alpha = s0.beta = make_double2(0.0, 0.0);
+    s0.alpha2 = s0.beta2 = make_double2(0.0, 0.0);
     s0.err = 0.0;
     s0.k = s0.done = s0.converged = s0.pad = 0;
     sc->red[0] = s0;

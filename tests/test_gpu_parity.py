@@ -51,12 +51,13 @@ def test_operators_bitwise_vs_reference(sm, name):
     assert bits_equal(np.concatenate([F.mu0, F.mu1]), a["ref_force"])
 
 
-@pytest.mark.parametrize("fused", [3, 1, 2, 0], ids=["onepass", "fused", "fused_inkernel", "sixkernel"])
+@pytest.mark.parametrize("fused", [4, 3, 1, 2, 0], ids=["twodir", "onepass", "fused", "fused_inkernel", "sixkernel"])
 @pytest.mark.parametrize("name", NAMES)
 def test_cg_vs_reference(sm, name, fused):
-    """Every CG path: the one-pass iteration (pass 2 folded into the next pass),
-    the two-pass fused iteration with scalar kernels, the same with alpha/beta
-    reduced in-kernel by the last block, and the six-kernel sequence."""
+    """Every CG path: the two-direction one-pass iteration (no r vector), the
+    one-pass iteration (pass 2 folded into the next pass), the two-pass fused
+    iteration with scalar kernels, the same with alpha/beta reduced in-kernel
+    by the last block, and the six-kernel sequence."""
     meta, a = load_fixture(name)
     Nx, Nt, m0 = meta["Nx"], meta["Nt"], meta["m0"]
     S = Nx * Nt
@@ -89,6 +90,91 @@ def test_dot_matches_reference(sm, name):
     z = sm.dot(chi, Dpsi)
     zr = complex(*meta["dot_chi_Dpsi"])
     assert abs(z - zr) <= 1e-13 * abs(zr)
+
+
+@pytest.mark.parametrize("Nx,Nt", [(64, 64), (256, 192)])  # redundant-scalar and scalar-kernel grids
+@pytest.mark.parametrize("stop", [16, 17, 1, 2])
+def test_twodir_pending_x_matches_onepass(sm, Nx, Nt, stop):
+    """The two-direction form updates x on even passes only: stopping after an
+    odd or even number of iterations (max_iter) must give the one-pass x."""
+    S = Nx * Nt
+    L = sm.init(Nx, Nt)
+    U, psi = sm.spinor(S), sm.spinor(S)
+    P = lambda a: a.ctypes.data  # noqa: E731
+    sm.lib.sm_fill_gauge(4321, 0.3246, Nt, 0, Nx, 0, Nt, P(U.mu0), P(U.mu1))
+    sm.lib.sm_fill_spinor(5678, Nt, 0, Nx, 0, Nt, P(psi.mu0), P(psi.mu1))
+    xs = {}
+    old = sm.CG.max_iter
+    try:
+        sm.CG.max_iter = stop
+        for fused in (3, 4):
+            sm.check(sm.lib.sm_tune_cg(L.ctx, fused, 0))
+            x = sm.spinor(S)
+            assert sm.conjugate_gradient(U, psi, x, -0.10) == 0
+            assert L.last_cg.iterations == stop
+            xs[fused] = flat(x)
+    finally:
+        sm.CG.max_iter = old
+    rel = np.linalg.norm(xs[4] - xs[3]) / np.linalg.norm(xs[3])
+    assert rel <= 1e-13, rel
+
+
+class _Hip:
+    """hipMalloc / hipMemcpy through the HIP runtime libsm_hip.so itself links
+    (no torch in this process: a second HIP runtime initialised after ours
+    finds no GPU)."""
+
+    def __init__(self):
+        self.rt = ctypes.CDLL("libamdhip64.so.7")
+        self.rt.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+        self.rt.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        self.rt.hipFree.argtypes = [ctypes.c_void_p]
+        self.rt.hipDeviceSynchronize.argtypes = []
+
+    def upload(self, a):
+        p = ctypes.c_void_p()
+        assert self.rt.hipMalloc(ctypes.byref(p), a.nbytes) == 0
+        assert self.rt.hipMemcpy(p, a.ctypes.data, a.nbytes, 1) == 0  # hipMemcpyHostToDevice
+        return p
+
+    def download(self, p, a):
+        assert self.rt.hipDeviceSynchronize() == 0
+        assert self.rt.hipMemcpy(a.ctypes.data, p, a.nbytes, 2) == 0  # hipMemcpyDeviceToHost
+        return a
+
+
+@pytest.mark.parametrize("passes", [17, 18])
+def test_twodir_stepwise_finish_matches_onepass(sm, passes):
+    """sm_cg_begin / sm_cg_iterate / sm_cg_finish without convergence (tol 0):
+    after an odd or even number of passes the two-direction x (pending update
+    added by sm_cg_finish) equals the one-pass x."""
+    Nx, Nt = 128, 96
+    S = Nx * Nt
+    L = sm.init(Nx, Nt)
+    U, psi = sm.spinor(S), sm.spinor(S)
+    P = lambda a: a.ctypes.data  # noqa: E731
+    sm.lib.sm_fill_gauge(4321, 0.3246, Nt, 0, Nx, 0, Nt, P(U.mu0), P(U.mu1))
+    sm.lib.sm_fill_spinor(5678, Nt, 0, Nx, 0, Nt, P(psi.mu0), P(psi.mu1))
+    hip = _Hip()
+    dU = hip.upload(np.concatenate([U.mu0, U.mu1]))
+    dphi = hip.upload(np.concatenate([psi.mu0, psi.mu1]))
+    dx = hip.upload(np.zeros(2 * S, dtype=np.complex128))
+    sm.check(sm.lib.sm_upload_gauge_dev(L.ctx, dU))
+    xs = {}
+    try:
+        for fused in (3, 4):
+            sm.check(sm.lib.sm_tune_cg(L.ctx, fused, 0))
+            sm.check(sm.lib.sm_cg_begin(L.ctx, dphi, dx, -0.10, 0.0))
+            sm.check(sm.lib.sm_cg_iterate(L.ctx, passes))
+            res = sm.CGResult()
+            sm.check(sm.lib.sm_cg_finish(L.ctx, ctypes.byref(res)))
+            assert res.iterations == passes - 1 and res.converged == 0
+            xs[fused] = hip.download(dx, np.empty(2 * S, dtype=np.complex128))
+    finally:
+        for p in (dU, dphi, dx):
+            hip.rt.hipFree(p)
+    rel = np.linalg.norm(xs[4] - xs[3]) / np.linalg.norm(xs[3])
+    assert rel <= 1e-13, rel
 
 
 def test_cg_nonconvergence_semantics(sm, capsys):
