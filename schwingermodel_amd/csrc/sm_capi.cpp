@@ -151,9 +151,9 @@ int apply(sm_ctx *c, const double2 *in, double2 *out, double mass, int dagger, c
         launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip,
                       1, TB - 2);
         HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
-        launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip, 0, 1);
+        // both edge block-columns (TB-1, then 0 by wrap-around) in one launch
         launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip,
-                      TB - 1, 1);
+                      TB - 1, 2);
     }
     HIP_TRY(hipGetLastError());
     return SM_OK;
@@ -672,8 +672,7 @@ static int cg_onepass(sm_ctx *c) {
     if (split) pass(tb_lo, tb_hi - tb_lo + 1);
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
     if (split) {
-        pass(0, tb_lo);
-        pass(tb_hi + 1, fc.TBk - tb_hi - 1);
+        pass(tb_hi + 1, fc.TBk - 1 - tb_hi + tb_lo);  // edge t-blocks (tb_hi, TBk) and [0, tb_lo), wrapping: one launch
     } else {
         pass(0, fc.TBk);
     }

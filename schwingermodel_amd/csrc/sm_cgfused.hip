@@ -358,6 +358,7 @@ __global__ void __launch_bounds__(256) cg_onepass_kernel(CG1Args a) {
             w = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (w >> 3);
         }
         tb = a.tb0 + w % a.tbn;
+        if (tb >= a.TBk) tb -= a.TBk;  // edge block-columns TBk-1 and 0 in one launch
         xc = w / a.tbn;
     }
     const int lane = threadIdx.x & 63;
@@ -508,7 +509,7 @@ __global__ void __launch_bounds__(256) cg_onepass_kernel(CG1Args a) {
     const double2 s1 = block_sum(acc_rA, sh);
     __syncthreads();
     const double2 s2 = block_sum(acc_n, sh);
-    double2 *p = a.partials + 3 * (long)(a.part0 + blockIdx.x);
+    double2 *p = a.partials + 3 * ((long)tb * a.XB + xc);  // one slot per tile
     if (!a.counter) {  // (also the redundant-scalar path: plain stores, read by the next launch)
         if (threadIdx.x == 0) {
             p[0] = s0;

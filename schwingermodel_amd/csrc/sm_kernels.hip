@@ -30,7 +30,7 @@ struct DArgs {
     long V;
     int Nx, Wt, t0, Ntg, xchunk;
     int TB, XB, xcd_remap;   // tile grid (t-blocks x x-chunks), 1-D launch
-    int tb0, tbn, part0;     // this launch covers t-blocks [tb0, tb0+tbn); partials at part0+block
+    int tb0, tbn, part0;     // this launch covers t-blocks [tb0, tb0+tbn) mod TB; partials by tile
     double mass;
 };
 
@@ -38,13 +38,16 @@ struct DArgs {
 // dispatcher deals to one XCD (L, L+8, L+16, ...: round-robin, speed only,
 // MI355X_MICROARCH.md) get a contiguous range of tiles, so the x-halo rows and
 // t-edge lines shared by neighbouring tiles are L2 hits on that XCD.
-__device__ __forceinline__ void block_tile(int L, int tb0, int tbn, int XB, int remap, int &tb, int &xc) {
+// The t-block range wraps modulo TB, so the two edge block-columns of a
+// t-shard (TB-1 and 0) are one launch.
+__device__ __forceinline__ void block_tile(int L, int tb0, int tbn, int TB, int XB, int remap, int &tb, int &xc) {
     int w = L;
     if (remap) {
         const int n = tbn * XB, q = n >> 3, r = n & 7, xcd = L & 7;
         w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
     }
     tb = tb0 + w % tbn;
+    if (tb >= TB) tb -= TB;
     xc = w / tbn;
 }
 
@@ -105,7 +108,7 @@ __device__ __forceinline__ void dslash_body(const DArgs &a) {
     __shared__ double2 sh[4];
     if (a.sc && a.sc->done) return;  // grid-uniform early exit after CG convergence
     int tb, xc;
-    block_tile(blockIdx.x, a.tb0, a.tbn, a.XB, a.xcd_remap, tb, xc);
+    block_tile(blockIdx.x, a.tb0, a.tbn, a.TB, a.XB, a.xcd_remap, tb, xc);
     const int t = tb * blockDim.x + threadIdx.x;
     const int xbeg = xc * a.xchunk;
     const int xend = min(a.Nx, xbeg + a.xchunk);
@@ -190,7 +193,7 @@ __device__ __forceinline__ void dslash_body(const DArgs &a) {
     }
     if (EPI == EPI_DOT) {
         double2 bs = block_sum(acc, sh);
-        if (threadIdx.x == 0) a.partials[a.part0 + blockIdx.x] = bs;
+        if (threadIdx.x == 0) a.partials[(long)tb * a.XB + xc] = bs;  // one slot per tile
     }
 }
 
