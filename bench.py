@@ -51,7 +51,8 @@ def parse():
     ap.add_argument("--transport", choices=["rccl", "hosted"], default="rccl",
                     help="multi-GPU wire: RCCL (production) or the host-staged test transport")
     ap.add_argument("--device", type=int, default=None, help="override LOCAL_RANK -> GPU mapping")
-    ap.add_argument("--cg-path", choices=["twodir", "onepass", "fused", "fused_inkernel", "sixkernel"], default="twodir")
+    ap.add_argument("--cg-path", choices=["recompute", "twodir", "onepass", "fused", "fused_inkernel", "sixkernel"],
+                    default="recompute")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling (SURVEY.md §8d config 4): a fixed nx x nt-per-gpu lattice split over the N GPUs")
     return ap.parse_args()
@@ -193,7 +194,7 @@ def main():
     apply_s = e0.elapsed_time(e1) / 1e3 / args.applies
     apply_GBps = BYTES_PER_SITE_APPLY * V / apply_s / 1e9
 
-    sm.check(sm.lib.sm_tune_cg(L.ctx, {"twodir": 4, "onepass": 3, "fused": 1, "fused_inkernel": 2, "sixkernel": 0}[args.cg_path], 0))
+    sm.check(sm.lib.sm_tune_cg(L.ctx, {"recompute": 5, "twodir": 4, "onepass": 3, "fused": 1, "fused_inkernel": 2, "sixkernel": 0}[args.cg_path], 0))
     # ---- CG iterations (tol = 0: never converges, full work every step) ----
     sm.check(sm.lib.sm_cg_begin(L.ctx, ctypes.c_void_p(phi.data_ptr()), ctypes.c_void_p(x.data_ptr()), M0, 0.0))
     sm.check(sm.lib.sm_cg_iterate(L.ctx, args.warmup))
@@ -209,7 +210,7 @@ def main():
     sm.check(sm.lib.sm_cg_status(L.ctx, ctypes.byref(res)))
     # the one-pass iteration's pass 0 (in the warmup) only forms Ad_0: every
     # later pass is one full reference iteration
-    setup_passes = 1 if args.cg_path in ("onepass", "twodir") else 0
+    setup_passes = 1 if args.cg_path in ("onepass", "twodir", "recompute") else 0
     assert res.iterations == args.warmup + args.steps - setup_passes and res.converged == 0
     t_ev = c0.elapsed_time(c1) / 1e3
     t_local = max(wall, t_ev)

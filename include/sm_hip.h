@@ -114,7 +114,11 @@ int sm_synchronize(sm_ctx *ctx);
  * variant selects the stencil code variant. Values <= 0 (< 0 for xcd_remap
  * and variant) keep the current setting. */
 int sm_tune(sm_ctx *ctx, int bt, int xchunk, int xcd_remap, int variant);
-/* CG path: fused = 4 (the default) is the two-direction one-pass iteration:
+/* CG path: fused = 5 (the default on sharded grids and one-shard grids of
+ * more than 128 fused blocks) is the two-direction iteration that recomputes
+ * Ad_{j-1} = D D^dag d_{j-1} in-kernel instead of storing it (sm_cgra.hip):
+ * 160 B/site. fused = 4 (the default on small one-shard grids) is the
+ * two-direction one-pass iteration that stores Ad:
  * no r vector (r_{j-1} = d_{j-1} - beta_{j-2} d_{j-2} is rebuilt from the two
  * stored directions) and x updated on even passes only, 224 B/site.
  * fused = 3 runs an iteration in ONE HBM pass with an r vector: the
@@ -123,7 +127,7 @@ int sm_tune(sm_ctx *ctx, int bt, int xchunk, int xcd_remap, int variant);
  * by a one-block scalar kernel (alpha, beta), 2 the same two passes with
  * alpha and beta reduced in-kernel by the last block of each pass (one shard
  * only), 0 the six-kernel
- * sequence; xchunk = rows per block of the fused kernel. < 0 / <= 0 keep. */
+ * sequence; xchunk = rows per block of the active fused kernel. < 0 / <= 0 keep. */
 int sm_tune_cg(sm_ctx *ctx, int fused, int xchunk);
 /* Streaming-bandwidth ceiling on the ctx stream (measured roofline reference):
  * out = a + b (two_reads = 1: the stencil's 2-read/1-write byte mix) or

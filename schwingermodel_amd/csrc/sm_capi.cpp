@@ -226,6 +226,22 @@ int halo2(sm_ctx *c, const double2 *field, double2 *face) {
     return halo2_multi(c, c->stream, f, r, 1);
 }
 
+// 4-deep faces of the recompute-Ad CG pass (sm_cgra.hip): [col -4..-1,
+// Wt..Wt+3][plane][x], 16 Nx complex each. faces4 layout (complex, units of
+// Nx): send lo 0, send hi 8, received d_{j-1} by pass parity at 16 and 32 (so
+// pass j still holds d_{j-2}'s faces from pass j-1), U at 48; 64 Nx in all.
+static double2 *face4_send(sm_ctx *c, int hi) { return c->faces4 + (size_t)(8 * hi) * c->g.Nx; }
+static double2 *face4_recv_d(sm_ctx *c, long pass) { return c->faces4 + (size_t)(16 + 16 * (pass & 1)) * c->g.Nx; }
+double2 *face4_recv_U(sm_ctx *c) { return c->faces4 + (size_t)48 * c->g.Nx; }
+bool cg_ra_ok(const sm_ctx *c) { return c->nshard == 1 || c->g.Wt >= 4; }
+
+// Pack and exchange the 4-deep t-faces of `field` into `recv` on stream s.
+static int halo4(sm_ctx *c, hipStream_t s, const double2 *field, double2 *recv) {
+    launch_pack_faces_k(s, c->g, 4, field, face4_send(c, 0), face4_send(c, 1));
+    return exchange_faces_on(c, s, face4_send(c, 0), face4_send(c, 1), recv, recv + (size_t)8 * c->g.Nx,
+                             (size_t)16 * c->g.Nx);
+}
+
 int exchange_ghost_U(sm_ctx *c) {
     if (c->nshard == 1) return SM_OK;
     // U_t(x, Wt-1) (plane 0 of my hi face) is the up-neighbour's U_t(x, -1)
@@ -234,8 +250,9 @@ int exchange_ghost_U(sm_ctx *c) {
     launch_pack_faces(c->stream, c->g, c->U, slo, shi);
     TRY(exchange_faces(c, slo, shi, rlo, rhi, (size_t)4 * c->g.Nx));
     HIP_TRY(hipMemcpyAsync(c->ghostU, rlo, sizeof(double2) * c->g.Nx, hipMemcpyDeviceToDevice, c->stream));
-    // 2-deep ghost links for the fused CG kernel
+    // 2-deep ghost links for the fused CG kernel, 4-deep for the recompute-Ad pass
     TRY(halo2(c, c->U, face2_recv(c, 2)));
+    if (cg_ra_ok(c)) TRY(halo4(c, c->stream, c->U, face4_recv_U(c)));
     return SM_OK;
 }
 
@@ -370,6 +387,10 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     c->nparts_dslash = dslash_blocks(c->g, c->cfg);
     c->nparts_red = reduce_blocks(2 * c->g.V);
     c->fcfg = cg_fused_config(c->g);
+    c->racfg = cg_ra_config(c->g);
+    // recompute-Ad pass where the grid is large or sharded; small one-shard
+    // grids keep the two-direction pass with redundant in-kernel scalars
+    c->cg_fused = (nshard > 1 || cg_fused_blocks(c->fcfg) > kInKernelScalarMaxBlocks) ? 5 : 4;
     if (const char *e = getenv("SM_CG_FUSED")) c->cg_fused = atoi(e);
     if (const char *e = getenv("SM_CG_INKERNEL_MAX_BLOCKS")) c->cg_inkernel_max_blocks = atoi(e);
     if (const char *e = getenv("SM_CG_REDUNDANT")) c->cg_redundant = atoi(e);
@@ -386,6 +407,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     chk(hipMalloc(&c->fields, fb * NFIELDS));
     chk(hipMalloc(&c->faces, sizeof(double2) * 2 * (size_t)Nx * 8));
     chk(hipMalloc(&c->faces2, sizeof(double2) * 56 * (size_t)Nx));
+    chk(hipMalloc(&c->faces4, sizeof(double2) * 64 * (size_t)Nx));
     chk(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
     chk(hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming));
     chk(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
@@ -437,7 +459,7 @@ int sm_destroy(sm_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
-    void *dev[] = {c->U, c->ghostU, c->fields, c->faces, c->faces2, c->partials, c->sums, c->Fbuf, c->sc,
+    void *dev[] = {c->U, c->ghostU, c->fields, c->faces, c->faces2, c->faces4, c->partials, c->sums, c->Fbuf, c->sc,
                    c->counters, c->U_alt, c->Pmd, c->Fmd, c->eo, c->Ucb, c->eo_faces};
     for (void *p : dev)
         if (p) (void)hipFree(p);
@@ -456,17 +478,18 @@ int sm_destroy(sm_ctx *c) {
 
 int sm_tune_cg(sm_ctx *c, int fused, int xchunk) {
     if (!c) return fail(SM_ERR_ARG, "null context");
-    if (fused > 4) return fail(SM_ERR_ARG, "fused must be 0, 1, 2, 3 or 4");
+    if (fused > 5) return fail(SM_ERR_ARG, "fused must be 0 .. 5");
     if (fused >= 0) {
         c->cg_fused = fused >= 3 ? fused : (fused != 0);
         c->cg_inkernel = fused == 2;
     }
     if (xchunk > 0) {
-        CGFusedCfg f = c->fcfg;
+        CGFusedCfg &cur = c->cg_fused == 5 ? c->racfg : c->fcfg;  // the active pass's geometry
+        CGFusedCfg f = cur;
         f.xchunk = xchunk;
         f.XB = (c->g.Nx + xchunk - 1) / xchunk;
         if (3 * cg_fused_blocks(f) > 2 * kMaxPartials) return fail(SM_ERR_ARG, "too many blocks");
-        c->fcfg = f;
+        cur = f;
     }
     return SM_OK;
 }
@@ -617,7 +640,7 @@ static double2 *cg_dbuf(sm_ctx *c, long i) {  // d_i of the two-direction form (
 static int cg_onepass(sm_ctx *c) {
     const long j = c->cg_issued;
     const bool odd = j & 1, first = j == 0;
-    const bool td = c->cg_fused == 4;
+    const bool td = c->cg_fused >= 4;  // mode 5 falls back here where the recompute-Ad pass does not fit
     double2 *dold = c->field(odd ? F_D2 : F_D), *dnew = c->field(odd ? F_D : F_D2);
     double2 *rold = c->field(odd ? F_R2 : F_R), *rnew = c->field(odd ? F_R : F_R2);
     double2 *aold = c->field(odd ? F_AD2 : F_AD), *anew = c->field(odd ? F_AD : F_AD2);
@@ -682,6 +705,60 @@ static int cg_onepass(sm_ctx *c) {
     return SM_OK;
 }
 
+// One pass of the recompute-Ad CG (cg_fused == 5, sm_cgra.hip): the
+// two-direction pass without the Ad vector, d_i in cg_dbuf(i). t-shards: the
+// 4-deep faces of d_{j-1} arrive in slot j & 1 on the comm stream while the
+// interior t-blocks run; d_{j-2}'s faces are still in slot (j-1) & 1.
+static int cg_ra_pass(sm_ctx *c) {
+    const long j = c->cg_issued;
+    const bool first = j == 0;
+    const double2 *d1 = first ? c->field(F_D) : cg_dbuf(c, j - 1);
+    const double2 *d2 = cg_dbuf(c, j - 2);
+    double2 *dn = cg_dbuf(c, j);
+    const CGFusedCfg &fc = c->racfg;
+    const int nparts = cg_fused_blocks(fc);
+    c->cg_pending_x = 1;  // sm_cg_finish checks the device's final pass parity
+    c->cg_flush_pass = -1;
+    if (c->nshard == 1) {
+        launch_cg_ra(c->stream, c->g, fc, 1, d1, d2, dn, c->cg_x, c->U, nullptr, nullptr, nullptr, c->cg_mass, j,
+                     c->sc, c->partials, 0, fc.TBk);
+        launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
+        return SM_OK;
+    }
+    double2 *f1 = face4_recv_d(c, j), *f2 = face4_recv_d(c, j - 1);
+    auto pass = [&](int tb0, int tbn) {
+        launch_cg_ra(c->stream, c->g, fc, c->nshard, d1, d2, dn, c->cg_x, c->U, f1, f2, face4_recv_U(c), c->cg_mass,
+                     j, c->sc, c->partials, tb0, tbn);
+    };
+    // interior t-blocks: every lane's column (56g-4 .. 56g+59) inside [0, Wt)
+    auto interior = [&](int tb) {
+        const int g_lo = 4 * tb, g_hi = std::min(4 * tb + 3, fc.NWT - 1);
+        return kRAWaveCols * g_lo - 4 >= 0 && kRAWaveCols * g_hi + kRAWaveCols + 3 <= c->g.Wt - 1;
+    };
+    int tb_lo = 0, tb_hi = -1;
+    for (int tb = 0; tb < fc.TBk; ++tb)
+        if (interior(tb)) {
+            if (tb_hi < 0) tb_lo = tb;
+            tb_hi = tb;
+        }
+    const bool split = tb_hi >= tb_lo && tb_hi >= 0;
+    HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
+    HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
+    TRY(halo4(c, c->comm_stream, d1, f1));
+    HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
+    if (split) pass(tb_lo, tb_hi - tb_lo + 1);
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+    if (split) {
+        pass(tb_hi + 1, fc.TBk - 1 - tb_hi + tb_lo);  // edge t-blocks (tb_hi, TBk) and [0, tb_lo), wrapping
+    } else {
+        pass(0, fc.TBk);
+    }
+    launch_cg1_local_sum(c->stream, nparts, c->partials, c->sc);
+    TRY(allreduce_dev(c, (double *)c->sc->sum3, 6));
+    launch_cg1_from_sums(c->stream, c->sc, first);
+    return SM_OK;
+}
+
 int sm_cg_iterate(sm_ctx *c, int niter) {
     TRY(check_ready(c));
     if (!c->cg_active) return fail(SM_ERR_STATE, "sm_cg_iterate before sm_cg_begin");
@@ -689,7 +766,9 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
     double2 *r = c->field(F_R), *Ad = c->field(F_AD), *t = c->field(F_T);
     double2 *x = c->cg_x;
     for (int i = 0; i < niter; ++i) {
-        if (c->cg_fused >= 3) {
+        if (c->cg_fused == 5 && cg_ra_ok(c)) {
+            TRY(cg_ra_pass(c));
+        } else if (c->cg_fused >= 3) {
             TRY(cg_onepass(c));
         } else if (c->cg_fused) {
             // pass 1: d_k, deferred x update, Ad = D D^dag d_k, <d_k, Ad>
@@ -769,7 +848,7 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
 
 int sm_cg_finish(sm_ctx *c, sm_cg_result *res) {
     if (!c || !res) return fail(SM_ERR_ARG, "null argument");
-    if (c->cg_active && c->cg_pending_x && c->cg_fused == 4) {
+    if (c->cg_active && c->cg_pending_x && c->cg_fused >= 4) {
         launch_cg_td_finish_x(c->stream, 2 * c->g.V, c->cg_x, cg_dbuf(c, 0), cg_dbuf(c, 1), cg_dbuf(c, 2), c->sc);
         HIP_TRY(hipGetLastError());
         c->cg_pending_x = 0;

@@ -1,0 +1,354 @@
+// sm_cgra.hip -- two-direction CG pass that recomputes Ad_{j-1} instead of
+// storing it (gfx950). Mode 5 of sm_tune_cg.
+//
+// Pass j of the two-direction CG (sm_cgfused.hip, cg_onepass_kernel<.,1,.>):
+//     r_{j-1} = d_{j-1} - d_{j-2} beta_{j-2}      (the reference's d *= beta; d += r,
+//                                                  src/conjugate_gradient.cpp:55-58)
+//     r_j     = r_{j-1} - alpha_{j-1} Ad_{j-1}    (:38-39)
+//     d_j     = d_{j-1} beta_{j-1} + r_j          (:55-58)
+//     x      <- (x + alpha_{j-2} d_{j-2}) + alpha_{j-1} d_{j-1}   on even j (:36-37)
+//     Ad_j    = D D^dag d_j ; partials <d_j,Ad_j>, <r_j,Ad_j>, |r_j|^2, |Ad_j|^2
+// Mode 4 stores Ad_j and reads it back in pass j+1. Here Ad_{j-1} = D D^dag
+// d_{j-1} is recomputed from the d_{j-1} rows the pass reads anyway, with the
+// same stencil code on the same operands, so it is bitwise the value pass j-1
+// used for its dots. A pass reads d_{j-1}, d_{j-2}, U (96 B/site) and writes
+// d_j (32), plus x on even passes (64): 160 B/site mean against 224 for mode 4
+// and 576 for the reference's sequence. The price is a second
+// D^dag + D per site: fp64 VALU work that runs under the HBM time.
+//
+// Geometry: a wave owns RW = 56 consecutive t-columns; its 64 lanes cover
+// columns T0-4 .. T0+59. The four stencil stages (D^dag, D on d_{j-1}; D^dag,
+// D on d_j) each take their t-neighbours from adjacent lanes through DPP wave
+// shifts, so each stage loses one lane per side: 4 halo lanes. Rows march
+// along x with every intermediate held in registers:
+//     S1  T'(y+3) = D^dag d_{j-1}     rows y+2 .. y+4 of d_{j-1}
+//     S2  A (y+2) = D T' = Ad_{j-1}   rows y+1 .. y+3 of T'
+//     S3  r_j, d_j at row y+2         (store d_j; x update)
+//     S4  T (y+1) = D^dag d_j         rows y .. y+2 of d_j
+//     S5  Ad_j(y) = D T               rows y-1 .. y+1 of T; dots
+// A block of chunk [x0, xe) runs y = x0-6 .. xe-1; the first iterations run
+// only the stages whose rows are needed (S1 from x0-6, S2/S3 from x0-4, S4
+// from x0-2, S5 from x0). r_j waits two rows for its dot with Ad_j in a
+// 3-slot LDS ring (each thread its own slots, no barrier).
+//
+// FOLD = 1 evaluates the hopping bracket with its products by 0, +-1 and +-i
+// folded into sign flips and swaps (dirac_bracket_folded): the same values up
+// to the sign of an exact zero, at 84 instead of ~126 fp64 operations a site.
+#include <type_traits>
+
+#include "sm_device.h"
+#include "sm_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace sm {
+
+constexpr int RW = kRAWaveCols;
+constexpr int RH = 4;  // halo lanes per side
+
+struct RAArgs {
+    const double2 *d1, *d2;       // d_{j-1}, d_{j-2}
+    double2 *dn;                  // d_j
+    double2 *x;
+    const double2 *U;
+    const double2 *f1, *f2, *fU;  // t-shard 4-deep faces [col -4..-1, Wt..Wt+3][plane][x]
+    CGScalars *sc;
+    double2 *partials;            // 3 per tile: <d,Ad>, <r,Ad>, (|r|^2, |Ad|^2)
+    long V;
+    int Nx, Wt, t0, Ntg;
+    int xchunk, NWT, TBk, XB, remap, first, rebuild;
+    int tb0, tbn;
+    double mass;
+};
+
+struct RSrc {
+    const double2 *p;
+    long xs, ps;
+};
+
+// Column c of a field: periodic wrap (one shard), in-domain, or the received
+// 4-deep face (t-shard). Clamped so every lane's address is valid; lanes
+// beyond the face depth only feed halo lanes.
+template <int SH>
+__device__ __forceinline__ RSrc rsrc(const double2 *base, const double2 *face, int c, const RAArgs &a) {
+    RSrc s;
+    if (!SH) {
+        int cw = c % a.Wt;
+        if (cw < 0) cw += a.Wt;
+        s.p = base + cw;
+        s.xs = a.Wt;
+        s.ps = a.V;
+    } else if (c >= 0 && c < a.Wt) {
+        s.p = base + c;
+        s.xs = a.Wt;
+        s.ps = a.V;
+    } else {
+        int fc = c < 0 ? c + RH : c - a.Wt + RH;
+        fc = fc < 0 ? 0 : (fc > 2 * RH - 1 ? 2 * RH - 1 : fc);
+        s.p = face + (long)fc * 2 * a.Nx;
+        s.xs = 1;
+        s.ps = a.Nx;
+    }
+    return s;
+}
+
+// D (DAG = 0) / D^dag (DAG = 1) at this lane's column: centre p, x-neighbours
+// pxm / pxp, t-neighbours from the adjacent lanes.
+template <int FOLD, int DAG>
+__device__ __forceinline__ Sp ra_site(double mass, double sr0, double sl0, const Sp &p, const Sp &pxm, const Sp &pxp,
+                                      double2 ut, double2 ux, double2 uxm) {
+    const Sp pm = shr(p), pp = shl(p);
+    const double2 utm = dpp_shr1(ut);
+    Sp o;
+    if (FOLD)
+        dirac_site_folded<DAG>(mass, sr0, sl0, p.a, p.b, pp.a, pp.b, pxp.a, pxp.b, pm.a, pm.b, pxm.a, pxm.b, ut, ux,
+                               utm, uxm, o.a, o.b);
+    else
+        dirac_site<DAG>(mass, sr0, sl0, p.a, p.b, pp.a, pp.b, pxp.a, pxp.b, pm.a, pm.b, pxm.a, pxm.b, ut, ux, utm,
+                        uxm, o.a, o.b);
+    return o;
+}
+
+template <int SH, int XP, int FOLD>
+__global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
+    __shared__ double2 sh[4];
+    __shared__ double2 rlds[3][2][256];
+    CGScalars *sc = a.sc;
+    if (sc->done) return;  // grid-uniform: converged (or max_iter) in an earlier pass
+    const double2 alpha = sc->alpha, beta = sc->beta;     // alpha_{j-1}, beta_{j-1}
+    const double2 alpha2 = sc->alpha2, beta2 = sc->beta2; // alpha_{j-2}, beta_{j-2}
+    int tb, xc;
+    {
+        int w = blockIdx.x;
+        if (a.remap) {  // consecutive ids of one XCD take x-adjacent tiles (L2 reuse of halo rows)
+            const int n = a.tbn * a.XB, q = n >> 3, rr = n & 7, xcd = w & 7;
+            w = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (w >> 3);
+        }
+        tb = a.tb0 + w % a.tbn;
+        if (tb >= a.TBk) tb -= a.TBk;  // edge block-columns TBk-1 and 0 in one launch
+        xc = w / a.tbn;
+    }
+    const int lane = threadIdx.x & 63;
+    const int g = tb * 4 + (threadIdx.x >> 6);
+    const int x0 = xc * a.xchunk;
+    const int xe = min(a.Nx, x0 + a.xchunk);
+    double2 acc_dA = make_double2(0.0, 0.0), acc_rA = make_double2(0.0, 0.0);
+    double2 acc_n = make_double2(0.0, 0.0);  // (|r|^2, |Ad|^2)
+    if (g < a.NWT && x0 < xe) {
+        const int Nx = a.Nx, Wt = a.Wt;
+        const int c = g * RW - RH + lane;
+        const bool own = lane >= RH && lane < RW + RH && c < Wt;
+        int tg = (a.t0 + c) % a.Ntg;
+        if (tg < 0) tg += a.Ntg;
+        const double sr0 = tg == a.Ntg - 1 ? -1.0 : 1.0;  // SignR[2n], include/dirac_operator.h:53-55
+        const double sl0 = tg == 0 ? -1.0 : 1.0;          // SignL[2n], :56-58
+        const double mass = a.mass;
+        const RSrc S1 = rsrc<SH>(a.d1, a.f1, c, a);
+        const RSrc S2 = rsrc<SH>(a.d2, a.f2, c, a);
+        const RSrc SU = rsrc<SH>(a.U, a.fU, c, a);
+        const int cx = c < 0 ? 0 : (c >= Wt ? Wt - 1 : c);
+        const bool first = a.first != 0, rebuild = a.rebuild != 0;
+        auto wrap = [Nx](int x) { int w = x % Nx; return w < 0 ? w + Nx : w; };
+        // d_{j-1}: rows x0-4 .. xe+3; U: x0-4 .. xe+2; d_{j-2}: x0-2 .. xe+1; x: owned rows
+        auto ld1 = [&](int xr, Sp &d) {
+            const double2 *p = S1.p + (long)wrap(min(xr, xe + 3)) * S1.xs;
+            d.a = p[0];
+            d.b = p[S1.ps];
+        };
+        auto ldu = [&](int xr, double2 &ut, double2 &ux) {
+            const double2 *p = SU.p + (long)wrap(min(xr, xe + 2)) * SU.xs;
+            ut = p[0];
+            ux = p[SU.ps];
+        };
+        auto ld2 = [&](int xr, Sp &q, Sp &xv) {
+            const double2 *p = S2.p + (long)wrap(min(max(xr, x0 - 2), xe + 1)) * S2.xs;
+            q.a = p[0];
+            q.b = p[S2.ps];
+            if (XP) {
+                const long n = (long)wrap(min(max(xr, x0), xe - 1)) * Wt + cx;
+                xv.a = a.x[n];
+                xv.b = a.x[n + a.V];
+            }
+        };
+        const double2 z = make_double2(0.0, 0.0);
+        const Sp zs = Sp{z, z};
+        // state at the top of iteration y (see the header)
+        Sp D2, D3, Ld;                                   // d_{j-1}(y+2), (y+3); in flight (y+4)
+        double2 Lut, Lux;                                // in flight U(y+3)
+        Sp Mq, Mx = zs;                                  // in flight d_{j-2}(y+2), x(y+2)
+        double2 Ut0 = z, Ut1 = z, Ut2, Ux0 = z, Ux1 = z, Ux2, Uxm = z;  // U_t(y..y+2), U_x(y-1..y+2)
+        Sp P1 = zs, P2 = zs;                             // T'(y+1), T'(y+2)
+        Sp J0 = zs, J1 = zs;                             // d_j at rows y, y+1
+        Sp Q0 = zs, Q1 = zs;                             // T(y-1), T(y)
+        const int y0 = x0 - 6;
+        ld1(y0 + 2, D2);
+        ld1(y0 + 3, D3);
+        ldu(y0 + 2, Ut2, Ux2);
+        ld1(y0 + 4, Ld);
+        ldu(y0 + 3, Lut, Lux);
+        ld2(y0 + 2, Mq, Mx);
+        int s_w = 2, s_r = 0;  // LDS ring slots of r_j rows y+2 (written) and y (read)
+        // stage mask M: bit 0 = S2 + S3, bit 1 = S4, bit 2 = S5 (S1 always)
+        auto step = [&](int y, auto mtag) {
+            constexpr int M = decltype(mtag)::value;
+            const Sp D4 = Ld;
+            const double2 Ut3 = Lut, Ux3 = Lux;
+            ld1(y + 5, Ld);
+            ldu(y + 4, Lut, Lux);
+            __builtin_amdgcn_sched_barrier(0);  // keep the next rows' loads issued here
+            const Sp P3 = ra_site<FOLD, 1>(mass, sr0, sl0, D3, D2, D4, Ut3, Ux3, Ux2);  // S1: T'(y+3)
+            Sp J2 = zs, Q2 = zs;
+            if constexpr ((M & 1) != 0) {
+                const Sp A = ra_site<FOLD, 0>(mass, sr0, sl0, P2, P1, P3, Ut2, Ux2, Ux1);  // S2: Ad_{j-1}(y+2)
+                // S3: r_j, d_j at row y+2
+                const int xr = y + 2;
+                const Sp Q = Mq, X = Mx;
+                Sp rp, R2;
+                rp.a = rebuild ? csub(D2.a, cmul(Q.a, beta2)) : D2.a;
+                rp.b = rebuild ? csub(D2.b, cmul(Q.b, beta2)) : D2.b;
+                R2.a = first ? rp.a : csub(rp.a, cmul(alpha, A.a));
+                R2.b = first ? rp.b : csub(rp.b, cmul(alpha, A.b));
+                J2.a = first ? D2.a : cadd(cmul(D2.a, beta), R2.a);
+                J2.b = first ? D2.b : cadd(cmul(D2.b, beta), R2.b);
+                if (xr >= x0 && xr < xe && own) {
+                    const long n = (long)xr * Wt + c;
+                    st_nt(a.dn + n, J2.a);
+                    st_nt(a.dn + n + a.V, J2.b);
+                    if (XP) {  // x_j = (x_{j-2} + alpha_{j-2} d_{j-2}) + alpha_{j-1} d_{j-1}
+                        st_nt(a.x + n, cadd(cadd(X.a, cmul(alpha2, Q.a)), cmul(alpha, D2.a)));
+                        st_nt(a.x + n + a.V, cadd(cadd(X.b, cmul(alpha2, Q.b)), cmul(alpha, D2.b)));
+                    }
+                    acc_n.x += cmul(R2.a, cconj(R2.a)).x;  // Re dot(r, r), include/variables.h:185-188
+                    acc_n.x += cmul(R2.b, cconj(R2.b)).x;
+                }
+                rlds[s_w][0][threadIdx.x] = R2.a;
+                rlds[s_w][1][threadIdx.x] = R2.b;
+            }
+            ld2(y + 3, Mq, Mx);  // consumed above: issued now, used next iteration
+            if constexpr ((M & 2) != 0) Q2 = ra_site<FOLD, 1>(mass, sr0, sl0, J1, J0, J2, Ut1, Ux1, Ux0);  // S4: T(y+1)
+            if constexpr ((M & 4) != 0) {
+                const Sp o = ra_site<FOLD, 0>(mass, sr0, sl0, Q1, Q0, Q2, Ut0, Ux0, Uxm);  // S5: Ad_j(y)
+                if (own) {
+                    const Sp R0 = Sp{rlds[s_r][0][threadIdx.x], rlds[s_r][1][threadIdx.x]};
+                    acc_dA = cadd(acc_dA, cmul(J0.a, cconj(o.a)));  // dot(d, Ad)
+                    acc_dA = cadd(acc_dA, cmul(J0.b, cconj(o.b)));
+                    acc_rA = cadd(acc_rA, cmul(R0.a, cconj(o.a)));  // dot(r, Ad)
+                    acc_rA = cadd(acc_rA, cmul(R0.b, cconj(o.b)));
+                    acc_n.y += cmul(o.a, cconj(o.a)).x;            // |Ad|^2
+                    acc_n.y += cmul(o.b, cconj(o.b)).x;
+                }
+            }
+            D2 = D3;
+            D3 = D4;
+            Uxm = Ux0;
+            Ut0 = Ut1;
+            Ux0 = Ux1;
+            Ut1 = Ut2;
+            Ux1 = Ux2;
+            Ut2 = Ut3;
+            Ux2 = Ux3;
+            P1 = P2;
+            P2 = P3;
+            J0 = J1;
+            J1 = J2;
+            Q0 = Q1;
+            Q1 = Q2;
+            s_w = s_w == 2 ? 0 : s_w + 1;
+            s_r = s_r == 2 ? 0 : s_r + 1;
+        };
+        int y = y0;
+        for (; y < x0 - 4; ++y) step(y, std::integral_constant<int, 0>());
+        for (; y < x0 - 2; ++y) step(y, std::integral_constant<int, 1>());
+        for (; y < x0; ++y) step(y, std::integral_constant<int, 3>());
+        for (; y < xe; ++y) step(y, std::integral_constant<int, 7>());
+    }
+    const double2 s0 = block_sum(acc_dA, sh);
+    __syncthreads();
+    const double2 s1 = block_sum(acc_rA, sh);
+    __syncthreads();
+    const double2 s2 = block_sum(acc_n, sh);
+    if (threadIdx.x == 0) {
+        double2 *p = a.partials + 3 * ((long)tb * a.XB + xc);  // one slot per tile
+        p[0] = s0;
+        p[1] = s1;
+        p[2] = s2;
+    }
+}
+
+CGFusedCfg cg_ra_config(const Geometry &g) {
+    CGFusedCfg c;
+    c.NWT = (g.Wt + RW - 1) / RW;
+    c.TBk = (c.NWT + 3) / 4;
+    // rows per block: a chunk re-reads 8 halo rows of d_{j-1} (4 per side) and
+    // runs 6 prologue steps, so chunks stay long; small lattices keep enough
+    // blocks to fill the chip
+    int target = 2048;
+    if (const char *e = getenv("SM_CGRA_BLOCKS")) target = atoi(e);
+    int nchunks = (target + c.TBk - 1) / c.TBk;
+    if (nchunks > g.Nx) nchunks = g.Nx;
+    if (nchunks < 1) nchunks = 1;
+    c.xchunk = (g.Nx + nchunks - 1) / nchunks;
+    if (g.Nx >= 512) {
+        const int xmin = g.Nx / 32 < 16 ? g.Nx / 32 : 16;
+        if (c.xchunk < xmin) c.xchunk = xmin;
+    }
+    if (const char *e = getenv("SM_CGRA_XCHUNK")) c.xchunk = atoi(e);
+    if (c.xchunk < 1) c.xchunk = 1;
+    c.XB = (g.Nx + c.xchunk - 1) / c.xchunk;
+    c.remap = 1;
+    c.fold = 1;
+    if (const char *e = getenv("SM_CGRA_FOLD")) c.fold = atoi(e);
+    return c;
+}
+
+void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard, const double2 *d1,
+                  const double2 *d2, double2 *dn, double2 *x, const double2 *U, const double2 *f1,
+                  const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
+                  int tb0, int tbn) {
+    if (tbn <= 0) return;
+    RAArgs a;
+    a.d1 = d1; a.d2 = d2; a.dn = dn; a.x = x; a.U = U;
+    a.f1 = f1; a.f2 = f2; a.fU = fU;
+    a.sc = sc; a.partials = partials;
+    a.V = g.V; a.Nx = g.Nx; a.Wt = g.Wt; a.t0 = g.t0; a.Ntg = g.Ntg;
+    a.xchunk = c.xchunk; a.NWT = c.NWT; a.TBk = c.TBk; a.XB = c.XB; a.remap = c.remap;
+    a.first = pass == 0;
+    a.rebuild = pass >= 2;  // pass 1 has r_0 = d_0 (no d_{-1})
+    a.tb0 = tb0;
+    a.tbn = tbn;
+    a.mass = mass;
+    const dim3 grid(tbn * c.XB), block(256);
+    const int xp = pass >= 2 && (pass & 1) == 0;  // x takes passes j-1 and j together
+    // one kernel per (shards, x pass, fold) combination
+    const int sel = (nshard > 1 ? 4 : 0) + (xp ? 2 : 0) + (c.fold ? 1 : 0);
+    switch (sel) {
+    case 0: hipLaunchKernelGGL((cg_ra_kernel<0, 0, 0>), grid, block, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((cg_ra_kernel<0, 0, 1>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((cg_ra_kernel<0, 1, 0>), grid, block, 0, s, a); break;
+    case 3: hipLaunchKernelGGL((cg_ra_kernel<0, 1, 1>), grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((cg_ra_kernel<1, 0, 0>), grid, block, 0, s, a); break;
+    case 5: hipLaunchKernelGGL((cg_ra_kernel<1, 0, 1>), grid, block, 0, s, a); break;
+    case 6: hipLaunchKernelGGL((cg_ra_kernel<1, 1, 0>), grid, block, 0, s, a); break;
+    default: hipLaunchKernelGGL((cg_ra_kernel<1, 1, 1>), grid, block, 0, s, a); break;
+    }
+}
+
+// k-deep t-faces: columns 0..k-1 go down (arrive as Wt..Wt+k-1), columns
+// Wt-k..Wt-1 go up (arrive as -k..-1). Buffers [col][plane][x], 2k*Nx complex.
+__global__ void pack_faces_k_kernel(int Nx, int Wt, long V, int k, const double2 *f, double2 *lo, double2 *hi) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= Nx) return;
+    const long row = (long)x * Wt;
+    for (int col = 0; col < k; ++col)
+        for (int p = 0; p < 2; ++p) {
+            lo[(long)(col * 2 + p) * Nx + x] = f[row + col + p * V];
+            hi[(long)(col * 2 + p) * Nx + x] = f[row + Wt - k + col + p * V];
+        }
+}
+
+void launch_pack_faces_k(hipStream_t s, const Geometry &g, int k, const double2 *field, double2 *lo, double2 *hi) {
+    hipLaunchKernelGGL(pack_faces_k_kernel, dim3((g.Nx + 255) / 256), dim3(256), 0, s, g.Nx, g.Wt, g.V, k, field,
+                       lo, hi);
+}
+
+}  // namespace sm

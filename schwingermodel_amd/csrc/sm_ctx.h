@@ -51,11 +51,15 @@ struct sm_ctx {
     sm::Geometry g{};
     sm::LaunchCfg cfg{};
     sm::CGFusedCfg fcfg{};
+    sm::CGFusedCfg racfg{};        // recompute-Ad CG pass (sm_cgra.hip)
     // CG iteration: 0 six kernels, 1 two-pass fused (scalar kernels), 2 two-pass
     // fused with in-kernel scalars, 3 one-pass (sm_cgfused.hip: 288 B/site,
     // 0.979 vs 1.040 ms per iteration at 4096^2, tools/tune_cg.py), 4 the
-    // two-direction one-pass form (the default: no r vector, x every other
-    // pass, 224 B/site; 0.776 vs 1.013 ms per iteration at 4096^2)
+    // two-direction one-pass form (no r vector, x every other pass, 224
+    // B/site; 0.776 vs 1.013 ms per iteration at 4096^2), 5 the two-direction
+    // pass that recomputes Ad instead of storing it (sm_cgra.hip, 160 B/site).
+    // Chosen at creation: 5 where the grid is large or sharded, 4 on small
+    // one-shard grids (redundant in-kernel scalars, latency-bound).
     int cg_fused = 4;
     // one shard: alpha/beta by the last block of each pass instead of two
     // one-block kernels. Measured equal at 4096^2 and 19 % slower at 1024^2
@@ -78,6 +82,7 @@ struct sm_ctx {
     double2 *fields = nullptr;     // NFIELDS * 2V
     double2 *faces = nullptr;      // 4 * 2Nx per spinor being exchanged (x2 for force)
     double2 *faces2 = nullptr;     // 2-deep faces: send lo/hi of 2 fields (4Nx each), recv d, r, U (8Nx each)
+    double2 *faces4 = nullptr;     // 4-deep faces (sm_capi.cpp face4_*): send lo/hi, recv d x2 (by pass parity), U
     double2 *partials = nullptr;   // 2 * max(nparts)
     double2 *sums = nullptr;       // 4 complex scratch (allreduce)
     double *Fbuf = nullptr;        // 2V doubles (force)
@@ -138,8 +143,8 @@ struct CgChunker {
     }
 };
 
-// Largest face exchanged, in doubles per x: 2 columns x 2 planes x complex.
-constexpr size_t kMaxFaceDoubles = 8;
+// Largest face exchanged, in doubles per x: 4 columns x 2 planes x complex.
+constexpr size_t kMaxFaceDoubles = 16;
 
 TFaces faces_for(sm_ctx *c, const double2 *in, const double2 *recv_lo, const double2 *recv_hi);
 double2 *face_buf(sm_ctx *c, int set, int which);
@@ -158,6 +163,8 @@ int check_ready(sm_ctx *c);
 int upload_plane_pair(sm_ctx *c, double2 *dst, const double *p0, const double *p1);
 int download_plane_pair(sm_ctx *c, const double2 *src, double *p0, double *p1);
 double2 *face2_recv(sm_ctx *c, int which);  // 0: d, 1: r, 2: U, 3: Ad
+double2 *face4_recv_U(sm_ctx *c);           // 4-deep ghost links (recompute-Ad CG)
+bool cg_ra_ok(const sm_ctx *c);             // the recompute-Ad pass fits this shard (Wt >= 4 when sharded)
 int exchange_ghost_U(sm_ctx *c);
 
 // even-odd preconditioned pseudofermion action (sm_eo.cpp); phi / chi in the

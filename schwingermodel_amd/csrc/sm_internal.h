@@ -103,9 +103,10 @@ void launch_cg_init_from_sums(hipStream_t s, const double2 *rr_pp, CGScalars *sc
 // ---- fused CG iteration (sm_cgfused.hip) ----
 constexpr int kFusedWaveCols = 60;  // output t-columns per wave (64 lanes - 2x2 halo)
 struct CGFusedCfg {
-    int NWT, TBk;        // wave tiles along t (60 columns each), blocks along t (4 waves)
+    int NWT, TBk;        // wave tiles along t (60 columns each; 56 for sm_cgra.hip), blocks along t (4 waves)
     int xchunk, XB;      // rows per block, blocks along x
     int remap;
+    int fold = 0;        // sm_cgra.hip: folded hopping-bracket arithmetic (dirac_bracket_folded)
 };
 CGFusedCfg cg_fused_config(const Geometry &g);
 int cg_fused_blocks(const CGFusedCfg &c);
@@ -124,6 +125,18 @@ void launch_cg_onepass(hipStream_t s, const Geometry &g, const CGFusedCfg &c, in
                        const double2 *prev_partials = nullptr,  // != null: redundant scalars (see below)
                        long pass = 0,
                        int twodir = 0);  // two-direction form: rold/fr = d_{j-2}, rnew unused
+// Two-direction pass that recomputes Ad_{j-1} = D D^dag d_{j-1} in-kernel
+// instead of storing Ad (sm_cgra.hip): 160 B/site; d_i in d[i % 3] as below.
+// Faces (t-shard, 4-deep [col -4..-1, Wt..Wt+3][plane][x]): f1 = d_{j-1},
+// f2 = d_{j-2} (the previous pass's f1), fU = U.
+constexpr int kRAWaveCols = 56;  // output t-columns per wave (64 lanes - 2x4 halo)
+CGFusedCfg cg_ra_config(const Geometry &g);
+void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard, const double2 *d1,
+                  const double2 *d2, double2 *dn, double2 *x, const double2 *U, const double2 *f1,
+                  const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
+                  int tb0, int tbn);
+// Pack the k-deep t-faces of a field: lo = columns 0..k-1, hi = columns Wt-k..Wt-1, [col][plane][x].
+void launch_pack_faces_k(hipStream_t s, const Geometry &g, int k, const double2 *field, double2 *lo, double2 *hi);
 // Two-direction form, after the last pass J = sc->k: if J is odd, x += alpha_{J-1} d_{J-1}
 // (d_i lives in d[i % 3]).
 void launch_cg_td_finish_x(hipStream_t s, long n, double2 *x, const double2 *d0, const double2 *d1,

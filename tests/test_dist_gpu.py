@@ -45,6 +45,20 @@ def test_sharded_twodir_cg_matches_reference(tmp_path, fixture, world):
     assert all(rep["cg_converged"])
 
 
+@pytest.mark.parametrize("fixture,world", [("l32x48_b3_m-0p10", 4), ("l64x64_b5_m-0p06", 2),
+                                           ("gen:48x1024:0.3:-0.05", 2), ("gen:32x960:0.4242:0.0", 4)])
+def test_sharded_recompute_cg_matches_reference(tmp_path, fixture, world):
+    """The recompute-Ad CG (SM_CG_FUSED=5: 4-deep faces of d_{j-1}, d_{j-2}'s
+    kept from the previous pass, 4-deep ghost links) on t-shards, including the
+    interior/edge split of Wt = 512 / 240: the reference's iteration count and
+    solution."""
+    rep = run_world("gpu", fixture, world, tmp_path, timeout=600, extra_env={"SM_CG_FUSED": "5"})
+    assert rep["checks"]["ref_cgx"] <= 1e-12
+    ref = rep["ref_cg_iters"]
+    assert len(set(rep["cg_iters"])) == 1 and abs(rep["cg_iters"][0] - ref) <= max(1, ref // 100)
+    assert all(rep["cg_converged"])
+
+
 @pytest.mark.parametrize("fixture,world", [("md16x16_hot_m0", 2), ("md32x48_b3_m0p1", 4), ("md64x64_b2_m0", 2)])
 def test_sharded_md_matches_reference(tmp_path, fixture, world):
     """MD layer on t-shards: bitwise plaquette / staples / gauge force, the

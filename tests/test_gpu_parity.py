@@ -51,10 +51,12 @@ def test_operators_bitwise_vs_reference(sm, name):
     assert bits_equal(np.concatenate([F.mu0, F.mu1]), a["ref_force"])
 
 
-@pytest.mark.parametrize("fused", [4, 3, 1, 2, 0], ids=["twodir", "onepass", "fused", "fused_inkernel", "sixkernel"])
+@pytest.mark.parametrize("fused", [5, 4, 3, 1, 2, 0],
+                         ids=["recompute", "twodir", "onepass", "fused", "fused_inkernel", "sixkernel"])
 @pytest.mark.parametrize("name", NAMES)
 def test_cg_vs_reference(sm, name, fused):
-    """Every CG path: the two-direction one-pass iteration (no r vector), the
+    """Every CG path: the two-direction iteration that recomputes Ad in-kernel,
+    the two-direction one-pass iteration (no r vector), the
     one-pass iteration (pass 2 folded into the next pass), the two-pass fused
     iteration with scalar kernels, the same with alpha/beta reduced in-kernel
     by the last block, and the six-kernel sequence."""
@@ -92,11 +94,12 @@ def test_dot_matches_reference(sm, name):
     assert abs(z - zr) <= 1e-13 * abs(zr)
 
 
-@pytest.mark.parametrize("Nx,Nt", [(64, 64), (256, 192)])  # redundant-scalar and scalar-kernel grids
+@pytest.mark.parametrize("Nx,Nt", [(64, 64), (256, 192), (130, 66)])  # redundant-scalar and scalar-kernel grids
 @pytest.mark.parametrize("stop", [16, 17, 1, 2])
 def test_twodir_pending_x_matches_onepass(sm, Nx, Nt, stop):
-    """The two-direction form updates x on even passes only: stopping after an
-    odd or even number of iterations (max_iter) must give the one-pass x."""
+    """The two-direction forms (Ad stored: 4; Ad recomputed: 5) update x on
+    even passes only: stopping after an odd or even number of iterations
+    (max_iter) must give the one-pass x."""
     S = Nx * Nt
     L = sm.init(Nx, Nt)
     U, psi = sm.spinor(S), sm.spinor(S)
@@ -107,7 +110,7 @@ def test_twodir_pending_x_matches_onepass(sm, Nx, Nt, stop):
     old = sm.CG.max_iter
     try:
         sm.CG.max_iter = stop
-        for fused in (3, 4):
+        for fused in (3, 4, 5):
             sm.check(sm.lib.sm_tune_cg(L.ctx, fused, 0))
             x = sm.spinor(S)
             assert sm.conjugate_gradient(U, psi, x, -0.10) == 0
@@ -115,8 +118,9 @@ def test_twodir_pending_x_matches_onepass(sm, Nx, Nt, stop):
             xs[fused] = flat(x)
     finally:
         sm.CG.max_iter = old
-    rel = np.linalg.norm(xs[4] - xs[3]) / np.linalg.norm(xs[3])
-    assert rel <= 1e-13, rel
+    for fused in (4, 5):
+        rel = np.linalg.norm(xs[fused] - xs[3]) / np.linalg.norm(xs[3])
+        assert rel <= 1e-13, (fused, rel)
 
 
 class _Hip:
@@ -162,7 +166,7 @@ def test_twodir_stepwise_finish_matches_onepass(sm, passes):
     sm.check(sm.lib.sm_upload_gauge_dev(L.ctx, dU))
     xs = {}
     try:
-        for fused in (3, 4):
+        for fused in (3, 4, 5):
             sm.check(sm.lib.sm_tune_cg(L.ctx, fused, 0))
             sm.check(sm.lib.sm_cg_begin(L.ctx, dphi, dx, -0.10, 0.0))
             sm.check(sm.lib.sm_cg_iterate(L.ctx, passes))
@@ -173,8 +177,43 @@ def test_twodir_stepwise_finish_matches_onepass(sm, passes):
     finally:
         for p in (dU, dphi, dx):
             hip.rt.hipFree(p)
-    rel = np.linalg.norm(xs[4] - xs[3]) / np.linalg.norm(xs[3])
-    assert rel <= 1e-13, rel
+    for fused in (4, 5):
+        rel = np.linalg.norm(xs[fused] - xs[3]) / np.linalg.norm(xs[3])
+        assert rel <= 1e-13, (fused, rel)
+
+
+@pytest.mark.parametrize("fold", ["1", "0"])
+@pytest.mark.parametrize("Nx,Nt,xchunk", [(96, 120, 0), (200, 56, 7), (5, 9, 0), (64, 64, 64)])
+def test_recompute_matches_twodir(sm, Nx, Nt, xchunk, fold):
+    """The recompute-Ad pass (folded and exact bracket arithmetic) against the
+    two-direction pass that stores Ad: the same iteration count to 1e-10 and
+    x within the reduction-order band, including chunks shorter than the
+    4-row halo, Nt not a multiple of the 56-column wave and a lattice smaller
+    than one wave's halo."""
+    import os
+    S = Nx * Nt
+    old = os.environ.get("SM_CGRA_FOLD")
+    os.environ["SM_CGRA_FOLD"] = fold  # read when the context is created
+    try:
+        L = sm.init(Nx, Nt)
+    finally:
+        if old is None:
+            del os.environ["SM_CGRA_FOLD"]
+        else:
+            os.environ["SM_CGRA_FOLD"] = old
+    U, psi = sm.spinor(S), sm.spinor(S)
+    P = lambda a: a.ctypes.data  # noqa: E731
+    sm.lib.sm_fill_gauge(4321, 0.4242, Nt, 0, Nx, 0, Nt, P(U.mu0), P(U.mu1))
+    sm.lib.sm_fill_spinor(5678, Nt, 0, Nx, 0, Nt, P(psi.mu0), P(psi.mu1))
+    out = {}
+    for fused in (4, 5):
+        sm.check(sm.lib.sm_tune_cg(L.ctx, fused, xchunk if fused == 5 else 0))
+        x = sm.spinor(S)
+        assert sm.conjugate_gradient(U, psi, x, -0.12) == 1
+        out[fused] = (flat(x), L.last_cg.iterations)
+    assert abs(out[5][1] - out[4][1]) <= 1, (out[5][1], out[4][1])
+    rel = np.linalg.norm(out[5][0] - out[4][0]) / np.linalg.norm(out[4][0])
+    assert rel <= 1e-11, rel
 
 
 def test_cg_nonconvergence_semantics(sm, capsys):
