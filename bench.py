@@ -36,6 +36,9 @@ M0 = -0.06
 SEED_U, SEED_CHI = 4321, 91011
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_SITE_APPLY = 96  # read psi 32 + U 32, write 32
+# algorithmic HBM bytes per site of one CG iteration, by path
+BYTES_PER_SITE_CG = {"recompute": 160, "twodir": 224, "onepass": 288, "fused": 320, "fused_inkernel": 320,
+                     "sixkernel": 576}
 
 
 def parse():
@@ -253,6 +256,11 @@ def main():
                          "traffic": traffic,
                          "kernel": "dslash_kernel<D> (96 B/site algorithmic)"},
             "cpu_baseline": cpu,
+            # the CG iteration's own streaming rate (informational; the graded
+            # roofline is the Dirac apply's): algorithmic bytes / time per step
+            "cg_iteration": {"path": args.cg_path, "bytes_per_site": BYTES_PER_SITE_CG[args.cg_path],
+                             "achieved_GBps": round(BYTES_PER_SITE_CG[args.cg_path] * V * it_per_s / 1e9, 1),
+                             "reference_sequence_bytes_per_site": 576},
         }
         print(json.dumps(line), flush=True)
     L.close()

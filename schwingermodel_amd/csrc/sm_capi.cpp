@@ -388,9 +388,11 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     c->nparts_red = reduce_blocks(2 * c->g.V);
     c->fcfg = cg_fused_config(c->g);
     c->racfg = cg_ra_config(c->g);
-    // recompute-Ad pass where the grid is large or sharded; small one-shard
-    // grids keep the two-direction pass with redundant in-kernel scalars
-    c->cg_fused = (nshard > 1 || cg_fused_blocks(c->fcfg) > kInKernelScalarMaxBlocks) ? 5 : 4;
+    // recompute-Ad pass from 1024^2 sites per shard up (tools/tune_cg.py, ms per
+    // iteration against the stored-Ad pass: 1024^2 0.054 vs 0.060, 2048^2 0.174
+    // vs 0.223, 4096^2 0.588 vs 0.778); below that the stored-Ad pass is faster
+    // (512^2 0.028 vs 0.030, 256^2 0.016 vs 0.019)
+    c->cg_fused = c->g.V >= (1L << 20) ? 5 : 4;
     if (const char *e = getenv("SM_CG_FUSED")) c->cg_fused = atoi(e);
     if (const char *e = getenv("SM_CG_INKERNEL_MAX_BLOCKS")) c->cg_inkernel_max_blocks = atoi(e);
     if (const char *e = getenv("SM_CG_REDUNDANT")) c->cg_redundant = atoi(e);
@@ -732,7 +734,7 @@ static int cg_ra_pass(sm_ctx *c) {
     };
     // interior t-blocks: every lane's column (56g-4 .. 56g+59) inside [0, Wt)
     auto interior = [&](int tb) {
-        const int g_lo = 4 * tb, g_hi = std::min(4 * tb + 3, fc.NWT - 1);
+        const int g_lo = fc.wpb * tb, g_hi = std::min(fc.wpb * tb + fc.wpb - 1, fc.NWT - 1);
         return kRAWaveCols * g_lo - 4 >= 0 && kRAWaveCols * g_hi + kRAWaveCols + 3 <= c->g.Wt - 1;
     };
     int tb_lo = 0, tb_hi = -1;

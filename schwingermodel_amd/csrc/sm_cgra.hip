@@ -56,7 +56,7 @@ struct RAArgs {
     double2 *partials;            // 3 per tile: <d,Ad>, <r,Ad>, (|r|^2, |Ad|^2)
     long V;
     int Nx, Wt, t0, Ntg;
-    int xchunk, NWT, TBk, XB, remap, first, rebuild;
+    int xchunk, NWT, TBk, XB, remap, first, rebuild, wpb;
     int tb0, tbn;
     double mass;
 };
@@ -115,8 +115,13 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
     __shared__ double2 rlds[3][2][256];
     CGScalars *sc = a.sc;
     if (sc->done) return;  // grid-uniform: converged (or max_iter) in an earlier pass
-    const double2 alpha = sc->alpha, beta = sc->beta;     // alpha_{j-1}, beta_{j-1}
-    const double2 alpha2 = sc->alpha2, beta2 = sc->beta2; // alpha_{j-2}, beta_{j-2}
+    // Passes 0 and 1 take zero multipliers instead of branches: pass 0 has
+    // d_0 = r_0 (alpha = beta = 0), pass 1 has r_0 = d_0 (beta2 = 0). The
+    // products by zero leave every value unchanged up to the sign of an exact zero.
+    const double2 z2 = make_double2(0.0, 0.0);
+    const bool first = a.first != 0, rebuild = a.rebuild != 0;
+    const double2 alpha = first ? z2 : sc->alpha, beta = first ? z2 : sc->beta;  // alpha_{j-1}, beta_{j-1}
+    const double2 alpha2 = sc->alpha2, beta2 = rebuild ? sc->beta2 : z2;         // alpha_{j-2}, beta_{j-2}
     int tb, xc;
     {
         int w = blockIdx.x;
@@ -129,7 +134,7 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
         xc = w / a.tbn;
     }
     const int lane = threadIdx.x & 63;
-    const int g = tb * 4 + (threadIdx.x >> 6);
+    const int g = tb * a.wpb + (threadIdx.x >> 6);
     const int x0 = xc * a.xchunk;
     const int xe = min(a.Nx, x0 + a.xchunk);
     double2 acc_dA = make_double2(0.0, 0.0), acc_rA = make_double2(0.0, 0.0);
@@ -147,7 +152,6 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
         const RSrc S2 = rsrc<SH>(a.d2, a.f2, c, a);
         const RSrc SU = rsrc<SH>(a.U, a.fU, c, a);
         const int cx = c < 0 ? 0 : (c >= Wt ? Wt - 1 : c);
-        const bool first = a.first != 0, rebuild = a.rebuild != 0;
         auto wrap = [Nx](int x) { int w = x % Nx; return w < 0 ? w + Nx : w; };
         // d_{j-1}: rows x0-4 .. xe+3; U: x0-4 .. xe+2; d_{j-2}: x0-2 .. xe+1; x: owned rows
         auto ld1 = [&](int xr, Sp &d) {
@@ -204,12 +208,12 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
                 const int xr = y + 2;
                 const Sp Q = Mq, X = Mx;
                 Sp rp, R2;
-                rp.a = rebuild ? csub(D2.a, cmul(Q.a, beta2)) : D2.a;
-                rp.b = rebuild ? csub(D2.b, cmul(Q.b, beta2)) : D2.b;
-                R2.a = first ? rp.a : csub(rp.a, cmul(alpha, A.a));
-                R2.b = first ? rp.b : csub(rp.b, cmul(alpha, A.b));
-                J2.a = first ? D2.a : cadd(cmul(D2.a, beta), R2.a);
-                J2.b = first ? D2.b : cadd(cmul(D2.b, beta), R2.b);
+                rp.a = csub(D2.a, cmul(Q.a, beta2));
+                rp.b = csub(D2.b, cmul(Q.b, beta2));
+                R2.a = csub(rp.a, cmul(alpha, A.a));
+                R2.b = csub(rp.b, cmul(alpha, A.b));
+                J2.a = cadd(cmul(D2.a, beta), R2.a);
+                J2.b = cadd(cmul(D2.b, beta), R2.b);
                 if (xr >= x0 && xr < xe && own) {
                     const long n = (long)xr * Wt + c;
                     st_nt(a.dn + n, J2.a);
@@ -260,6 +264,13 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
         for (; y < x0 - 4; ++y) step(y, std::integral_constant<int, 0>());
         for (; y < x0 - 2; ++y) step(y, std::integral_constant<int, 1>());
         for (; y < x0; ++y) step(y, std::integral_constant<int, 3>());
+        // three steps per trip: the period-3 rotations (d_{j-1}, T', d_j, T)
+        // become register renaming instead of copies
+        for (; y + 2 < xe; y += 3) {
+            step(y, std::integral_constant<int, 7>());
+            step(y + 1, std::integral_constant<int, 7>());
+            step(y + 2, std::integral_constant<int, 7>());
+        }
         for (; y < xe; ++y) step(y, std::integral_constant<int, 7>());
     }
     const double2 s0 = block_sum(acc_dA, sh);
@@ -278,25 +289,29 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
 CGFusedCfg cg_ra_config(const Geometry &g) {
     CGFusedCfg c;
     c.NWT = (g.Wt + RW - 1) / RW;
-    c.TBk = (c.NWT + 3) / 4;
+    c.wpb = 4;
+    if (const char *e = getenv("SM_CGRA_WPB")) c.wpb = atoi(e);
+    if (c.wpb != 1 && c.wpb != 2) c.wpb = 4;
+    c.TBk = (c.NWT + c.wpb - 1) / c.wpb;
     // rows per block: a chunk re-reads 8 halo rows of d_{j-1} (4 per side) and
-    // runs 6 prologue steps, so chunks stay long; small lattices keep enough
-    // blocks to fill the chip
-    int target = 2048;
-    if (const char *e = getenv("SM_CGRA_BLOCKS")) target = atoi(e);
-    int nchunks = (target + c.TBk - 1) / c.TBk;
-    if (nchunks > g.Nx) nchunks = g.Nx;
-    if (nchunks < 1) nchunks = 1;
-    c.xchunk = (g.Nx + nchunks - 1) / nchunks;
-    if (g.Nx >= 512) {
-        const int xmin = g.Nx / 32 < 16 ? g.Nx / 32 : 16;
-        if (c.xchunk < xmin) c.xchunk = xmin;
+    // runs 6 prologue steps, so chunks stay long where the grid is big enough
+    // (tools/tune_cg.py, ms per iteration: 4096^2 32 rows 0.588 vs 16 0.604
+    // vs 64 0.596; 2048^2 16 rows 0.174 vs 12 0.183; 1024^2 12 rows 0.054 vs
+    // 16 0.063). Smaller lattices fill the chip first (>= 2 rows).
+    if (g.Nx >= 1024) {
+        c.xchunk = g.Nx >= 4096 ? 32 : (g.Nx >= 2048 ? 16 : 12);
+    } else {
+        int nchunks = (2048 + c.TBk - 1) / c.TBk;
+        if (nchunks > g.Nx) nchunks = g.Nx;
+        if (nchunks < 1) nchunks = 1;
+        c.xchunk = (g.Nx + nchunks - 1) / nchunks;
+        if (c.xchunk < 2) c.xchunk = 2;
     }
     if (const char *e = getenv("SM_CGRA_XCHUNK")) c.xchunk = atoi(e);
     if (c.xchunk < 1) c.xchunk = 1;
     c.XB = (g.Nx + c.xchunk - 1) / c.xchunk;
     c.remap = 1;
-    c.fold = 1;
+    c.fold = 1;  // 0.604 vs 0.625 ms per iteration at 4096^2 (exact bracket arithmetic)
     if (const char *e = getenv("SM_CGRA_FOLD")) c.fold = atoi(e);
     return c;
 }
@@ -311,13 +326,13 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
     a.f1 = f1; a.f2 = f2; a.fU = fU;
     a.sc = sc; a.partials = partials;
     a.V = g.V; a.Nx = g.Nx; a.Wt = g.Wt; a.t0 = g.t0; a.Ntg = g.Ntg;
-    a.xchunk = c.xchunk; a.NWT = c.NWT; a.TBk = c.TBk; a.XB = c.XB; a.remap = c.remap;
+    a.xchunk = c.xchunk; a.NWT = c.NWT; a.TBk = c.TBk; a.XB = c.XB; a.remap = c.remap; a.wpb = c.wpb;
     a.first = pass == 0;
     a.rebuild = pass >= 2;  // pass 1 has r_0 = d_0 (no d_{-1})
     a.tb0 = tb0;
     a.tbn = tbn;
     a.mass = mass;
-    const dim3 grid(tbn * c.XB), block(256);
+    const dim3 grid(tbn * c.XB), block(64 * c.wpb);
     const int xp = pass >= 2 && (pass & 1) == 0;  // x takes passes j-1 and j together
     // one kernel per (shards, x pass, fold) combination
     const int sel = (nshard > 1 ? 4 : 0) + (xp ? 2 : 0) + (c.fold ? 1 : 0);

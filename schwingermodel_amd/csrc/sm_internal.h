@@ -107,6 +107,7 @@ struct CGFusedCfg {
     int xchunk, XB;      // rows per block, blocks along x
     int remap;
     int fold = 0;        // sm_cgra.hip: folded hopping-bracket arithmetic (dirac_bracket_folded)
+    int wpb = 4;         // sm_cgra.hip: waves per block (1, 2, 4)
 };
 CGFusedCfg cg_fused_config(const Geometry &g);
 int cg_fused_blocks(const CGFusedCfg &c);

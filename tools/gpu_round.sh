@@ -1,0 +1,11 @@
+# Full GPU gate + bench + profiles of the current build (outputs under gpurun_out/, tag $1)
+export TMPDIR=/tmp
+T=${1:-cur}
+mkdir -p gpurun_out
+rm -rf gpurun_out/prof_stats_$T gpurun_out/prof_fetch_$T gpurun_out/prof_write_$T
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gputests_$T.log 2>&1 &&
+timeout -k 10 400 python3 bench.py > gpurun_out/bench_$T.log 2>&1 &&
+timeout -k 10 200 python tools/tune_cg.py --n 4096 --paths twodir,recompute --xchunk 0 --iters 40 --rounds 3 > gpurun_out/tune4096_$T.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_stats_$T -o run -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline > gpurun_out/prof_stats_$T.log 2>&1 &&
+timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch_$T -o run -- python3 bench.py --steps 10 --warmup 2 --applies 10 --no-cpu-baseline > gpurun_out/prof_fetch_$T.log 2>&1 &&
+timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write_$T -o run -- python3 bench.py --steps 10 --warmup 2 --applies 10 --no-cpu-baseline > gpurun_out/prof_write_$T.log 2>&1

@@ -42,15 +42,16 @@ def main():
     ap.add_argument("--nx", type=int, default=4096)
     ap.add_argument("--nt", type=int, default=4096)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--suffix", default="", help="input dirs prof_stats<suffix> etc. (tools/gpu_round.sh writes _<tag>)")
     a = ap.parse_args()
     pdir = os.path.join(REPO, "profiles")
     os.makedirs(pdir, exist_ok=True)
     tag = f"{a.round}{a.tag}"
-    stats = os.path.join(a.out_dir, "prof_stats", "run_kernel_stats.csv")
+    stats = os.path.join(a.out_dir, "prof_stats" + a.suffix, "run_kernel_stats.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(pdir, f"{tag}_kernel_stats.csv"))
-    fetch = per_kernel(os.path.join(a.out_dir, "prof_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
-    write = per_kernel(os.path.join(a.out_dir, "prof_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    fetch = per_kernel(os.path.join(a.out_dir, "prof_fetch" + a.suffix, "run_counter_collection.csv"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(a.out_dir, "prof_write" + a.suffix, "run_counter_collection.csv"), "WRITE_SIZE")
     avg_ns = {}
     if os.path.exists(stats):
         with open(stats) as f:
