@@ -149,14 +149,21 @@ def main():
     ap.add_argument("--hmc", action="store_true")
     ap.add_argument("--hmc-ref", action="store_true", help="with --hmc: also the CPU reference (~4 min)")
     ap.add_argument("--hmc-large", type=int, default=0)
+    ap.add_argument("--tag", default="", help="cg_path tag added to every line")
     a = ap.parse_args()
+
+    def emit(d):
+        if a.tag:
+            d["cg_path"] = a.tag
+        print(json.dumps(d), flush=True)
+
     for cid in [int(v) for v in a.configs.split(",") if v]:
-        print(json.dumps(run_config(cid)), flush=True)
+        emit(run_config(cid))
     if a.hmc:
-        print(json.dumps(run_hmc(a.hmc_ref)), flush=True)
+        emit(run_hmc(a.hmc_ref))
     if a.hmc_large:
-        print(json.dumps(run_hmc_large(a.hmc_large)), flush=True)
-        print(json.dumps(run_hmc_large(a.hmc_large, even_odd=1)), flush=True)
+        emit(run_hmc_large(a.hmc_large))
+        emit(run_hmc_large(a.hmc_large, even_odd=1))
 
 
 if __name__ == "__main__":

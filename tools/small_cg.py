@@ -18,7 +18,7 @@ import time
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-PATHS = {"sixkernel": 0, "fused": 1, "fused_inkernel": 2, "onepass": 3, "twodir": 4}
+PATHS = {"sixkernel": 0, "fused": 1, "fused_inkernel": 2, "onepass": 3, "twodir": 4, "recompute": 5}
 
 
 def main():
