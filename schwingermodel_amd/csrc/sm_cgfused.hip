@@ -549,12 +549,28 @@ constexpr int SB = 1024;
 __device__ void sum3_partials(int nparts, const double2 *part, double2 out[3]) {
     __shared__ double2 sh[3][SB / 64];
     double2 acc[3] = {make_double2(0.0, 0.0), make_double2(0.0, 0.0), make_double2(0.0, 0.0)};
-    for (int i = threadIdx.x; i < nparts; i += SB) {
-        const double2 *p = part + 3 * (long)i;
-        const double2 v0 = p[0], v1 = p[1], v2 = p[2];
-        acc[0] = cadd(acc[0], v0);
-        acc[1] = cadd(acc[1], v1);
-        acc[2] = cadd(acc[2], v2);
+    // a thread's partials i = tid, tid + SB, ... summed in that order; up to
+    // four of them loaded together (one memory latency instead of four)
+    constexpr int K = 4;
+    for (int base = threadIdx.x; base < nparts; base += K * SB) {
+        double2 v[K][3];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int i = base + k * SB;
+            if (i < nparts) {
+                const double2 *p = part + 3 * (long)i;
+                v[k][0] = p[0];
+                v[k][1] = p[1];
+                v[k][2] = p[2];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (base + k * SB < nparts) {
+                acc[0] = cadd(acc[0], v[k][0]);
+                acc[1] = cadd(acc[1], v[k][1]);
+                acc[2] = cadd(acc[2], v[k][2]);
+            }
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
@@ -645,18 +661,18 @@ void launch_cg1_flush(hipStream_t s, int nparts, const double2 *partials, CGScal
 }
 
 __global__ void __launch_bounds__(SB) cg1_scalar_kernel(int nparts, const double2 *part, CGScalars *sc, int first) {
-    if (sc->done) return;
+    // the partial loads do not wait for the `done` flag's load: a finished
+    // solve only skips the scalar update
     double2 t[3];
     sum3_partials(nparts, part, t);
-    if (threadIdx.x == 0) cg1_scalars(sc, first, t[0], t[1], t[2]);
+    if (threadIdx.x == 0 && !sc->done) cg1_scalars(sc, first, t[0], t[1], t[2]);
 }
 
 // Multi-shard: local sums into sc->sum3 (all-reduced by the host), then the scalars.
 __global__ void __launch_bounds__(SB) cg1_local_sum_kernel(int nparts, const double2 *part, CGScalars *sc) {
-    if (sc->done) return;
     double2 t[3];
     sum3_partials(nparts, part, t);
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && !sc->done) {
         sc->sum3[0] = t[0];
         sc->sum3[1] = t[1];
         sc->sum3[2] = t[2];
