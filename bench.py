@@ -233,8 +233,8 @@ def main():
         line = {
             "metric": "CG iterations/sec + Dirac-apply achieved HBM GB/s, 4096^2 fp64",
             "value": round(value, 3),
-            "unit": ("CG iterations/s (one 4096x4096 lattice over all GPUs)" if args.strong
-                     else "CG iterations/s (4096x4096 sites per GPU, whole job)"),
+            "unit": (f"CG iterations/s (one {Nx}x{Nt} lattice over all GPUs)" if args.strong
+                     else f"CG iterations/s ({Nx}x{Wt} sites per GPU, whole job)"),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
