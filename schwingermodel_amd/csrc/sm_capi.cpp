@@ -134,26 +134,35 @@ int apply(sm_ctx *c, const double2 *in, double2 *out, double mass, int dagger, c
           double2 *partials, const CGScalars *skip) {
     TFaces f;
     const int TB = (c->g.Wt + c->cfg.bt - 1) / c->cfg.bt;
-    if (c->nshard == 1 || TB < 3) {
+    const bool one = c->nshard == 1;
+    if (TB < 3 || (one && !c->split_test)) {
         TRY(halo(c, in, 0, &f));
         launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip);
     } else {
-        // t-blocks 1..TB-2 never touch t = 0 / Wt-1: run them while the faces
-        // travel on the comm stream, then the two edge block-columns
+        // t-blocks 1..TB-2 never touch t = 0 / Wt-1: they run on the main
+        // stream while the faces travel on the comm stream; the two edge
+        // block-columns follow the faces there, concurrently with the interior
+        const bool conc = one ? c->split_test == 2 : c->edge_concurrent != 0;
         double2 *slo = face_buf(c, 0, 0), *shi = face_buf(c, 0, 1);
         double2 *rlo = face_buf(c, 0, 2), *rhi = face_buf(c, 0, 3);
         HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
         HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
-        launch_pack_faces(c->comm_stream, c->g, in, slo, shi);
-        TRY(exchange_faces_on(c, c->comm_stream, slo, shi, rlo, rhi, (size_t)4 * c->g.Nx));
+        if (!one) {
+            launch_pack_faces(c->comm_stream, c->g, in, slo, shi);
+            TRY(exchange_faces_on(c, c->comm_stream, slo, shi, rlo, rhi, (size_t)4 * c->g.Nx));
+        }
+        f = one ? faces_for(c, in, nullptr, nullptr) : faces_for(c, in, rlo, rhi);
+        // both edge block-columns (TB-1, then 0 by wrap-around) in one launch
+        if (conc)
+            launch_dslash(c->comm_stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip,
+                          TB - 1, 2);
         HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
-        f = faces_for(c, in, rlo, rhi);
         launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip,
                       1, TB - 2);
         HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
-        // both edge block-columns (TB-1, then 0 by wrap-around) in one launch
-        launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip,
-                      TB - 1, 2);
+        if (!conc)
+            launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip,
+                          TB - 1, 2);
     }
     HIP_TRY(hipGetLastError());
     return SM_OK;
@@ -394,6 +403,8 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     // (512^2 0.028 vs 0.030, 256^2 0.016 vs 0.019)
     c->cg_fused = c->g.V >= (1L << 20) ? 5 : 4;
     if (const char *e = getenv("SM_CG_FUSED")) c->cg_fused = atoi(e);
+    if (const char *e = getenv("SM_EDGE_CONCURRENT")) c->edge_concurrent = atoi(e);
+    if (const char *e = getenv("SM_SPLIT_TEST")) c->split_test = atoi(e);
     if (const char *e = getenv("SM_CG_INKERNEL_MAX_BLOCKS")) c->cg_inkernel_max_blocks = atoi(e);
     if (const char *e = getenv("SM_CG_REDUNDANT")) c->cg_redundant = atoi(e);
     if (const char *e = getenv("SM_EO_FUSED")) c->eo_fused = atoi(e);
@@ -663,15 +674,15 @@ static int cg_onepass(sm_ctx *c) {
     const bool redundant = inkernel && c->cg_redundant;
     double2 *part = redundant ? c->partials + (j & 1) * 3 * (size_t)nparts : c->partials;
     const double2 *prev = redundant ? c->partials + ((j + 1) & 1) * 3 * (size_t)nparts : nullptr;
-    auto pass = [&](int tb0, int tbn) {
-        launch_cg_onepass(c->stream, c->g, fc, c->nshard, dold, rold, aold, dnew, rnew, anew, c->cg_x, c->U,
+    auto pass = [&](int tb0, int tbn, hipStream_t st) {
+        launch_cg_onepass(st, c->g, fc, c->nshard, dold, rold, aold, dnew, rnew, anew, c->cg_x, c->U,
                           face2_recv(c, 0), face2_recv(c, 1), face2_recv(c, 3), face2_recv(c, 2), c->cg_mass,
                           first, c->sc, part, tb0, tbn, inkernel && !redundant ? c->counters : nullptr, prev, j,
                           td);
     };
     if (td) c->cg_pending_x = 1;  // sm_cg_finish checks the device's final pass parity
     if (c->nshard == 1) {
-        pass(0, fc.TBk);
+        pass(0, fc.TBk, c->stream);
         if (!inkernel) launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
         c->cg_flush_pass = redundant ? j : -1;
         return SM_OK;
@@ -693,13 +704,17 @@ static int cg_onepass(sm_ctx *c) {
     HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
     TRY(halo2_multi(c, c->comm_stream, flds, fcs, 3));
+    // edge t-blocks (tb_hi, TBk) and [0, tb_lo), wrapping: one launch, on the
+    // comm stream behind the faces, concurrent with the interior launch
+    const bool conc = split && c->edge_concurrent;
+    if (conc) pass(tb_hi + 1, fc.TBk - 1 - tb_hi + tb_lo, c->comm_stream);
     HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
-    if (split) pass(tb_lo, tb_hi - tb_lo + 1);
+    if (split) pass(tb_lo, tb_hi - tb_lo + 1, c->stream);
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
-    if (split) {
-        pass(tb_hi + 1, fc.TBk - 1 - tb_hi + tb_lo);  // edge t-blocks (tb_hi, TBk) and [0, tb_lo), wrapping: one launch
-    } else {
-        pass(0, fc.TBk);
+    if (!split) {
+        pass(0, fc.TBk, c->stream);
+    } else if (!conc) {
+        pass(tb_hi + 1, fc.TBk - 1 - tb_hi + tb_lo, c->stream);
     }
     launch_cg1_local_sum(c->stream, nparts, c->partials, c->sc);
     TRY(allreduce_dev(c, (double *)c->sc->sum3, 6));
@@ -721,16 +736,17 @@ static int cg_ra_pass(sm_ctx *c) {
     const int nparts = cg_fused_blocks(fc);
     c->cg_pending_x = 1;  // sm_cg_finish checks the device's final pass parity
     c->cg_flush_pass = -1;
-    if (c->nshard == 1) {
+    const bool one = c->nshard == 1;
+    if (one && !c->split_test) {
         launch_cg_ra(c->stream, c->g, fc, 1, d1, d2, dn, c->cg_x, c->U, nullptr, nullptr, nullptr, c->cg_mass, j,
                      c->sc, c->partials, 0, fc.TBk);
         launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
         return SM_OK;
     }
-    double2 *f1 = face4_recv_d(c, j), *f2 = face4_recv_d(c, j - 1);
-    auto pass = [&](int tb0, int tbn) {
-        launch_cg_ra(c->stream, c->g, fc, c->nshard, d1, d2, dn, c->cg_x, c->U, f1, f2, face4_recv_U(c), c->cg_mass,
-                     j, c->sc, c->partials, tb0, tbn);
+    double2 *f1 = one ? nullptr : face4_recv_d(c, j), *f2 = one ? nullptr : face4_recv_d(c, j - 1);
+    auto pass = [&](int tb0, int tbn, hipStream_t st) {
+        launch_cg_ra(st, c->g, fc, c->nshard, d1, d2, dn, c->cg_x, c->U, f1, f2, one ? nullptr : face4_recv_U(c),
+                     c->cg_mass, j, c->sc, c->partials, tb0, tbn);
     };
     // interior t-blocks: every lane's column (56g-4 .. 56g+59) inside [0, Wt)
     auto interior = [&](int tb) {
@@ -746,14 +762,22 @@ static int cg_ra_pass(sm_ctx *c) {
     const bool split = tb_hi >= tb_lo && tb_hi >= 0;
     HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
-    TRY(halo4(c, c->comm_stream, d1, f1));
+    if (!one) TRY(halo4(c, c->comm_stream, d1, f1));
+    // edge t-blocks (tb_hi, TBk) and [0, tb_lo), wrapping: one launch on the
+    // comm stream behind the faces, concurrent with the interior launch
+    const bool conc = split && (one ? c->split_test == 2 : c->edge_concurrent != 0);
+    if (conc) pass(tb_hi + 1, fc.TBk - 1 - tb_hi + tb_lo, c->comm_stream);
     HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
-    if (split) pass(tb_lo, tb_hi - tb_lo + 1);
+    if (split) pass(tb_lo, tb_hi - tb_lo + 1, c->stream);
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
-    if (split) {
-        pass(tb_hi + 1, fc.TBk - 1 - tb_hi + tb_lo);  // edge t-blocks (tb_hi, TBk) and [0, tb_lo), wrapping
-    } else {
-        pass(0, fc.TBk);
+    if (!split) {
+        pass(0, fc.TBk, c->stream);
+    } else if (!conc) {
+        pass(tb_hi + 1, fc.TBk - 1 - tb_hi + tb_lo, c->stream);
+    }
+    if (one) {
+        launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
+        return SM_OK;
     }
     launch_cg1_local_sum(c->stream, nparts, c->partials, c->sc);
     TRY(allreduce_dev(c, (double *)c->sc->sum3, 6));

@@ -71,6 +71,12 @@ struct sm_ctx {
     hipStream_t own_stream = nullptr, stream = nullptr;
     hipStream_t comm_stream = nullptr;  // halo exchange overlapped with interior compute
     hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
+    // t-shards: the edge block-columns run on the comm stream right after the
+    // halo, concurrently with the interior launch (0: after it, on the main
+    // stream). split_test > 0 runs the same interior/edge split on ONE shard
+    // (1: edge after interior, 2: concurrent) to measure it on one GPU.
+    int edge_concurrent = 1;
+    int split_test = 0;
     ncclComm_t comm = nullptr;
     bool hosted = false;            // host-callback transport instead of RCCL
     sm_host_transport tr{};
