@@ -46,12 +46,14 @@ def test_sharded_twodir_cg_matches_reference(tmp_path, fixture, world):
 
 
 @pytest.mark.parametrize("fixture,world", [("l32x48_b3_m-0p10", 4), ("l64x64_b5_m-0p06", 2),
-                                           ("gen:48x1024:0.3:-0.05", 2), ("gen:32x960:0.4242:0.0", 4)])
+                                           ("gen:48x1024:0.3:-0.05", 2), ("gen:32x960:0.4242:0.0", 4),
+                                           ("l16x16_b2_m-0p19", 4), ("l16x16_b2_m-0p19", 8)])
 def test_sharded_recompute_cg_matches_reference(tmp_path, fixture, world):
     """The recompute-Ad CG (SM_CG_FUSED=5: 4-deep faces of d_{j-1}, d_{j-2}'s
     kept from the previous pass, 4-deep ghost links) on t-shards, including the
-    interior/edge split of Wt = 512 / 240: the reference's iteration count and
-    solution."""
+    interior/edge split of Wt = 512 / 240, the narrowest shard it takes (Wt = 4)
+    and the fall-back to the stored-Ad pass below it (Wt = 2): the reference's
+    iteration count and solution."""
     rep = run_world("gpu", fixture, world, tmp_path, timeout=600, extra_env={"SM_CG_FUSED": "5"})
     assert rep["checks"]["ref_cgx"] <= 1e-12
     ref = rep["ref_cg_iters"]
