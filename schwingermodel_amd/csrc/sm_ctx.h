@@ -106,6 +106,8 @@ struct sm_ctx {
     double2 *Ucb = nullptr;         // gauge field in checkerboard layout (even, odd)
     double2 *eo_faces = nullptr;    // t-sharded: checkerboard face slots (sm_eo.cpp)
     int eo_fused = 1;               // Dhat as one fused marching pass (0: two hop launches)
+    int eo_cg_td = 1;               // even-odd CG: the one-pass two-direction kernel (sm_eotd.hip, one shard;
+                                    // 0.54 vs 0.94 ms per iteration at 4096^2 for the six launches)
     int eo_cg_folded = 0;           // even-odd CG: 1 = 2 passes + scalars per iteration (opt-in:
                                     // measured slower than the 6 launches from 512^2 to 2048^2)
     // active CG

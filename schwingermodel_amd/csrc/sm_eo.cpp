@@ -200,9 +200,69 @@ static int eo_cg_folded(sm_ctx *c, const double2 *b, double2 *x, double mass, do
     return SM_OK;
 }
 
+// One-pass two-direction CG on Dhat Dhat^dag (c->eo_cg_td, one shard;
+// sm_eotd.hip): pass j forms r_j, d_j, the even-pass x update and Ad_j =
+// Dhat Dhat^dag d_j in one launch, then cg1_scalars. d_i rotates through three
+// buffers (d_0 from cg_init in EO_D), Ad_j goes to abuf[j & 1]; after an odd
+// final pass the pending alpha d is added (launch_cg_td_finish_x). ~256 B per
+// even site and pass against ~575 for the six-launch iteration.
+static int eo_cg_twodir(sm_ctx *c, const double2 *b, double2 *x, double mass, double tol, int max_iter,
+                        sm_cg_result *res) {
+    const long n = c->g.V;
+    const int nred = reduce_blocks(n);
+    double2 *dslot[3] = {eo_vec(c, EO_D2), eo_vec(c, EO_R), eo_vec(c, EO_D)};
+    auto dbuf = [&](long i) { return dslot[((i % 3) + 3) % 3]; };
+    double2 *abuf[2] = {eo_vec(c, EO_AD), eo_vec(c, EO_R2)};
+    if (x != b) launch_copy(c->stream, n, b, x);
+    int np;
+    TRY(eo_M(c, x, eo_vec(c, EO_AD), mass, &np));
+    double2 *prr = c->partials, *ppp = c->partials + nred;
+    launch_cg_init(c->stream, n, b, eo_vec(c, EO_AD), eo_vec(c, EO_R), eo_vec(c, EO_D), prr, ppp);  // r_0, d_0
+    launch_cg_finalize_init(c->stream, nred, prr, ppp, c->sc, tol);
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)&c->sc->max_iter, max_iter, 1, c->stream));
+    const EoTdCfg cfg = eo_td_config(c->g);
+    const int nparts = eo_td_blocks(cfg);
+    if (3 * nparts > 2 * kMaxPartials) return fail(SM_ERR_ARG, "even-odd CG grid too large");
+    long j = 0;
+    auto pass = [&]() {
+        const bool first = j == 0;
+        // pass 0 reads d_0 and takes zero multipliers: its d_{j-2} / Ad_{j-1}
+        // operands only need to be finite, so they alias d_0 too
+        const double2 *d1 = first ? eo_vec(c, EO_D) : dbuf(j - 1);
+        const double2 *d2 = j >= 2 ? dbuf(j - 2) : d1;
+        const double2 *aold = first ? d1 : abuf[(j - 1) & 1];
+        launch_eo_td(c->stream, c->g, cfg, d1, d2, aold, dbuf(j), abuf[j & 1], x, ucb(c, 0), ucb(c, 1), mass, j,
+                     c->sc, c->partials);
+        launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
+        ++j;
+    };
+    const long passes = (long)max_iter + 1;
+    CgChunker plan;
+    int chunk = plan.chunk;
+    while (j < passes) {
+        const long nb = (passes - j) < chunk ? (passes - j) : chunk;
+        for (long i = 0; i < nb; ++i) pass();
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(c->h_sc, c->sc, sizeof(CGScalars), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (c->h_sc->done) break;
+        chunk = plan.next(c->h_sc->k, c->h_sc->err, tol * c->h_sc->phi_norm);
+    }
+    launch_cg_td_finish_x(c->stream, n, x, dbuf(0), dbuf(1), dbuf(2), c->sc);  // odd final pass: pending alpha d
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(c->h_sc, c->sc, sizeof(CGScalars), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    res->converged = c->h_sc->converged;
+    res->iterations = c->h_sc->k;
+    res->residual = c->h_sc->err;
+    res->phi_norm = c->h_sc->phi_norm;
+    return SM_OK;
+}
+
 // CG on Dhat Dhat^dag x = b (x0 = b, the reference's convention), the
 // reference's recurrence and stop test on half-lattice vectors.
 int eo_cg(sm_ctx *c, const double2 *b, double2 *x, double mass, double tol, int max_iter, sm_cg_result *res) {
+    if (c->eo_cg_td && c->nshard == 1) return eo_cg_twodir(c, b, x, mass, tol, max_iter, res);
     if (c->eo_cg_folded && c->eo_fused) return eo_cg_folded(c, b, x, mass, tol, max_iter, res);
     const long n = c->g.V;  // complex entries of an even vector
     const int nparts = reduce_blocks(n);

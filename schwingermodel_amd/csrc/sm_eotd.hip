@@ -1,0 +1,281 @@
+// sm_eotd.hip -- one-pass even-odd CG iteration on Dhat Dhat^dag (gfx950),
+// the two-direction recurrence of sm_cgfused.hip on half-lattice vectors.
+//
+// Pass j (even sites; r is never stored, Ad is):
+//     r_{j-1} = d_{j-1} - d_{j-2} beta_{j-2};  r_j = r_{j-1} - alpha_{j-1} Ad_{j-1}
+//     d_j = d_{j-1} beta_{j-1} + r_j;  on even j x <- (x + alpha_{j-2} d_{j-2}) + alpha_{j-1} d_{j-1}
+//     W = Dhat^dag d_j,  Ad_j = Dhat W  (four checkerboard hops, in registers)
+//     partials |W|^2 (= <d_j, Ad_j>), <r_j, Ad_j>, |r_j|^2, |Ad_j|^2
+// then cg1_scalars as for the full operator (sm_cgfused.hip). A pass reads
+// d_{j-1}, d_{j-2}, Ad_{j-1} and both link parities (160 B per even site) and
+// writes d_j, Ad_j (64) plus x on even passes: ~256 B per even site against
+// ~575 for the six-launch iteration (sm_eo.cpp eo_cg).
+//
+// Layout (sm_eo.hip): a parity-p field holds Vh = Nx*Wh sites, h = x*Wh + k,
+// t = 2k + ((p + x) & 1). Hops between parities use entries k-1+s, k+s of the
+// same row (s row-dependent) and entry k of rows x +- 1. A wave owns 56
+// k-columns (4 halo lanes per side: one per hop), rows march along x:
+//     F   row y+4: r_j, d_j                       (d_{j-1}, d_{j-2}, Ad_{j-1} loaded)
+//     H1  row y+3: T1 = D_oe^dag-hop of d_j        (odd)
+//     H2  row y+2: W  = Dhat^dag d_j               (even; |W|^2)
+//     H3  row y+1: T2 = D_oe-hop of W              (odd)
+//     H4  row y  : Ad_j = Dhat W                   (even; dots with r_j(y))
+// The hops use the folded bracket (dirac_bracket_folded): the same values as
+// the reference arithmetic up to the sign of an exact zero. One shard only.
+// Registers: 256 VGPRs + ~105 AGPRs, so one wave per SIMD; measured 0.54 ms
+// per iteration at 4096^2 against 0.94 ms for the six launches.
+#include <type_traits>
+
+#include "sm_device.h"
+#include "sm_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace sm {
+
+constexpr int EW4 = kEoTdWaveCols;
+constexpr int EH4 = 4;  // halo lanes per side
+
+struct EoTDArgs {
+    const double2 *d1, *d2, *aold;  // d_{j-1}, d_{j-2}, Ad_{j-1}
+    double2 *dn, *anew, *x;
+    const double2 *Ue, *Uo;         // checkerboard links: plane 0 U_t, plane 1 U_x
+    CGScalars *sc;
+    double2 *partials;              // 3 per block: (|W|^2, 0), <r,Ad>, (|r|^2, |Ad|^2)
+    long Vh;
+    int Nx, Wh, t0, Ntg;
+    int xchunk, NWT, TBk, XB, first, rebuild;
+    double mass;
+};
+
+template <int XP>
+__global__ void __launch_bounds__(256) eo_td_kernel(EoTDArgs a) {
+    __shared__ double2 sh[4];
+    __shared__ double2 rlds[5][2][256];  // r_j of rows y .. y+4
+    CGScalars *sc = a.sc;
+    if (sc->done) return;  // grid-uniform
+    const double2 z2 = make_double2(0.0, 0.0);
+    const bool first = a.first != 0, rebuild = a.rebuild != 0;
+    const double2 alpha = first ? z2 : sc->alpha, beta = first ? z2 : sc->beta;
+    const double2 alpha2 = sc->alpha2, beta2 = rebuild ? sc->beta2 : z2;
+    const int tb = blockIdx.x % a.TBk, xc = blockIdx.x / a.TBk;
+    const int lane = threadIdx.x & 63;
+    const int gw = tb * 4 + (threadIdx.x >> 6);
+    const int x0 = xc * a.xchunk, xe = min(a.Nx, x0 + a.xchunk);
+    double aW = 0.0, aR = 0.0, aA = 0.0;  // |W|^2, |r|^2, |Ad|^2
+    double2 aRA = z2;                      // <r, Ad>
+    if (gw < a.NWT && x0 < xe) {
+        const int Wh = a.Wh, Nx = a.Nx;
+        const long Vh = a.Vh;
+        const int k = gw * EW4 - EH4 + lane;
+        int kw = k % Wh;
+        if (kw < 0) kw += Wh;
+        const bool own = lane >= EH4 && lane < EW4 + EH4 && k < Wh;
+        const double m = a.mass, hm = 0.5 / a.mass;
+        auto wrapx = [Nx](int x) { int w = x % Nx; return w < 0 ? w + Nx : w; };
+        auto hidx = [&](int y) { return (long)wrapx(y) * Wh + kw; };
+        auto signs = [&](int t, double &sr0, double &sl0) {
+            int tg = (a.t0 + t) % a.Ntg;
+            if (tg < 0) tg += a.Ntg;
+            sr0 = tg == a.Ntg - 1 ? -1.0 : 1.0;
+            sl0 = tg == 0 ? -1.0 : 1.0;
+        };
+        struct Lk {
+            double2 et, ex, ot, ox;  // even / odd links at (y, k)
+        };
+        auto ldl = [&](int y, Lk &L) {
+            const long h = hidx(min(max(y, x0 - 4), xe + 2));
+            L.et = a.Ue[h];
+            L.ex = a.Ue[h + Vh];
+            L.ot = a.Uo[h];
+            L.ox = a.Uo[h + Vh];
+        };
+        struct Fr {
+            Sp d1, d2, ad, xv;
+        };
+        auto ldf = [&](int y, Fr &F) {
+            const long h = hidx(min(max(y, x0 - 4), xe + 3));
+            F.d1 = Sp{a.d1[h], a.d1[h + Vh]};
+            F.d2 = Sp{a.d2[h], a.d2[h + Vh]};
+            F.ad = Sp{a.aold[h], a.aold[h + Vh]};
+            if (XP) {
+                const long hx = hidx(min(max(y, x0), xe - 1));
+                F.xv = Sp{a.x[hx], a.x[hx + Vh]};
+            }
+        };
+        // odd hop at odd site (y, k) from an even field: T = -0.5 H_oe v
+        auto todd = [&](auto dag, int y, const Sp &vc, const Sp &vxm, const Sp &vxp, const Lk &L, double2 ex_m) {
+            constexpr int DG = decltype(dag)::value;
+            const bool ye = (y & 1) == 0;
+            const Sp pm = ye ? vc : shr(vc), pp = ye ? shl(vc) : vc;
+            const double2 utm = ye ? L.et : dpp_shr1(L.et);
+            double sr0, sl0;
+            signs(2 * k + (ye ? 1 : 0), sr0, sl0);
+            double2 h0, h1;
+            dirac_bracket_folded<DG>(sr0, sl0, pp.a, pp.b, vxp.a, vxp.b, pm.a, pm.b, vxm.a, vxm.b, L.ot, L.ox, utm,
+                                     ex_m, h0, h1);
+            return Sp{rmul(-0.5, h0), rmul(-0.5, h1)};
+        };
+        // even hop at even site (x, k) from an odd field: m v + (0.5/m) H_eo T
+        auto eout = [&](auto dag, int x, const Sp &Tc, const Sp &Txm, const Sp &Txp, const Lk &L, double2 ox_m,
+                        const Sp &vc) {
+            constexpr int DG = decltype(dag)::value;
+            const bool xev = (x & 1) == 0;
+            const Sp pm = xev ? shr(Tc) : Tc, pp = xev ? Tc : shl(Tc);
+            const double2 utm = xev ? dpp_shr1(L.ot) : L.ot;
+            double sr0, sl0;
+            signs(2 * k + (xev ? 0 : 1), sr0, sl0);
+            double2 h0, h1;
+            dirac_bracket_folded<DG>(sr0, sl0, pp.a, pp.b, Txp.a, Txp.b, pm.a, pm.b, Txm.a, Txm.b, L.et, L.ex, utm,
+                                     ox_m, h0, h1);
+            return Sp{cadd(rmul(m, vc.a), rmul(hm, h0)), cadd(rmul(m, vc.b), rmul(hm, h1))};
+        };
+        using DAG1 = std::integral_constant<int, 1>;
+        using DAG0 = std::integral_constant<int, 0>;
+        const double2 z = z2;
+        const Sp zs = Sp{z, z};
+        const Lk zl = Lk{z, z, z, z};
+        // state at the top of iteration y (links Lk at rows y-1 .. y+2 held, y+3 in flight)
+        Fr Fin;                            // in flight: row y+4
+        Lk Lin;                            // in flight: row y+3
+        Lk Lm = zl, L0 = zl, L1 = zl, L2 = zl;  // rows y-1, y, y+1, y+2
+        Sp J2 = zs, J3 = zs;               // d_j rows y+2, y+3
+        Sp A1 = zs, A2 = zs;               // T1 rows y+1, y+2
+        Sp W0 = zs, W1 = zs;               // W rows y, y+1
+        Sp B0 = zs, Bm = zs;               // T2 rows y, y-1
+        Fin.xv = zs;
+        const int y0 = x0 - 8;
+        ldf(y0 + 4, Fin);
+        ldl(y0 + 3, Lin);
+        int s_w = 4, s_r = 0;              // r_j ring slots of rows y+4 (written) and y (read)
+        // stage mask M: bit 0 H1, bit 1 H2, bit 2 H3, bit 3 H4 (F always)
+        auto step = [&](int y, auto mtag) {
+            constexpr int M = decltype(mtag)::value;
+            const Fr F = Fin;
+            const Lk L3 = Lin;
+            ldf(y + 5, Fin);
+            ldl(y + 4, Lin);
+            __builtin_amdgcn_sched_barrier(0);
+            // F: r_j, d_j at row y+4
+            const int xr = y + 4;
+            Sp rp, R4, J4;
+            rp.a = csub(F.d1.a, cmul(F.d2.a, beta2));
+            rp.b = csub(F.d1.b, cmul(F.d2.b, beta2));
+            R4.a = csub(rp.a, cmul(alpha, F.ad.a));
+            R4.b = csub(rp.b, cmul(alpha, F.ad.b));
+            J4.a = cadd(cmul(F.d1.a, beta), R4.a);
+            J4.b = cadd(cmul(F.d1.b, beta), R4.b);
+            if (xr >= x0 && xr < xe && own) {
+                const long h = (long)xr * Wh + kw;
+                st_nt(a.dn + h, J4.a);
+                st_nt(a.dn + h + Vh, J4.b);
+                if (XP) {
+                    st_nt(a.x + h, cadd(cadd(F.xv.a, cmul(alpha2, F.d2.a)), cmul(alpha, F.d1.a)));
+                    st_nt(a.x + h + Vh, cadd(cadd(F.xv.b, cmul(alpha2, F.d2.b)), cmul(alpha, F.d1.b)));
+                }
+                aR += cmul(R4.a, cconj(R4.a)).x;
+                aR += cmul(R4.b, cconj(R4.b)).x;
+            }
+            rlds[s_w][0][threadIdx.x] = R4.a;
+            rlds[s_w][1][threadIdx.x] = R4.b;
+            Sp A3 = zs, W2 = zs, B1 = zs;
+            if constexpr ((M & 1) != 0) A3 = todd(DAG1(), y + 3, J3, J2, J4, L3, L2.ex);  // H1: T1(y+3)
+            if constexpr ((M & 2) != 0) {                                                  // H2: W(y+2)
+                W2 = eout(DAG1(), y + 2, A2, A1, A3, L2, L1.ox, J2);
+                if (y + 2 >= x0 && y + 2 < xe && own) {
+                    aW += cmul(W2.a, cconj(W2.a)).x;  // |W|^2 = <d_j, Dhat Dhat^dag d_j>
+                    aW += cmul(W2.b, cconj(W2.b)).x;
+                }
+            }
+            if constexpr ((M & 4) != 0) B1 = todd(DAG0(), y + 1, W1, W0, W2, L1, L0.ex);   // H3: T2(y+1)
+            if constexpr ((M & 8) != 0) {                                                  // H4: Ad_j(y)
+                const Sp o = eout(DAG0(), y, B0, Bm, B1, L0, Lm.ox, W0);
+                if (own) {
+                    const long h = (long)y * Wh + kw;
+                    st_nt(a.anew + h, o.a);
+                    st_nt(a.anew + h + Vh, o.b);
+                    const Sp R0 = Sp{rlds[s_r][0][threadIdx.x], rlds[s_r][1][threadIdx.x]};
+                    aRA = cadd(aRA, cmul(R0.a, cconj(o.a)));  // dot(r, Ad)
+                    aRA = cadd(aRA, cmul(R0.b, cconj(o.b)));
+                    aA += cmul(o.a, cconj(o.a)).x;
+                    aA += cmul(o.b, cconj(o.b)).x;
+                }
+            }
+            Lm = L0;
+            L0 = L1;
+            L1 = L2;
+            L2 = L3;
+            J2 = J3;
+            J3 = J4;
+            A1 = A2;
+            A2 = A3;
+            W0 = W1;
+            W1 = W2;
+            Bm = B0;
+            B0 = B1;
+            s_w = s_w == 4 ? 0 : s_w + 1;
+            s_r = s_r == 4 ? 0 : s_r + 1;
+        };
+        int y = y0;
+        for (int n = 0; n < 2; ++n, ++y) step(y, std::integral_constant<int, 0>());
+        for (int n = 0; n < 2; ++n, ++y) step(y, std::integral_constant<int, 1>());
+        for (int n = 0; n < 2; ++n, ++y) step(y, std::integral_constant<int, 3>());
+        for (int n = 0; n < 2; ++n, ++y) step(y, std::integral_constant<int, 7>());
+        for (; y < xe; ++y) step(y, std::integral_constant<int, 15>());
+    }
+    const double2 s0 = block_sum(make_double2(aW, 0.0), sh);
+    __syncthreads();
+    const double2 s1 = block_sum(aRA, sh);
+    __syncthreads();
+    const double2 s2 = block_sum(make_double2(aR, aA), sh);
+    if (threadIdx.x == 0) {
+        double2 *p = a.partials + 3 * (long)blockIdx.x;
+        p[0] = s0;
+        p[1] = s1;
+        p[2] = s2;
+    }
+}
+
+EoTdCfg eo_td_config(const Geometry &g) {
+    EoTdCfg c;
+    const int Wh = g.Wt / 2;
+    c.NWT = (Wh + EW4 - 1) / EW4;
+    c.TBk = (c.NWT + 3) / 4;
+    // rows per block: 16 from 1024 rows up (tools/tune_eo.py, ms per iteration
+    // incl. host transfers: 4096^2 16 rows 0.90 vs 24 1.01 vs 32 1.03; 1024^2
+    // 16 rows 0.058 vs 8 0.066 vs 12 0.065). The kernel runs one block per CU
+    // (360 registers per lane), so 1024^2 at 16 rows is 192 blocks, one round.
+    if (g.Nx >= 1024) {
+        c.xchunk = 16;
+    } else {
+        int nchunks = (2048 + c.TBk - 1) / c.TBk;
+        if (nchunks > g.Nx) nchunks = g.Nx;
+        if (nchunks < 1) nchunks = 1;
+        c.xchunk = (g.Nx + nchunks - 1) / nchunks;
+        if (c.xchunk < 2) c.xchunk = 2;
+    }
+    if (const char *e = getenv("SM_EOTD_XCHUNK")) c.xchunk = atoi(e);
+    if (c.xchunk < 1) c.xchunk = 1;
+    c.XB = (g.Nx + c.xchunk - 1) / c.xchunk;
+    return c;
+}
+
+int eo_td_blocks(const EoTdCfg &c) { return c.TBk * c.XB; }
+
+void launch_eo_td(hipStream_t s, const Geometry &g, const EoTdCfg &c, const double2 *d1, const double2 *d2,
+                  const double2 *aold, double2 *dn, double2 *anew, double2 *x, const double2 *Ue, const double2 *Uo,
+                  double mass, long pass, CGScalars *sc, double2 *partials) {
+    EoTDArgs a;
+    a.d1 = d1; a.d2 = d2; a.aold = aold; a.dn = dn; a.anew = anew; a.x = x;
+    a.Ue = Ue; a.Uo = Uo; a.sc = sc; a.partials = partials;
+    a.Vh = g.V / 2; a.Nx = g.Nx; a.Wh = g.Wt / 2; a.t0 = g.t0; a.Ntg = g.Ntg;
+    a.xchunk = c.xchunk; a.NWT = c.NWT; a.TBk = c.TBk; a.XB = c.XB;
+    a.first = pass == 0;
+    a.rebuild = pass >= 2;
+    a.mass = mass;
+    const dim3 grid(c.TBk * c.XB), block(256);
+    if (pass >= 2 && (pass & 1) == 0) hipLaunchKernelGGL(eo_td_kernel<1>, grid, block, 0, s, a);
+    else hipLaunchKernelGGL(eo_td_kernel<0>, grid, block, 0, s, a);
+}
+
+}  // namespace sm

@@ -217,6 +217,19 @@ void launch_eo_cg_pass(hipStream_t s, const Geometry &g, const EoFusedCfg &c, in
                        const double2 *Ue, const double2 *Uo, double mass, const EoFaces &f, CGScalars *sc,
                        double2 *partials);
 
+// One-pass even-odd CG iteration on Dhat Dhat^dag (sm_eotd.hip, one shard):
+// the two-direction recurrence, four checkerboard hops in registers; 3
+// partials per block ((|W|^2, 0), <r,Ad>, (|r|^2, |Ad|^2)) for cg1_scalars.
+constexpr int kEoTdWaveCols = 56;
+struct EoTdCfg {
+    int NWT, TBk, xchunk, XB;
+};
+EoTdCfg eo_td_config(const Geometry &g);
+int eo_td_blocks(const EoTdCfg &c);
+void launch_eo_td(hipStream_t s, const Geometry &g, const EoTdCfg &c, const double2 *d1, const double2 *d2,
+                  const double2 *aold, double2 *dn, double2 *anew, double2 *x, const double2 *Ue, const double2 *Uo,
+                  double mass, long pass, CGScalars *sc, double2 *partials);
+
 // Pack the t = 0 and t = Wt-1 columns (both planes) into contiguous faces.
 void launch_pack_faces(hipStream_t s, const Geometry &g, const double2 *field, double2 *lo_face,
                        double2 *hi_face);

@@ -120,23 +120,39 @@ def test_eo_cg_solves_and_converges_faster(sm, name):
     assert res.iterations < 0.6 * meta["cg_iters"], (res.iterations, meta["cg_iters"])
 
 
-@pytest.mark.parametrize("name", ["l64x64_b5_m-0p06", "l32x48_b3_m-0p10", "l16x16_b2_m-0p19"])
-def test_folded_eo_cg_matches_six_kernel_eo_cg(sm, name):
+def _gen_eo_case(sm, Nx, Nt):
+    S = Nx * Nt
+    a = {"U": np.empty(4 * S), "psi": np.empty(4 * S)}
+    sm.lib.sm_fill_gauge(4321, 0.3246, Nt, 0, Nx, 0, Nt, ptr(a["U"][:2 * S]), ptr(a["U"][2 * S:]))
+    sm.lib.sm_fill_spinor(5678, Nt, 0, Nx, 0, Nt, ptr(a["psi"][:2 * S]), ptr(a["psi"][2 * S:]))
+    return {"Nx": Nx, "Nt": Nt, "m0": -0.1}, a
+
+
+@pytest.mark.parametrize("variant", ["SM_EO_CG_FOLDED", "SM_EO_CG_TD"], ids=["folded", "twodir"])
+@pytest.mark.parametrize("name", ["l64x64_b5_m-0p06", "l32x48_b3_m-0p10", "l16x16_b2_m-0p19", "gen:256x120",
+                                  "gen:8x12"])
+def test_folded_eo_cg_matches_six_kernel_eo_cg(sm, name, variant):
     """The folded even-odd CG (2 passes + scalars per iteration, the one-pass
-    recurrence) against the six-launch even-odd CG with the reference's
-    recurrence: same stop rule, iterations +-1 %, solution to 1e-10 (the
-    one-pass beta differs from the reference's by rounding only)."""
-    meta, a = load_fixture(name)
+    recurrence) and the one-pass two-direction kernel (sm_eotd.hip: four
+    checkerboard hops in registers, <d, Ad> as |Dhat^dag d|^2) against the
+    six-launch even-odd CG with the reference's recurrence: same stop rule,
+    iterations +-1 %, solution to 1e-10 (their beta differs from the
+    reference's by rounding only)."""
+    if name.startswith("gen:"):
+        Nx, Nt = (int(v) for v in name[4:].split("x"))
+        meta, a = _gen_eo_case(sm, Nx, Nt)
+    else:
+        meta, a = load_fixture(name)
     Nx, Nt, m0 = meta["Nx"], meta["Nt"], meta["m0"]
     S = Nx * Nt
     phi = even_only(a["psi"], Nx, Nt)
     out = {}
     for folded in ("1", "0"):
-        os.environ["SM_EO_CG_FOLDED"] = folded  # read when the context is created
+        os.environ[variant] = folded  # read when the context is created
         try:
             L = sm.Lattice(Nx, Nt)
         finally:
-            os.environ.pop("SM_EO_CG_FOLDED", None)
+            os.environ.pop(variant, None)
         sm.check(sm.lib.sm_upload_gauge(L.ctx, ptr(a["U"][:2 * S]), ptr(a["U"][2 * S:])))
         x = np.empty(4 * S)
         res = sm.CGResult()

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-iteration time of the even-odd CG (sm_eo_cg, tol 0) for fused-Dhat chunk heights.
 
-    python tools/tune_eo.py [--n 1024] [--xchunk 2,4,8,16] [--iters 200] [--folded 1,0]
+    python tools/tune_eo.py [--n 1024] [--xchunk 2,4,8,16] [--iters 200] [--modes six,folded,twodir]
 
 Host-pointer API: the timing includes the upload of phi and the download of
 x (subtract, or compare variants at equal --iters).
@@ -22,7 +22,8 @@ def main():
     ap.add_argument("--n", type=int, default=1024)
     ap.add_argument("--xchunk", default="0,2,4,8,16")
     ap.add_argument("--iters", type=int, default=200)
-    ap.add_argument("--folded", default="1", help="comma list: 1 folded CG (2 passes), 0 six-launch CG")
+    ap.add_argument("--modes", default="folded",
+                    help="comma list: six (six-launch CG), folded (2 passes), twodir (one pass, sm_eotd.hip)")
     a = ap.parse_args()
     import numpy as np
     import schwingermodel_amd as sm
@@ -32,12 +33,16 @@ def main():
     sm.lib.sm_fill_gauge(4321, 0.3246, N, 0, N, 0, N, U.ctypes.data, U[2 * S:].ctypes.data)
     sm.lib.sm_fill_spinor(91011, N, 0, N, 0, N, phi.ctypes.data, phi[2 * S:].ctypes.data)
     x = np.empty(4 * S)
-    for xc, folded in [(int(v), f) for v in a.xchunk.split(",") for f in a.folded.split(",")]:
+    env = {"six": {}, "folded": {"SM_EO_CG_FOLDED": "1"}, "twodir": {"SM_EO_CG_TD": "1"}}
+    for xc, mode in [(int(v), m) for v in a.xchunk.split(",") for m in a.modes.split(",")]:
+        xkey = "SM_EOTD_XCHUNK" if mode == "twodir" else "SM_EO_XCHUNK"
         if xc > 0:
-            os.environ["SM_EO_XCHUNK"] = str(xc)
-        os.environ["SM_EO_CG_FOLDED"] = folded
-        L = sm.Lattice(N, N)   # (SM_EO_XCHUNK is read per launch: keep it set for the solves)
-        os.environ.pop("SM_EO_CG_FOLDED", None)
+            os.environ[xkey] = str(xc)   # read per solve: kept set for the solves
+        for k, v in env[mode].items():
+            os.environ[k] = v
+        L = sm.Lattice(N, N)
+        for k in env[mode]:
+            os.environ.pop(k, None)
         sm.check(sm.lib.sm_upload_gauge(L.ctx, U.ctypes.data, U[2 * S:].ctypes.data))
         res = sm.CGResult()
         best = None
@@ -48,8 +53,8 @@ def main():
             dt = time.perf_counter() - t
             best = dt if best is None else min(best, dt)
         L.close()
-        os.environ.pop("SM_EO_XCHUNK", None)
-        print(json.dumps({"n": N, "xchunk": xc, "folded": int(folded), "iters": res.iterations,
+        os.environ.pop(xkey, None)
+        print(json.dumps({"n": N, "xchunk": xc, "mode": mode, "iters": res.iterations,
                           "ms_per_it": round(1e3 * best / a.iters, 4)}), flush=True)
 
 
