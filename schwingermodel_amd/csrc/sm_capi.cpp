@@ -474,7 +474,7 @@ int sm_destroy(sm_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
     void *dev[] = {c->U, c->ghostU, c->fields, c->faces, c->faces2, c->faces4, c->partials, c->sums, c->Fbuf, c->sc,
-                   c->counters, c->U_alt, c->Pmd, c->Fmd, c->eo, c->Ucb, c->eo_faces};
+                   c->counters, c->U_alt, c->Pmd, c->Fmd, c->eo, c->Ucb, c->eo_faces, c->eo_faces4};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_sc) (void)hipHostFree(c->h_sc);

@@ -105,6 +105,7 @@ struct sm_ctx {
     double2 *eo = nullptr;          // checkerboard work vectors, V complex each
     double2 *Ucb = nullptr;         // gauge field in checkerboard layout (even, odd)
     double2 *eo_faces = nullptr;    // t-sharded: checkerboard face slots (sm_eo.cpp)
+    double2 *eo_faces4 = nullptr;   // t-sharded: 4-deep checkerboard face slots of the one-pass eo CG
     int eo_fused = 1;               // Dhat as one fused marching pass (0: two hop launches)
     int eo_cg_td = 1;               // even-odd CG: the one-pass two-direction kernel (sm_eotd.hip, one shard;
                                     // 0.54 vs 0.94 ms per iteration at 4096^2 for the six launches)

@@ -43,6 +43,20 @@ static double2 *ucb(sm_ctx *c, int parity) { return c->Ucb + (size_t)parity * c-
 enum { EOF_SEND, EOF_UE, EOF_UO, EOF_V, EOF_W, EOF_R, EOF_A, EOF_N };
 static double2 *eo_face(sm_ctx *c, int slot) { return c->eo_faces + (size_t)slot * 8 * c->g.Nx; }
 
+// 4-deep face slots of the one-pass eo CG (16*Nx complex each): 0 send
+// staging, 1 / 2 even / odd links, 3 / 4 d_{j-1} by pass parity (pass j still
+// holds d_{j-2}'s), 5 Ad_{j-1}.
+enum { EOF4_SEND, EOF4_UE, EOF4_UO, EOF4_D0, EOF4_D1, EOF4_AD, EOF4_N };
+static double2 *eo_face4(sm_ctx *c, int slot) { return c->eo_faces4 + (size_t)slot * 16 * c->g.Nx; }
+static bool eo_td_sharded_ok(const sm_ctx *c) { return c->nshard > 1 && c->g.Wt >= 8; }
+
+static int eo_halo4(sm_ctx *c, const double2 *f, int slot) {
+    double2 *snd = eo_face4(c, EOF4_SEND), *rcv = eo_face4(c, slot);
+    const size_t half = (size_t)8 * c->g.Nx;  // complex per side
+    launch_pack_cb_faces4(c->stream, c->g, f, snd);
+    return exchange_faces_on(c, c->stream, snd, snd + half, rcv, rcv + half, 2 * half);
+}
+
 // Exchange the checkerboard t-faces of f into face slot `slot`; returns the
 // received faces (null on one shard: the kernels wrap periodically).
 static int eo_halo(sm_ctx *c, const double2 *f, int slot, const double2 **out) {
@@ -77,6 +91,8 @@ int eo_ready(sm_ctx *c) {
         HIP_TRY(hipMalloc(&c->eo, sizeof(double2) * (size_t)EO_N * c->g.V));
         HIP_TRY(hipMalloc(&c->Ucb, sizeof(double2) * 2 * (size_t)c->g.V));
         if (c->nshard > 1) HIP_TRY(hipMalloc(&c->eo_faces, sizeof(double2) * (size_t)EOF_N * 8 * c->g.Nx));
+        if (eo_td_sharded_ok(c))
+            HIP_TRY(hipMalloc(&c->eo_faces4, sizeof(double2) * (size_t)EOF4_N * 16 * c->g.Nx));
     }
     // checkerboard copy of the current gauge field (U changes between calls)
     launch_to_cb(c->stream, c->g, c->U, ucb(c, 0), ucb(c, 1));
@@ -84,6 +100,10 @@ int eo_ready(sm_ctx *c) {
     const double2 *f;
     TRY(eo_halo(c, ucb(c, 0), EOF_UE, &f));
     TRY(eo_halo(c, ucb(c, 1), EOF_UO, &f));
+    if (eo_td_sharded_ok(c)) {
+        TRY(eo_halo4(c, ucb(c, 0), EOF4_UE));
+        TRY(eo_halo4(c, ucb(c, 1), EOF4_UO));
+    }
     return SM_OK;
 }
 
@@ -200,8 +220,8 @@ static int eo_cg_folded(sm_ctx *c, const double2 *b, double2 *x, double mass, do
     return SM_OK;
 }
 
-// One-pass two-direction CG on Dhat Dhat^dag (c->eo_cg_td, one shard;
-// sm_eotd.hip): pass j forms r_j, d_j, the even-pass x update and Ad_j =
+// One-pass two-direction CG on Dhat Dhat^dag (c->eo_cg_td; t-shards of width
+// >= 8 exchange 4-deep checkerboard faces of d_{j-1} and Ad_{j-1}; sm_eotd.hip): pass j forms r_j, d_j, the even-pass x update and Ad_j =
 // Dhat Dhat^dag d_j in one launch, then cg1_scalars. d_i rotates through three
 // buffers (d_0 from cg_init in EO_D), Ad_j goes to abuf[j & 1]; after an odd
 // final pass the pending alpha d is added (launch_cg_td_finish_x). ~256 B per
@@ -218,30 +238,55 @@ static int eo_cg_twodir(sm_ctx *c, const double2 *b, double2 *x, double mass, do
     TRY(eo_M(c, x, eo_vec(c, EO_AD), mass, &np));
     double2 *prr = c->partials, *ppp = c->partials + nred;
     launch_cg_init(c->stream, n, b, eo_vec(c, EO_AD), eo_vec(c, EO_R), eo_vec(c, EO_D), prr, ppp);  // r_0, d_0
-    launch_cg_finalize_init(c->stream, nred, prr, ppp, c->sc, tol);
+    if (c->nshard == 1) {
+        launch_cg_finalize_init(c->stream, nred, prr, ppp, c->sc, tol);
+    } else {
+        launch_sum_partials(c->stream, nred, prr, c->sums);
+        launch_sum_partials(c->stream, nred, ppp, c->sums + 1);
+        TRY(allreduce_dev(c, (double *)c->sums, 4));
+        launch_cg_init_from_sums(c->stream, c->sums, c->sc, tol);
+    }
     HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)&c->sc->max_iter, max_iter, 1, c->stream));
     const EoTdCfg cfg = eo_td_config(c->g);
     const int nparts = eo_td_blocks(cfg);
     if (3 * nparts > 2 * kMaxPartials) return fail(SM_ERR_ARG, "even-odd CG grid too large");
     long j = 0;
-    auto pass = [&]() {
+    auto pass = [&]() -> int {
         const bool first = j == 0;
         // pass 0 reads d_0 and takes zero multipliers: its d_{j-2} / Ad_{j-1}
         // operands only need to be finite, so they alias d_0 too
         const double2 *d1 = first ? eo_vec(c, EO_D) : dbuf(j - 1);
         const double2 *d2 = j >= 2 ? dbuf(j - 2) : d1;
         const double2 *aold = first ? d1 : abuf[(j - 1) & 1];
+        EoTdFaces f;
+        if (c->nshard > 1) {  // faces of d_{j-1} (d_{j-2}'s are the previous pass's) and Ad_{j-1}
+            const int sd = (j & 1) ? EOF4_D1 : EOF4_D0, sp = (j & 1) ? EOF4_D0 : EOF4_D1;
+            TRY(eo_halo4(c, d1, sd));
+            f.d1 = eo_face4(c, sd);
+            f.d2 = j >= 2 ? eo_face4(c, sp) : f.d1;
+            if (!first) TRY(eo_halo4(c, aold, EOF4_AD));
+            f.ad = first ? f.d1 : eo_face4(c, EOF4_AD);
+            f.ue = eo_face4(c, EOF4_UE);
+            f.uo = eo_face4(c, EOF4_UO);
+        }
         launch_eo_td(c->stream, c->g, cfg, d1, d2, aold, dbuf(j), abuf[j & 1], x, ucb(c, 0), ucb(c, 1), mass, j,
-                     c->sc, c->partials);
-        launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
+                     c->sc, c->partials, f);
+        if (c->nshard == 1) {
+            launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
+        } else {
+            launch_cg1_local_sum(c->stream, nparts, c->partials, c->sc);
+            TRY(allreduce_dev(c, (double *)c->sc->sum3, 6));
+            launch_cg1_from_sums(c->stream, c->sc, first);
+        }
         ++j;
+        return SM_OK;
     };
     const long passes = (long)max_iter + 1;
     CgChunker plan;
     int chunk = plan.chunk;
     while (j < passes) {
         const long nb = (passes - j) < chunk ? (passes - j) : chunk;
-        for (long i = 0; i < nb; ++i) pass();
+        for (long i = 0; i < nb; ++i) TRY(pass());
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(c->h_sc, c->sc, sizeof(CGScalars), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
@@ -262,7 +307,7 @@ static int eo_cg_twodir(sm_ctx *c, const double2 *b, double2 *x, double mass, do
 // CG on Dhat Dhat^dag x = b (x0 = b, the reference's convention), the
 // reference's recurrence and stop test on half-lattice vectors.
 int eo_cg(sm_ctx *c, const double2 *b, double2 *x, double mass, double tol, int max_iter, sm_cg_result *res) {
-    if (c->eo_cg_td && c->nshard == 1) return eo_cg_twodir(c, b, x, mass, tol, max_iter, res);
+    if (c->eo_cg_td && (c->nshard == 1 || eo_td_sharded_ok(c))) return eo_cg_twodir(c, b, x, mass, tol, max_iter, res);
     if (c->eo_cg_folded && c->eo_fused) return eo_cg_folded(c, b, x, mass, tol, max_iter, res);
     const long n = c->g.V;  // complex entries of an even vector
     const int nparts = reduce_blocks(n);

@@ -21,7 +21,9 @@
 //     H3  row y+1: T2 = D_oe-hop of W              (odd)
 //     H4  row y  : Ad_j = Dhat W                   (even; dots with r_j(y))
 // The hops use the folded bracket (dirac_bracket_folded): the same values as
-// the reference arithmetic up to the sign of an exact zero. One shard only.
+// the reference arithmetic up to the sign of an exact zero. t-shards (SH = 1):
+// halo lanes outside the shard read 4-deep checkerboard faces
+// ([side][plane][col][x]: side 0 = my k = col-4, side 1 = my k = Wh+col).
 // Registers: 256 VGPRs + ~105 AGPRs, so one wave per SIMD; measured 0.54 ms
 // per iteration at 4096^2 against 0.94 ms for the six launches.
 #include <type_traits>
@@ -40,6 +42,7 @@ struct EoTDArgs {
     const double2 *d1, *d2, *aold;  // d_{j-1}, d_{j-2}, Ad_{j-1}
     double2 *dn, *anew, *x;
     const double2 *Ue, *Uo;         // checkerboard links: plane 0 U_t, plane 1 U_x
+    const double2 *f1, *f2, *fa, *fue, *fuo;  // SH: 4-deep faces of d1, d2, aold, Ue, Uo
     CGScalars *sc;
     double2 *partials;              // 3 per block: (|W|^2, 0), <r,Ad>, (|r|^2, |Ad|^2)
     long Vh;
@@ -48,7 +51,7 @@ struct EoTDArgs {
     double mass;
 };
 
-template <int XP>
+template <int XP, int SH>
 __global__ void __launch_bounds__(256) eo_td_kernel(EoTDArgs a) {
     __shared__ double2 sh[4];
     __shared__ double2 rlds[5][2][256];  // r_j of rows y .. y+4
@@ -71,9 +74,14 @@ __global__ void __launch_bounds__(256) eo_td_kernel(EoTDArgs a) {
         int kw = k % Wh;
         if (kw < 0) kw += Wh;
         const bool own = lane >= EH4 && lane < EW4 + EH4 && k < Wh;
+        const bool inside = k >= 0 && k < Wh;
+        const int side = k < 0 ? 0 : 1;
+        const int fcol = min(max(k < 0 ? k + EH4 : k - Wh, 0), EH4 - 1);
         const double m = a.mass, hm = 0.5 / a.mass;
         auto wrapx = [Nx](int x) { int w = x % Nx; return w < 0 ? w + Nx : w; };
         auto hidx = [&](int y) { return (long)wrapx(y) * Wh + kw; };
+        // face entry (plane 0) of row y for this lane; plane 1 is 4*Nx further
+        auto fidx = [&](int y) { return (long)((side * 2) * EH4 + fcol) * Nx + wrapx(y); };
         auto signs = [&](int t, double &sr0, double &sl0) {
             int tg = (a.t0 + t) % a.Ntg;
             if (tg < 0) tg += a.Ntg;
@@ -84,20 +92,37 @@ __global__ void __launch_bounds__(256) eo_td_kernel(EoTDArgs a) {
             double2 et, ex, ot, ox;  // even / odd links at (y, k)
         };
         auto ldl = [&](int y, Lk &L) {
-            const long h = hidx(min(max(y, x0 - 4), xe + 2));
-            L.et = a.Ue[h];
-            L.ex = a.Ue[h + Vh];
-            L.ot = a.Uo[h];
-            L.ox = a.Uo[h + Vh];
+            const int yc = min(max(y, x0 - 4), xe + 2);
+            if (!SH || inside) {
+                const long h = hidx(yc);
+                L.et = a.Ue[h];
+                L.ex = a.Ue[h + Vh];
+                L.ot = a.Uo[h];
+                L.ox = a.Uo[h + Vh];
+            } else {
+                const long f = fidx(yc), p1 = (long)EH4 * Nx;
+                L.et = a.fue[f];
+                L.ex = a.fue[f + p1];
+                L.ot = a.fuo[f];
+                L.ox = a.fuo[f + p1];
+            }
         };
         struct Fr {
             Sp d1, d2, ad, xv;
         };
         auto ldf = [&](int y, Fr &F) {
-            const long h = hidx(min(max(y, x0 - 4), xe + 3));
-            F.d1 = Sp{a.d1[h], a.d1[h + Vh]};
-            F.d2 = Sp{a.d2[h], a.d2[h + Vh]};
-            F.ad = Sp{a.aold[h], a.aold[h + Vh]};
+            const int yc = min(max(y, x0 - 4), xe + 3);
+            if (!SH || inside) {
+                const long h = hidx(yc);
+                F.d1 = Sp{a.d1[h], a.d1[h + Vh]};
+                F.d2 = Sp{a.d2[h], a.d2[h + Vh]};
+                F.ad = Sp{a.aold[h], a.aold[h + Vh]};
+            } else {
+                const long f = fidx(yc), p1 = (long)EH4 * Nx;
+                F.d1 = Sp{a.f1[f], a.f1[f + p1]};
+                F.d2 = Sp{a.f2[f], a.f2[f + p1]};
+                F.ad = Sp{a.fa[f], a.fa[f + p1]};
+            }
             if (XP) {
                 const long hx = hidx(min(max(y, x0), xe - 1));
                 F.xv = Sp{a.x[hx], a.x[hx + Vh]};
@@ -264,18 +289,42 @@ int eo_td_blocks(const EoTdCfg &c) { return c.TBk * c.XB; }
 
 void launch_eo_td(hipStream_t s, const Geometry &g, const EoTdCfg &c, const double2 *d1, const double2 *d2,
                   const double2 *aold, double2 *dn, double2 *anew, double2 *x, const double2 *Ue, const double2 *Uo,
-                  double mass, long pass, CGScalars *sc, double2 *partials) {
+                  double mass, long pass, CGScalars *sc, double2 *partials, const EoTdFaces &f) {
     EoTDArgs a;
     a.d1 = d1; a.d2 = d2; a.aold = aold; a.dn = dn; a.anew = anew; a.x = x;
     a.Ue = Ue; a.Uo = Uo; a.sc = sc; a.partials = partials;
+    a.f1 = f.d1; a.f2 = f.d2; a.fa = f.ad; a.fue = f.ue; a.fuo = f.uo;
     a.Vh = g.V / 2; a.Nx = g.Nx; a.Wh = g.Wt / 2; a.t0 = g.t0; a.Ntg = g.Ntg;
     a.xchunk = c.xchunk; a.NWT = c.NWT; a.TBk = c.TBk; a.XB = c.XB;
     a.first = pass == 0;
     a.rebuild = pass >= 2;
     a.mass = mass;
     const dim3 grid(c.TBk * c.XB), block(256);
-    if (pass >= 2 && (pass & 1) == 0) hipLaunchKernelGGL(eo_td_kernel<1>, grid, block, 0, s, a);
-    else hipLaunchKernelGGL(eo_td_kernel<0>, grid, block, 0, s, a);
+    const bool xp = pass >= 2 && (pass & 1) == 0;
+    if (f.d1) {
+        if (xp) hipLaunchKernelGGL((eo_td_kernel<1, 1>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((eo_td_kernel<0, 1>), grid, block, 0, s, a);
+    } else {
+        if (xp) hipLaunchKernelGGL((eo_td_kernel<1, 0>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((eo_td_kernel<0, 0>), grid, block, 0, s, a);
+    }
+}
+
+// 4-deep checkerboard t-faces [side][plane][col][x]: side 0 = columns k = 0..3
+// (sent down), side 1 = k = Wh-4..Wh-1 (sent up); 16*Nx complex.
+__global__ void __launch_bounds__(256) pack_cb_faces4_kernel(int Nx, int Wh, long Vh, const double2 *f, double2 *out) {
+    const int n = 16 * Nx;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int x = i % Nx, r = i / Nx;
+        const int col = r & 3, plane = (r >> 2) & 1, side = r >> 3;
+        const int k = side ? Wh - 4 + col : col;
+        out[i] = f[plane * Vh + (long)x * Wh + k];
+    }
+}
+
+void launch_pack_cb_faces4(hipStream_t s, const Geometry &g, const double2 *f, double2 *out) {
+    hipLaunchKernelGGL(pack_cb_faces4_kernel, dim3((16 * g.Nx + 255) / 256), dim3(256), 0, s, g.Nx, g.Wt / 2,
+                       g.V / 2, f, out);
 }
 
 }  // namespace sm

@@ -226,9 +226,15 @@ struct EoTdCfg {
 };
 EoTdCfg eo_td_config(const Geometry &g);
 int eo_td_blocks(const EoTdCfg &c);
+// t-shards: 4-deep checkerboard faces ([side][plane][col][x], 16*Nx complex)
+// of d_{j-1}, d_{j-2}, Ad_{j-1} and both link parities; all null on one shard.
+struct EoTdFaces {
+    const double2 *d1 = nullptr, *d2 = nullptr, *ad = nullptr, *ue = nullptr, *uo = nullptr;
+};
 void launch_eo_td(hipStream_t s, const Geometry &g, const EoTdCfg &c, const double2 *d1, const double2 *d2,
                   const double2 *aold, double2 *dn, double2 *anew, double2 *x, const double2 *Ue, const double2 *Uo,
-                  double mass, long pass, CGScalars *sc, double2 *partials);
+                  double mass, long pass, CGScalars *sc, double2 *partials, const EoTdFaces &f);
+void launch_pack_cb_faces4(hipStream_t s, const Geometry &g, const double2 *f, double2 *out);
 
 // Pack the t = 0 and t = Wt-1 columns (both planes) into contiguous faces.
 void launch_pack_faces(hipStream_t s, const Geometry &g, const double2 *field, double2 *lo_face,

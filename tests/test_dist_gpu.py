@@ -86,18 +86,22 @@ def test_sharded_md_matches_reference(tmp_path, fixture, world):
     assert t["U_rel"] <= 1e-8
 
 
-@pytest.mark.parametrize("fixture,world,fused,folded", [
-    ("gen:32x48:0.4242:0.0", 2, "1", "0"), ("gen:32x48:0.3:-0.1", 4, "1", "0"),
-    ("gen:32x48:0.3:-0.1", 4, "0", "0"),         # the two-launch Dhat (eo_hop with faces)
-    ("gen:32x48:0.3:-0.1", 4, "1", "1"),         # the folded eo CG (faces of d, r, Ad, W)
+@pytest.mark.parametrize("fixture,world,fused,folded,td", [
+    ("gen:32x48:0.4242:0.0", 2, "1", "0", "1"),   # the one-pass eo CG (4-deep faces of d, Ad)
+    ("gen:32x48:0.3:-0.1", 4, "1", "0", "1"),
+    ("gen:32x48:0.3:-0.1", 8, "1", "0", "1"),     # Wt = 6 < 8: falls back to the six-launch iteration
+    ("gen:32x48:0.3:-0.1", 4, "1", "0", "0"),     # the six-launch iteration
+    ("gen:32x48:0.3:-0.1", 4, "0", "0", "0"),     # the two-launch Dhat (eo_hop with faces)
+    ("gen:32x48:0.3:-0.1", 4, "1", "1", "0"),     # the folded eo CG (faces of d, r, Ad, W)
     # Wh = 128: three waves per strip, interior waves without halo lanes
-    ("gen:24x512:0.3246:-0.05", 2, "1", "0"), ("gen:24x512:0.3246:-0.05", 2, "1", "1")])
-def test_sharded_even_odd_matches_one_shard(tmp_path, fixture, world, fused, folded):
+    ("gen:24x512:0.3246:-0.05", 2, "1", "0", "1"), ("gen:24x512:0.3246:-0.05", 2, "1", "1", "0")])
+def test_sharded_even_odd_matches_one_shard(tmp_path, fixture, world, fused, folded, td):
     """Even-odd layer on t-shards (checkerboard faces over the host transport)
     vs one shard: Dhat / Dhat^dag bitwise (same per-element arithmetic), the
     half-lattice CG to 1e-10 in the same iteration count (+-1 %), the MD force
     to 1e-10, and an HMC trajectory with the same accept decision."""
-    rep = run_world("eo", fixture, world, tmp_path, timeout=600, extra_env={"SM_EO_FUSED": fused, "SM_EO_CG_FOLDED": folded})
+    rep = run_world("eo", fixture, world, tmp_path, timeout=600,
+                    extra_env={"SM_EO_FUSED": fused, "SM_EO_CG_FOLDED": folded, "SM_EO_CG_TD": td})
     c = rep["checks"]
     assert c["dhat"] is True and c["dhatdag"] is True, c
     # the sharded dots sum per-shard partials: a different rounding order
