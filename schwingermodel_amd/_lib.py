@@ -7,7 +7,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsm_hip.so")
+LIB_PATH = os.environ.get("SM_LIB_PATH") or os.path.join(HERE, "libsm_hip.so")  # override: A/B runs only
 HEADER = os.path.join(os.path.dirname(HERE), "include", "sm_hip.h")
 
 

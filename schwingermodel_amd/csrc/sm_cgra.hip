@@ -94,18 +94,49 @@ __device__ __forceinline__ RSrc rsrc(const double2 *base, const double2 *face, i
 
 // D (DAG = 0) / D^dag (DAG = 1) at this lane's column: centre p, x-neighbours
 // pxm / pxp, t-neighbours from the adjacent lanes.
+//
+// FOLD: dirac_bracket_folded's terms with the t-hops moved to the sending
+// lane, so each hop crosses lanes as ONE complex (4 DPP moves instead of 10):
+// the forward hop needs only the spin combination at t+1 (D: pt0 - pt1,
+// D^dag: pt0 + pt1), formed by its owner and shifted; the backward hop's whole
+// product conj(U_t(t-1)) * combo(t-1) is formed by lane t-1 with its own link
+// and shifted, and the antiperiodic sign applied after the shift. Negation
+// commutes exactly with the rounded products and sums, so C = sl0 * that
+// product equals the folded form's (U*sl0)^* combo up to the sign of an exact
+// zero: the values are dirac_site_folded's.
 template <int FOLD, int DAG>
 __device__ __forceinline__ Sp ra_site(double mass, double sr0, double sl0, const Sp &p, const Sp &pxm, const Sp &pxp,
                                       double2 ut, double2 ux, double2 uxm) {
-    const Sp pm = shr(p), pp = shl(p);
-    const double2 utm = dpp_shr1(ut);
     Sp o;
-    if (FOLD)
-        dirac_site_folded<DAG>(mass, sr0, sl0, p.a, p.b, pp.a, pp.b, pxp.a, pxp.b, pm.a, pm.b, pxm.a, pxm.b, ut, ux,
-                               utm, uxm, o.a, o.b);
-    else
+    if (FOLD) {
+        const double2 qf = DAG ? cadd(p.a, p.b) : csub(p.a, p.b);  // forward-hop combination at this site
+        const double2 qb = DAG ? csub(p.a, p.b) : cadd(p.a, p.b);  // backward-hop combination at this site
+        const double2 Cb = cmul(make_double2(ut.x, -ut.y), qb);    // conj(U_t) * qb, for lane t+1
+        const double2 qt = dpp_shl1(qf);
+        const double2 Cs = dpp_shr1(Cb);
+        const double2 A = cmul(make_double2(ut.x * sr0, ut.y * sr0), qt);
+        const double2 C = make_double2(Cs.x * sl0, Cs.y * sl0);
+        const double2 e = make_double2(uxm.x, -uxm.y);
+        double2 h0, h1;
+        if (!DAG) {
+            const double2 B = cmul(ux, make_double2(pxp.a.x - pxp.b.y, pxp.a.y + pxp.b.x));  // px0 + i px1
+            const double2 E = cmul(e, make_double2(pxm.a.x + pxm.b.y, pxm.a.y - pxm.b.x));   // pxm0 - i pxm1
+            h0 = cadd(cadd(cadd(A, B), C), E);
+            h1 = cadd(cadd(cadd(cneg(A), mul_mi(B)), C), mul_i(E));
+        } else {
+            const double2 E = cmul(e, make_double2(pxm.a.x - pxm.b.y, pxm.a.y + pxm.b.x));   // pxm0 + i pxm1
+            const double2 B = cmul(ux, make_double2(pxp.a.x + pxp.b.y, pxp.a.y - pxp.b.x));  // px0 - i px1
+            h0 = cadd(cadd(cadd(C, E), A), B);
+            h1 = cadd(cadd(cadd(cneg(C), mul_mi(E)), A), mul_i(B));
+        }
+        o.a = csub(rmul(mass, p.a), rmul(0.5, h0));
+        o.b = csub(rmul(mass, p.b), rmul(0.5, h1));
+    } else {
+        const Sp pm = shr(p), pp = shl(p);
+        const double2 utm = dpp_shr1(ut);
         dirac_site<DAG>(mass, sr0, sl0, p.a, p.b, pp.a, pp.b, pxp.a, pxp.b, pm.a, pm.b, pxm.a, pxm.b, ut, ux, utm,
                         uxm, o.a, o.b);
+    }
     return o;
 }
 

@@ -164,13 +164,13 @@ __device__ __forceinline__ double2 block_sum(double2 v, double2 *sh) {
 // Wave-wide lane shifts by one (DPP wave_shr:1 / wave_shl:1, GFX9-family
 // incl. gfx950): no LDS, no barrier. Lane 0 (shr) / lane 63 (shl) receive 0.
 __device__ __forceinline__ double dpp_shr1(double v) {  // lane l <- lane l-1
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xf, 0xf, false);
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xf, 0xf, true);
     return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double dpp_shl1(double v) {  // lane l <- lane l+1
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xf, 0xf, false);
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xf, 0xf, true);
     return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double2 dpp_shr1(double2 v) { return make_double2(dpp_shr1(v.x), dpp_shr1(v.y)); }
