@@ -51,6 +51,44 @@ struct EoTDArgs {
     double mass;
 };
 
+// One checkerboard hop's bracket (dirac_bracket_folded's terms) at a lane whose
+// forward t-neighbour is lane+1 and backward one this lane (FWD = true), or
+// forward this lane and backward lane-1 (FWD = false). The shifted hop crosses
+// lanes as ONE complex: the forward spin combination, or the whole backward
+// product conj(U_t) * combination formed by the sending lane with its own link
+// (Ub) and signed after the shift. Negation commutes exactly with the rounded
+// products and sums, so every value equals dirac_bracket_folded's up to the
+// sign of an exact zero. v: centre (t-neighbour source), vxp / vxm: x+-1.
+template <int DG, bool FWD>
+__device__ __forceinline__ void eo_bracket(double sr0, double sl0, const Sp &v, const Sp &vxp, const Sp &vxm,
+                                           double2 Ut, double2 Ux, double2 Ub, double2 Uxm, double2 &h0,
+                                           double2 &h1) {
+    const double2 qf = DG ? cadd(v.a, v.b) : csub(v.a, v.b);  // forward-hop combination
+    const double2 qb = DG ? csub(v.a, v.b) : cadd(v.a, v.b);  // backward-hop combination
+    const double2 a = make_double2(Ut.x * sr0, Ut.y * sr0);
+    double2 A, C;
+    if (FWD) {
+        A = cmul(a, dpp_shl1(qf));
+        C = cmul(make_double2(Ub.x * sl0, -(Ub.y * sl0)), qb);
+    } else {
+        A = cmul(a, qf);
+        const double2 Cs = dpp_shr1(cmul(make_double2(Ub.x, -Ub.y), qb));
+        C = make_double2(Cs.x * sl0, Cs.y * sl0);
+    }
+    const double2 e = make_double2(Uxm.x, -Uxm.y);
+    if (!DG) {
+        const double2 B = cmul(Ux, make_double2(vxp.a.x - vxp.b.y, vxp.a.y + vxp.b.x));  // px0 + i px1
+        const double2 E = cmul(e, make_double2(vxm.a.x + vxm.b.y, vxm.a.y - vxm.b.x));   // pxm0 - i pxm1
+        h0 = cadd(cadd(cadd(A, B), C), E);
+        h1 = cadd(cadd(cadd(cneg(A), mul_mi(B)), C), mul_i(E));
+    } else {
+        const double2 E = cmul(e, make_double2(vxm.a.x - vxm.b.y, vxm.a.y + vxm.b.x));   // pxm0 + i pxm1
+        const double2 B = cmul(Ux, make_double2(vxp.a.x + vxp.b.y, vxp.a.y - vxp.b.x));  // px0 - i px1
+        h0 = cadd(cadd(cadd(C, E), A), B);
+        h1 = cadd(cadd(cadd(cneg(C), mul_mi(E)), A), mul_i(B));
+    }
+}
+
 template <int XP, int SH>
 __global__ void __launch_bounds__(256) eo_td_kernel(EoTDArgs a) {
     __shared__ double2 sh[4];
@@ -128,31 +166,27 @@ __global__ void __launch_bounds__(256) eo_td_kernel(EoTDArgs a) {
                 F.xv = Sp{a.x[hx], a.x[hx + Vh]};
             }
         };
-        // odd hop at odd site (y, k) from an even field: T = -0.5 H_oe v
-        auto todd = [&](auto dag, int y, const Sp &vc, const Sp &vxm, const Sp &vxp, const Lk &L, double2 ex_m) {
+        // odd hop at odd site (y, k) from an even field: T = -0.5 H_oe v. YE: row
+        // y even (the backward t-neighbour is this lane, the forward one lane+1).
+        auto todd = [&](auto dag, auto ye, const Sp &vc, const Sp &vxm, const Sp &vxp, const Lk &L, double2 ex_m) {
             constexpr int DG = decltype(dag)::value;
-            const bool ye = (y & 1) == 0;
-            const Sp pm = ye ? vc : shr(vc), pp = ye ? shl(vc) : vc;
-            const double2 utm = ye ? L.et : dpp_shr1(L.et);
+            constexpr bool YE = decltype(ye)::value;
             double sr0, sl0;
-            signs(2 * k + (ye ? 1 : 0), sr0, sl0);
+            signs(2 * k + (YE ? 1 : 0), sr0, sl0);
             double2 h0, h1;
-            dirac_bracket_folded<DG>(sr0, sl0, pp.a, pp.b, vxp.a, vxp.b, pm.a, pm.b, vxm.a, vxm.b, L.ot, L.ox, utm,
-                                     ex_m, h0, h1);
+            eo_bracket<DG, YE>(sr0, sl0, vc, vxp, vxm, L.ot, L.ox, L.et, ex_m, h0, h1);
             return Sp{rmul(-0.5, h0), rmul(-0.5, h1)};
         };
-        // even hop at even site (x, k) from an odd field: m v + (0.5/m) H_eo T
-        auto eout = [&](auto dag, int x, const Sp &Tc, const Sp &Txm, const Sp &Txp, const Lk &L, double2 ox_m,
+        // even hop at even site (x, k) from an odd field: m v + (0.5/m) H_eo T.
+        // XEV: row x even (the backward t-neighbour is lane-1, the forward one this lane).
+        auto eout = [&](auto dag, auto xev, const Sp &Tc, const Sp &Txm, const Sp &Txp, const Lk &L, double2 ox_m,
                         const Sp &vc) {
             constexpr int DG = decltype(dag)::value;
-            const bool xev = (x & 1) == 0;
-            const Sp pm = xev ? shr(Tc) : Tc, pp = xev ? Tc : shl(Tc);
-            const double2 utm = xev ? dpp_shr1(L.ot) : L.ot;
+            constexpr bool XEV = decltype(xev)::value;
             double sr0, sl0;
-            signs(2 * k + (xev ? 0 : 1), sr0, sl0);
+            signs(2 * k + (XEV ? 0 : 1), sr0, sl0);
             double2 h0, h1;
-            dirac_bracket_folded<DG>(sr0, sl0, pp.a, pp.b, Txp.a, Txp.b, pm.a, pm.b, Txm.a, Txm.b, L.et, L.ex, utm,
-                                     ox_m, h0, h1);
+            eo_bracket<DG, !XEV>(sr0, sl0, Tc, Txp, Txm, L.et, L.ex, L.ot, ox_m, h0, h1);
             return Sp{cadd(rmul(m, vc.a), rmul(hm, h0)), cadd(rmul(m, vc.b), rmul(hm, h1))};
         };
         using DAG1 = std::integral_constant<int, 1>;
@@ -174,8 +208,12 @@ __global__ void __launch_bounds__(256) eo_td_kernel(EoTDArgs a) {
         ldl(y0 + 3, Lin);
         int s_w = 4, s_r = 0;              // r_j ring slots of rows y+4 (written) and y (read)
         // stage mask M: bit 0 H1, bit 1 H2, bit 2 H3, bit 3 H4 (F always)
-        auto step = [&](int y, auto mtag) {
+        // P: parity of row y (x0 is even: Nx and xchunk are)
+        auto step = [&](int y, auto mtag, auto ptag) {
             constexpr int M = decltype(mtag)::value;
+            constexpr bool E0 = decltype(ptag)::value == 0;  // rows y, y+2, y+4 even
+            using PE = std::integral_constant<bool, E0>;
+            using PO = std::integral_constant<bool, !E0>;
             const Fr F = Fin;
             const Lk L3 = Lin;
             ldf(y + 5, Fin);
@@ -204,17 +242,17 @@ __global__ void __launch_bounds__(256) eo_td_kernel(EoTDArgs a) {
             rlds[s_w][0][threadIdx.x] = R4.a;
             rlds[s_w][1][threadIdx.x] = R4.b;
             Sp A3 = zs, W2 = zs, B1 = zs;
-            if constexpr ((M & 1) != 0) A3 = todd(DAG1(), y + 3, J3, J2, J4, L3, L2.ex);  // H1: T1(y+3)
+            if constexpr ((M & 1) != 0) A3 = todd(DAG1(), PO(), J3, J2, J4, L3, L2.ex);  // H1: T1(y+3)
             if constexpr ((M & 2) != 0) {                                                  // H2: W(y+2)
-                W2 = eout(DAG1(), y + 2, A2, A1, A3, L2, L1.ox, J2);
+                W2 = eout(DAG1(), PE(), A2, A1, A3, L2, L1.ox, J2);
                 if (y + 2 >= x0 && y + 2 < xe && own) {
                     aW += cmul(W2.a, cconj(W2.a)).x;  // |W|^2 = <d_j, Dhat Dhat^dag d_j>
                     aW += cmul(W2.b, cconj(W2.b)).x;
                 }
             }
-            if constexpr ((M & 4) != 0) B1 = todd(DAG0(), y + 1, W1, W0, W2, L1, L0.ex);   // H3: T2(y+1)
+            if constexpr ((M & 4) != 0) B1 = todd(DAG0(), PO(), W1, W0, W2, L1, L0.ex);   // H3: T2(y+1)
             if constexpr ((M & 8) != 0) {                                                  // H4: Ad_j(y)
-                const Sp o = eout(DAG0(), y, B0, Bm, B1, L0, Lm.ox, W0);
+                const Sp o = eout(DAG0(), PE(), B0, Bm, B1, L0, Lm.ox, W0);
                 if (own) {
                     const long h = (long)y * Wh + kw;
                     st_nt(a.anew + h, o.a);
@@ -241,12 +279,21 @@ __global__ void __launch_bounds__(256) eo_td_kernel(EoTDArgs a) {
             s_w = s_w == 4 ? 0 : s_w + 1;
             s_r = s_r == 4 ? 0 : s_r + 1;
         };
-        int y = y0;
-        for (int n = 0; n < 2; ++n, ++y) step(y, std::integral_constant<int, 0>());
-        for (int n = 0; n < 2; ++n, ++y) step(y, std::integral_constant<int, 1>());
-        for (int n = 0; n < 2; ++n, ++y) step(y, std::integral_constant<int, 3>());
-        for (int n = 0; n < 2; ++n, ++y) step(y, std::integral_constant<int, 7>());
-        for (; y < xe; ++y) step(y, std::integral_constant<int, 15>());
+        using Ev = std::integral_constant<int, 0>;
+        using Od = std::integral_constant<int, 1>;
+        int y = y0;  // even; every chunk has an even number of rows
+        step(y, std::integral_constant<int, 0>(), Ev());
+        step(y + 1, std::integral_constant<int, 0>(), Od());
+        step(y + 2, std::integral_constant<int, 1>(), Ev());
+        step(y + 3, std::integral_constant<int, 1>(), Od());
+        step(y + 4, std::integral_constant<int, 3>(), Ev());
+        step(y + 5, std::integral_constant<int, 3>(), Od());
+        step(y + 6, std::integral_constant<int, 7>(), Ev());
+        step(y + 7, std::integral_constant<int, 7>(), Od());
+        for (y += 8; y < xe; y += 2) {
+            step(y, std::integral_constant<int, 15>(), Ev());
+            step(y + 1, std::integral_constant<int, 15>(), Od());
+        }
     }
     const double2 s0 = block_sum(make_double2(aW, 0.0), sh);
     __syncthreads();
@@ -280,7 +327,8 @@ EoTdCfg eo_td_config(const Geometry &g) {
         if (c.xchunk < 2) c.xchunk = 2;
     }
     if (const char *e = getenv("SM_EOTD_XCHUNK")) c.xchunk = atoi(e);
-    if (c.xchunk < 1) c.xchunk = 1;
+    if (c.xchunk < 2) c.xchunk = 2;
+    c.xchunk += c.xchunk & 1;  // even: the kernel's row parities are static
     c.XB = (g.Nx + c.xchunk - 1) / c.xchunk;
     return c;
 }
