@@ -34,6 +34,10 @@
 // FOLD = 1 evaluates the hopping bracket with its products by 0, +-1 and +-i
 // folded into sign flips and swaps (dirac_bracket_folded): the same values up
 // to the sign of an exact zero, at 84 instead of ~126 fp64 operations a site.
+// FOLD = 2 (the default) also forms the complex products, the CG updates and
+// the dots with fused multiply-adds: one rounding where GCC's expansion has
+// two or three, so the iterates differ from FOLD = 1 at rounding level (the
+// parity bar for CG is the converged solution, 1e-12).
 #include <type_traits>
 
 #include "sm_device.h"
@@ -92,6 +96,33 @@ __device__ __forceinline__ RSrc rsrc(const double2 *base, const double2 *face, i
     return s;
 }
 
+// Complex products for the FOLD = 2 build: fused multiply-adds (one rounding
+// per component instead of three); FOLD <= 1 keeps GCC's separately rounded
+// expansion. cm = a b, cfma = c + a b, cfms = c - a b.
+template <int FOLD>
+__device__ __forceinline__ double2 cm(double2 a, double2 b) {
+    if (FOLD < 2) return cmul(a, b);
+    return make_double2(__builtin_fma(a.x, b.x, -(a.y * b.y)), __builtin_fma(a.x, b.y, a.y * b.x));
+}
+template <int FOLD>
+__device__ __forceinline__ double2 cfma(double2 c, double2 a, double2 b) {
+    if (FOLD < 2) return cadd(c, cmul(a, b));
+    return make_double2(__builtin_fma(a.x, b.x, __builtin_fma(-a.y, b.y, c.x)),
+                        __builtin_fma(a.x, b.y, __builtin_fma(a.y, b.x, c.y)));
+}
+template <int FOLD>
+__device__ __forceinline__ double2 cfms(double2 c, double2 a, double2 b) {
+    if (FOLD < 2) return csub(c, cmul(a, b));
+    return make_double2(__builtin_fma(-a.x, b.x, __builtin_fma(a.y, b.y, c.x)),
+                        __builtin_fma(-a.x, b.y, __builtin_fma(-a.y, b.x, c.y)));
+}
+// |z|^2 accumulated: acc + Re(z conj z)
+template <int FOLD>
+__device__ __forceinline__ double nacc(double acc, double2 z) {
+    if (FOLD < 2) return acc + cmul(z, cconj(z)).x;
+    return __builtin_fma(z.x, z.x, __builtin_fma(z.y, z.y, acc));
+}
+
 // D (DAG = 0) / D^dag (DAG = 1) at this lane's column: centre p, x-neighbours
 // pxm / pxp, t-neighbours from the adjacent lanes.
 //
@@ -111,26 +142,28 @@ __device__ __forceinline__ Sp ra_site(double mass, double sr0, double sl0, const
     if (FOLD) {
         const double2 qf = DAG ? cadd(p.a, p.b) : csub(p.a, p.b);  // forward-hop combination at this site
         const double2 qb = DAG ? csub(p.a, p.b) : cadd(p.a, p.b);  // backward-hop combination at this site
-        const double2 Cb = cmul(make_double2(ut.x, -ut.y), qb);    // conj(U_t) * qb, for lane t+1
+        const double2 Cb = cm<FOLD>(make_double2(ut.x, -ut.y), qb);  // conj(U_t) * qb, for lane t+1
         const double2 qt = dpp_shl1(qf);
         const double2 Cs = dpp_shr1(Cb);
-        const double2 A = cmul(make_double2(ut.x * sr0, ut.y * sr0), qt);
+        const double2 A = cm<FOLD>(make_double2(ut.x * sr0, ut.y * sr0), qt);
         const double2 C = make_double2(Cs.x * sl0, Cs.y * sl0);
         const double2 e = make_double2(uxm.x, -uxm.y);
         double2 h0, h1;
         if (!DAG) {
-            const double2 B = cmul(ux, make_double2(pxp.a.x - pxp.b.y, pxp.a.y + pxp.b.x));  // px0 + i px1
-            const double2 E = cmul(e, make_double2(pxm.a.x + pxm.b.y, pxm.a.y - pxm.b.x));   // pxm0 - i pxm1
+            const double2 B = cm<FOLD>(ux, make_double2(pxp.a.x - pxp.b.y, pxp.a.y + pxp.b.x));  // px0 + i px1
+            const double2 E = cm<FOLD>(e, make_double2(pxm.a.x + pxm.b.y, pxm.a.y - pxm.b.x));   // pxm0 - i pxm1
             h0 = cadd(cadd(cadd(A, B), C), E);
             h1 = cadd(cadd(cadd(cneg(A), mul_mi(B)), C), mul_i(E));
         } else {
-            const double2 E = cmul(e, make_double2(pxm.a.x - pxm.b.y, pxm.a.y + pxm.b.x));   // pxm0 + i pxm1
-            const double2 B = cmul(ux, make_double2(pxp.a.x + pxp.b.y, pxp.a.y - pxp.b.x));  // px0 - i px1
+            const double2 E = cm<FOLD>(e, make_double2(pxm.a.x - pxm.b.y, pxm.a.y + pxm.b.x));   // pxm0 + i pxm1
+            const double2 B = cm<FOLD>(ux, make_double2(pxp.a.x + pxp.b.y, pxp.a.y - pxp.b.x));  // px0 - i px1
             h0 = cadd(cadd(cadd(C, E), A), B);
             h1 = cadd(cadd(cadd(cneg(C), mul_mi(E)), A), mul_i(B));
         }
-        o.a = csub(rmul(mass, p.a), rmul(0.5, h0));
-        o.b = csub(rmul(mass, p.b), rmul(0.5, h1));
+        // mass p - 0.5 h as fma(-0.5, h, mass p): 0.5 h is exact, so both are
+        // the one rounding of (mass p) - 0.5 h
+        o.a = make_double2(__builtin_fma(-0.5, h0.x, mass * p.a.x), __builtin_fma(-0.5, h0.y, mass * p.a.y));
+        o.b = make_double2(__builtin_fma(-0.5, h1.x, mass * p.b.x), __builtin_fma(-0.5, h1.y, mass * p.b.y));
     } else {
         const Sp pm = shr(p), pp = shl(p);
         const double2 utm = dpp_shr1(ut);
@@ -239,22 +272,22 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
                 const int xr = y + 2;
                 const Sp Q = Mq, X = Mx;
                 Sp rp, R2;
-                rp.a = csub(D2.a, cmul(Q.a, beta2));
-                rp.b = csub(D2.b, cmul(Q.b, beta2));
-                R2.a = csub(rp.a, cmul(alpha, A.a));
-                R2.b = csub(rp.b, cmul(alpha, A.b));
-                J2.a = cadd(cmul(D2.a, beta), R2.a);
-                J2.b = cadd(cmul(D2.b, beta), R2.b);
+                rp.a = cfms<FOLD>(D2.a, Q.a, beta2);
+                rp.b = cfms<FOLD>(D2.b, Q.b, beta2);
+                R2.a = cfms<FOLD>(rp.a, alpha, A.a);
+                R2.b = cfms<FOLD>(rp.b, alpha, A.b);
+                J2.a = cfma<FOLD>(R2.a, D2.a, beta);
+                J2.b = cfma<FOLD>(R2.b, D2.b, beta);
                 if (xr >= x0 && xr < xe && own) {
                     const long n = (long)xr * Wt + c;
                     st_nt(a.dn + n, J2.a);
                     st_nt(a.dn + n + a.V, J2.b);
                     if (XP) {  // x_j = (x_{j-2} + alpha_{j-2} d_{j-2}) + alpha_{j-1} d_{j-1}
-                        st_nt(a.x + n, cadd(cadd(X.a, cmul(alpha2, Q.a)), cmul(alpha, D2.a)));
-                        st_nt(a.x + n + a.V, cadd(cadd(X.b, cmul(alpha2, Q.b)), cmul(alpha, D2.b)));
+                        st_nt(a.x + n, cfma<FOLD>(cfma<FOLD>(X.a, alpha2, Q.a), alpha, D2.a));
+                        st_nt(a.x + n + a.V, cfma<FOLD>(cfma<FOLD>(X.b, alpha2, Q.b), alpha, D2.b));
                     }
-                    acc_n.x += cmul(R2.a, cconj(R2.a)).x;  // Re dot(r, r), include/variables.h:185-188
-                    acc_n.x += cmul(R2.b, cconj(R2.b)).x;
+                    acc_n.x = nacc<FOLD>(acc_n.x, R2.a);  // Re dot(r, r), include/variables.h:185-188
+                    acc_n.x = nacc<FOLD>(acc_n.x, R2.b);
                 }
                 rlds[s_w][0][threadIdx.x] = R2.a;
                 rlds[s_w][1][threadIdx.x] = R2.b;
@@ -265,12 +298,12 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
                 const Sp o = ra_site<FOLD, 0>(mass, sr0, sl0, Q1, Q0, Q2, Ut0, Ux0, Uxm);  // S5: Ad_j(y)
                 if (own) {
                     const Sp R0 = Sp{rlds[s_r][0][threadIdx.x], rlds[s_r][1][threadIdx.x]};
-                    acc_dA = cadd(acc_dA, cmul(J0.a, cconj(o.a)));  // dot(d, Ad)
-                    acc_dA = cadd(acc_dA, cmul(J0.b, cconj(o.b)));
-                    acc_rA = cadd(acc_rA, cmul(R0.a, cconj(o.a)));  // dot(r, Ad)
-                    acc_rA = cadd(acc_rA, cmul(R0.b, cconj(o.b)));
-                    acc_n.y += cmul(o.a, cconj(o.a)).x;            // |Ad|^2
-                    acc_n.y += cmul(o.b, cconj(o.b)).x;
+                    acc_dA = cfma<FOLD>(acc_dA, J0.a, cconj(o.a));  // dot(d, Ad)
+                    acc_dA = cfma<FOLD>(acc_dA, J0.b, cconj(o.b));
+                    acc_rA = cfma<FOLD>(acc_rA, R0.a, cconj(o.a));  // dot(r, Ad)
+                    acc_rA = cfma<FOLD>(acc_rA, R0.b, cconj(o.b));
+                    acc_n.y = nacc<FOLD>(acc_n.y, o.a);            // |Ad|^2
+                    acc_n.y = nacc<FOLD>(acc_n.y, o.b);
                 }
             }
             D2 = D3;
@@ -342,7 +375,11 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
     if (c.xchunk < 1) c.xchunk = 1;
     c.XB = (g.Nx + c.xchunk - 1) / c.xchunk;
     c.remap = 1;
-    c.fold = 1;  // 0.604 vs 0.625 ms per iteration at 4096^2 (exact bracket arithmetic)
+    // 1: folded bracket, 0.604 vs 0.625 ms per iteration at 4096^2 against the
+    // exact bracket arithmetic; 2: plus fused multiply-adds, ~1 % faster again
+    // (tools/ab_fold.sh, ABBA: 0.513-0.517 vs 0.519-0.520 ms burst, 0.548-0.554
+    // vs 0.552-0.557 sustained)
+    c.fold = 2;
     if (const char *e = getenv("SM_CGRA_FOLD")) c.fold = atoi(e);
     return c;
 }
@@ -366,17 +403,17 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
     const dim3 grid(tbn * c.XB), block(64 * c.wpb);
     const int xp = pass >= 2 && (pass & 1) == 0;  // x takes passes j-1 and j together
     // one kernel per (shards, x pass, fold) combination
-    const int sel = (nshard > 1 ? 4 : 0) + (xp ? 2 : 0) + (c.fold ? 1 : 0);
+    const int f = c.fold >= 2 ? 2 : (c.fold ? 1 : 0);
+    const int sel = (nshard > 1 ? 6 : 0) + (xp ? 3 : 0) + f;
+#define SM_RA_CASE(SH, XP, F) \
+    case (SH) * 6 + (XP) * 3 + (F): hipLaunchKernelGGL((cg_ra_kernel<SH, XP, F>), grid, block, 0, s, a); break;
     switch (sel) {
-    case 0: hipLaunchKernelGGL((cg_ra_kernel<0, 0, 0>), grid, block, 0, s, a); break;
-    case 1: hipLaunchKernelGGL((cg_ra_kernel<0, 0, 1>), grid, block, 0, s, a); break;
-    case 2: hipLaunchKernelGGL((cg_ra_kernel<0, 1, 0>), grid, block, 0, s, a); break;
-    case 3: hipLaunchKernelGGL((cg_ra_kernel<0, 1, 1>), grid, block, 0, s, a); break;
-    case 4: hipLaunchKernelGGL((cg_ra_kernel<1, 0, 0>), grid, block, 0, s, a); break;
-    case 5: hipLaunchKernelGGL((cg_ra_kernel<1, 0, 1>), grid, block, 0, s, a); break;
-    case 6: hipLaunchKernelGGL((cg_ra_kernel<1, 1, 0>), grid, block, 0, s, a); break;
-    default: hipLaunchKernelGGL((cg_ra_kernel<1, 1, 1>), grid, block, 0, s, a); break;
+        SM_RA_CASE(0, 0, 0) SM_RA_CASE(0, 0, 1) SM_RA_CASE(0, 0, 2)
+        SM_RA_CASE(0, 1, 0) SM_RA_CASE(0, 1, 1) SM_RA_CASE(0, 1, 2)
+        SM_RA_CASE(1, 0, 0) SM_RA_CASE(1, 0, 1) SM_RA_CASE(1, 0, 2)
+        SM_RA_CASE(1, 1, 0) SM_RA_CASE(1, 1, 1) SM_RA_CASE(1, 1, 2)
     }
+#undef SM_RA_CASE
 }
 
 // k-deep t-faces: columns 0..k-1 go down (arrive as Wt..Wt+k-1), columns

@@ -182,7 +182,7 @@ def test_twodir_stepwise_finish_matches_onepass(sm, passes):
         assert rel <= 1e-13, (fused, rel)
 
 
-@pytest.mark.parametrize("fold", ["1", "0"])
+@pytest.mark.parametrize("fold", ["2", "1", "0"])
 @pytest.mark.parametrize("Nx,Nt,xchunk", [(96, 120, 0), (200, 56, 7), (5, 9, 0), (64, 64, 64)])
 def test_recompute_matches_twodir(sm, Nx, Nt, xchunk, fold):
     """The recompute-Ad pass (folded and exact bracket arithmetic) against the
