@@ -96,33 +96,6 @@ __device__ __forceinline__ RSrc rsrc(const double2 *base, const double2 *face, i
     return s;
 }
 
-// Complex products for the FOLD = 2 build: fused multiply-adds (one rounding
-// per component instead of three); FOLD <= 1 keeps GCC's separately rounded
-// expansion. cm = a b, cfma = c + a b, cfms = c - a b.
-template <int FOLD>
-__device__ __forceinline__ double2 cm(double2 a, double2 b) {
-    if (FOLD < 2) return cmul(a, b);
-    return make_double2(__builtin_fma(a.x, b.x, -(a.y * b.y)), __builtin_fma(a.x, b.y, a.y * b.x));
-}
-template <int FOLD>
-__device__ __forceinline__ double2 cfma(double2 c, double2 a, double2 b) {
-    if (FOLD < 2) return cadd(c, cmul(a, b));
-    return make_double2(__builtin_fma(a.x, b.x, __builtin_fma(-a.y, b.y, c.x)),
-                        __builtin_fma(a.x, b.y, __builtin_fma(a.y, b.x, c.y)));
-}
-template <int FOLD>
-__device__ __forceinline__ double2 cfms(double2 c, double2 a, double2 b) {
-    if (FOLD < 2) return csub(c, cmul(a, b));
-    return make_double2(__builtin_fma(-a.x, b.x, __builtin_fma(a.y, b.y, c.x)),
-                        __builtin_fma(-a.x, b.y, __builtin_fma(-a.y, b.x, c.y)));
-}
-// |z|^2 accumulated: acc + Re(z conj z)
-template <int FOLD>
-__device__ __forceinline__ double nacc(double acc, double2 z) {
-    if (FOLD < 2) return acc + cmul(z, cconj(z)).x;
-    return __builtin_fma(z.x, z.x, __builtin_fma(z.y, z.y, acc));
-}
-
 // D (DAG = 0) / D^dag (DAG = 1) at this lane's column: centre p, x-neighbours
 // pxm / pxp, t-neighbours from the adjacent lanes.
 //

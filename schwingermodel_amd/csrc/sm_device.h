@@ -143,6 +143,34 @@ __device__ __forceinline__ void dirac_site(double mass, double sr0, double sl0, 
     s1 = csub(rmul(mass, p1), rmul(0.5, h1));
 }
 
+// Complex products of the CG passes built with FOLD = 2 (sm_cgra.hip,
+// sm_eotd.hip): fused multiply-adds, one rounding per component instead of
+// two or three; FOLD <= 1 keeps GCC's separately rounded expansion.
+// cm = a b, cfma = c + a b, cfms = c - a b, nacc = acc + |z|^2.
+template <int FOLD>
+__device__ __forceinline__ double2 cm(double2 a, double2 b) {
+    if (FOLD < 2) return cmul(a, b);
+    return make_double2(__builtin_fma(a.x, b.x, -(a.y * b.y)), __builtin_fma(a.x, b.y, a.y * b.x));
+}
+template <int FOLD>
+__device__ __forceinline__ double2 cfma(double2 c, double2 a, double2 b) {
+    if (FOLD < 2) return cadd(c, cmul(a, b));
+    return make_double2(__builtin_fma(a.x, b.x, __builtin_fma(-a.y, b.y, c.x)),
+                        __builtin_fma(a.x, b.y, __builtin_fma(a.y, b.x, c.y)));
+}
+template <int FOLD>
+__device__ __forceinline__ double2 cfms(double2 c, double2 a, double2 b) {
+    if (FOLD < 2) return csub(c, cmul(a, b));
+    return make_double2(__builtin_fma(-a.x, b.x, __builtin_fma(a.y, b.y, c.x)),
+                        __builtin_fma(-a.x, b.y, __builtin_fma(-a.y, b.x, c.y)));
+}
+// |z|^2 accumulated: acc + Re(z conj z)
+template <int FOLD>
+__device__ __forceinline__ double nacc(double acc, double2 z) {
+    if (FOLD < 2) return acc + cmul(z, cconj(z)).x;
+    return __builtin_fma(z.x, z.x, __builtin_fma(z.y, z.y, acc));
+}
+
 // Deterministic block sum: wave butterfly, then lane-0 sums waves in order.
 __device__ __forceinline__ double2 block_sum(double2 v, double2 *sh) {
 #pragma unroll
