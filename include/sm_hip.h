@@ -114,7 +114,7 @@ int sm_synchronize(sm_ctx *ctx);
  * variant selects the stencil code variant. Values <= 0 (< 0 for xcd_remap
  * and variant) keep the current setting. */
 int sm_tune(sm_ctx *ctx, int bt, int xchunk, int xcd_remap, int variant);
-/* CG path: fused = 5 (the default from 1024^2 sites per shard up) is the
+/* CG path: fused = 5 (the default from 256^2 sites per shard up) is the
  * two-direction iteration that recomputes
  * Ad_{j-1} = D D^dag d_{j-1} in-kernel instead of storing it (sm_cgra.hip):
  * 160 B/site. fused = 4 (the default on smaller shards) is the

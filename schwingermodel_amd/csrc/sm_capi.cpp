@@ -401,11 +401,12 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     // iteration against the stored-Ad pass: 1024^2 0.054 vs 0.060, 2048^2 0.174
     // vs 0.223, 4096^2 0.588 vs 0.778); below that the stored-Ad pass is faster
     // (512^2 0.028 vs 0.030, 256^2 0.016 vs 0.019)
-    c->cg_fused = c->g.V >= (1L << 20) ? 5 : 4;
+    c->cg_fused = c->g.V >= (1L << 16) ? 5 : 4;  // recompute-Ad from 256^2 sites per shard (tools/small_cg.py)
     if (const char *e = getenv("SM_CG_FUSED")) c->cg_fused = atoi(e);
     if (const char *e = getenv("SM_EDGE_CONCURRENT")) c->edge_concurrent = atoi(e);
     if (const char *e = getenv("SM_SPLIT_TEST")) c->split_test = atoi(e);
     if (const char *e = getenv("SM_CG_INKERNEL_MAX_BLOCKS")) c->cg_inkernel_max_blocks = atoi(e);
+    if (const char *e = getenv("SM_CGRA_RED_MAX_BLOCKS")) c->cg_ra_red_max_blocks = atoi(e);
     if (const char *e = getenv("SM_CG_REDUNDANT")) c->cg_redundant = atoi(e);
     if (const char *e = getenv("SM_EO_FUSED")) c->eo_fused = atoi(e);
     if (const char *e = getenv("SM_EO_CG_FOLDED")) c->eo_cg_folded = atoi(e);
@@ -686,6 +687,7 @@ static int cg_onepass(sm_ctx *c) {
         pass(0, fc.TBk, c->stream);
         if (!inkernel) launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
         c->cg_flush_pass = redundant ? j : -1;
+        c->cg_flush_nparts = nparts;
         return SM_OK;
     }
     // interior t-blocks while the 2-deep faces of d, r, Ad travel (one round)
@@ -739,9 +741,19 @@ static int cg_ra_pass(sm_ctx *c) {
     c->cg_flush_pass = -1;
     const bool one = c->nshard == 1;
     if (one && !c->split_test) {
+        // redundant scalars on small grids (partials by pass parity; every block
+        // of the next pass evaluates them; sm_cg_iterate flushes the last pass)
+        const bool red = c->cg_redundant && fc.fold >= 2 && nparts <= c->cg_ra_red_max_blocks;
+        double2 *part = red ? c->partials + (j & 1) * 3 * (size_t)nparts : c->partials;
+        const double2 *prev = red ? c->partials + ((j + 1) & 1) * 3 * (size_t)nparts : nullptr;
         launch_cg_ra(c->stream, c->g, fc, 1, d1, d2, dn, c->cg_x, c->U, nullptr, nullptr, nullptr, c->cg_mass, j,
-                     c->sc, c->partials, 0, fc.TBk);
-        launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
+                     c->sc, part, 0, fc.TBk, prev);
+        if (red) {
+            c->cg_flush_pass = j;
+            c->cg_flush_nparts = nparts;
+        } else {
+            launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
+        }
         return SM_OK;
     }
     double2 *f1 = one ? nullptr : face4_recv_d(c, j), *f2 = one ? nullptr : face4_recv_d(c, j - 1);
@@ -865,7 +877,7 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
     }
     if (c->cg_fused >= 3 && c->cg_flush_pass >= 0) {  // redundant scalars: evaluate the last pass for the host
         const long J = c->cg_flush_pass;
-        const int nparts = cg_fused_blocks(c->fcfg);
+        const int nparts = c->cg_flush_nparts;
         launch_cg1_flush(c->stream, nparts, c->partials + (J & 1) * 3 * (size_t)nparts, c->sc, J);
         c->cg_flush_pass = -1;
     }

@@ -63,6 +63,8 @@ struct RAArgs {
     int xchunk, NWT, TBk, XB, remap, first, rebuild, wpb;
     int tb0, tbn;
     double mass;
+    const double2 *prev;  // RED: pass j-1's partials
+    long pass;
 };
 
 struct RSrc {
@@ -146,19 +148,46 @@ __device__ __forceinline__ Sp ra_site(double mass, double sr0, double sl0, const
     return o;
 }
 
-template <int SH, int XP, int FOLD>
+template <int SH, int XP, int FOLD, int RED = 0>
 __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
     __shared__ double2 sh[4];
     __shared__ double2 rlds[3][2][256];
     CGScalars *sc = a.sc;
-    if (sc->done) return;  // grid-uniform: converged (or max_iter) in an earlier pass
     // Passes 0 and 1 take zero multipliers instead of branches: pass 0 has
     // d_0 = r_0 (alpha = beta = 0), pass 1 has r_0 = d_0 (beta2 = 0). The
     // products by zero leave every value unchanged up to the sign of an exact zero.
     const double2 z2 = make_double2(0.0, 0.0);
     const bool first = a.first != 0, rebuild = a.rebuild != 0;
-    const double2 alpha = first ? z2 : sc->alpha, beta = first ? z2 : sc->beta;  // alpha_{j-1}, beta_{j-1}
-    const double2 alpha2 = sc->alpha2, beta2 = rebuild ? sc->beta2 : z2;         // alpha_{j-2}, beta_{j-2}
+    double2 alpha, beta, alpha2, beta2;  // alpha_{j-1}, beta_{j-1}, alpha_{j-2}, beta_{j-2}
+    if (RED) {  // every block evaluates pass j-1's scalars itself (same sums, same order)
+        __shared__ double2 s_ab[4];
+        __shared__ int s_stop;
+        if (!first) {
+            const CGRed s = cg1_redundant(sc, a.prev, a.TBk * a.XB, a.pass, sh);
+            if (threadIdx.x == 0) {
+                s_ab[0] = s.alpha;
+                s_ab[1] = s.beta;
+                s_ab[2] = s.alpha2;
+                s_ab[3] = s.beta2;
+                s_stop = s.done;
+            }
+        } else if (threadIdx.x == 0) {
+            s_ab[0] = s_ab[1] = s_ab[2] = s_ab[3] = z2;
+            s_stop = 0;
+        }
+        __syncthreads();
+        if (s_stop) return;  // block-uniform
+        alpha = first ? z2 : s_ab[0];
+        beta = first ? z2 : s_ab[1];
+        alpha2 = s_ab[2];
+        beta2 = rebuild ? s_ab[3] : z2;
+    } else {
+        if (sc->done) return;  // grid-uniform: converged (or max_iter) in an earlier pass
+        alpha = first ? z2 : sc->alpha;
+        beta = first ? z2 : sc->beta;
+        alpha2 = sc->alpha2;
+        beta2 = rebuild ? sc->beta2 : z2;
+    }
     int tb, xc;
     {
         int w = blockIdx.x;
@@ -360,7 +389,7 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
 void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard, const double2 *d1,
                   const double2 *d2, double2 *dn, double2 *x, const double2 *U, const double2 *f1,
                   const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
-                  int tb0, int tbn) {
+                  int tb0, int tbn, const double2 *prev_partials) {
     if (tbn <= 0) return;
     RAArgs a;
     a.d1 = d1; a.d2 = d2; a.dn = dn; a.x = x; a.U = U;
@@ -373,10 +402,17 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
     a.tb0 = tb0;
     a.tbn = tbn;
     a.mass = mass;
+    a.prev = prev_partials;
+    a.pass = pass;
     const dim3 grid(tbn * c.XB), block(64 * c.wpb);
     const int xp = pass >= 2 && (pass & 1) == 0;  // x takes passes j-1 and j together
     // one kernel per (shards, x pass, fold) combination
     const int f = c.fold >= 2 ? 2 : (c.fold ? 1 : 0);
+    if (prev_partials && nshard == 1 && f == 2 && tb0 == 0 && tbn == c.TBk) {
+        if (xp) hipLaunchKernelGGL((cg_ra_kernel<0, 1, 2, 1>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((cg_ra_kernel<0, 0, 2, 1>), grid, block, 0, s, a);
+        return;
+    }
     const int sel = (nshard > 1 ? 6 : 0) + (xp ? 3 : 0) + f;
 #define SM_RA_CASE(SH, XP, F) \
     case (SH) * 6 + (XP) * 3 + (F): hipLaunchKernelGGL((cg_ra_kernel<SH, XP, F>), grid, block, 0, s, a); break;

@@ -68,6 +68,8 @@ struct sm_ctx {
     int cg_inkernel_max_blocks = sm::kInKernelScalarMaxBlocks;  // one-pass path (sm_cgfused.hip)
     int cg_redundant = 1;           // those grids: every block evaluates the previous pass's scalars
     long cg_flush_pass = -1;        // last one-pass pass whose scalars still await evaluation
+    int cg_flush_nparts = 0;        // its partial count (the one-pass or the recompute-Ad grid)
+    int cg_ra_red_max_blocks = 512; // recompute-Ad pass: redundant scalars up to this many blocks (one shard)
     hipStream_t own_stream = nullptr, stream = nullptr;
     hipStream_t comm_stream = nullptr;  // halo exchange overlapped with interior compute
     hipEvent_t ev_ready = nullptr, ev_halo = nullptr;

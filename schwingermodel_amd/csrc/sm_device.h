@@ -189,6 +189,59 @@ __device__ __forceinline__ double2 block_sum(double2 v, double2 *sh) {
     return r;
 }
 
+// ---- one-pass CG scalars (sm_cgfused.hip, sm_cgra.hip) ----------------------
+// From the three global sums: stop test on the direct |r_j|^2 (j >= 1), then
+// alpha_j and beta_j (src/conjugate_gradient.cpp:33, 43-61).
+__device__ __forceinline__ CGRed cg1_eval(CGRed s, double tol, double phi_norm, int max_iter, int first, double2 dA,
+                                          double2 rA, double2 nn) {
+    const double rr = nn.x, AA = nn.y;
+    if (!first) {
+        s.err = sqrt(rr);
+        s.k += 1;
+        if (s.err < tol * phi_norm) {
+            s.done = 1;
+            s.converged = 1;
+            return s;
+        }
+        if (s.k >= max_iter) {
+            s.done = 1;
+            return s;
+        }
+    }
+    s.rn = make_double2(rr, 0.0);
+    const double2 al = cdiv(rr, 0.0, dA.x, dA.y);   // r_norm2 / dot(d, Ad)
+    s.alpha2 = s.alpha;                             // two-direction CG keeps one pass of history
+    s.beta2 = s.beta;
+    s.alpha = al;
+    const double est = rr - 2.0 * (al.x * rA.x + al.y * rA.y) + (al.x * al.x + al.y * al.y) * AA;
+    s.beta = cdiv(est, 0.0, rr, 0.0);               // err^2 / r_norm2
+    return s;
+}
+
+// Redundant scalars: S_{j-1} from S_{j-2} (red[j & 1]) and pass j-1's partials,
+// evaluated by every block (all threads: block sums in a fixed order); block 0
+// stores it to red[(j-1) & 1]. Returns S_{j-1} (valid in thread 0).
+__device__ __forceinline__ CGRed cg1_redundant(CGScalars *sc, const double2 *prev, int nparts, long j, double2 *sh) {
+    CGRed s = sc->red[j & 1];
+    if (!s.done) {
+        double2 acc[3] = {make_double2(0.0, 0.0), make_double2(0.0, 0.0), make_double2(0.0, 0.0)};
+        for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
+            acc[0] = cadd(acc[0], prev[3 * i]);
+            acc[1] = cadd(acc[1], prev[3 * i + 1]);
+            acc[2] = cadd(acc[2], prev[3 * i + 2]);
+        }
+        double2 t[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            t[q] = block_sum(acc[q], sh);
+            __syncthreads();
+        }
+        s = cg1_eval(s, sc->tol, sc->phi_norm, sc->max_iter, j - 1 == 0, t[0], t[1], t[2]);
+    }
+    if (threadIdx.x == 0 && blockIdx.x == 0) sc->red[(j - 1) & 1] = s;
+    return s;
+}
+
 // Wave-wide lane shifts by one (DPP wave_shr:1 / wave_shl:1, GFX9-family
 // incl. gfx950): no LDS, no barrier. Lane 0 (shr) / lane 63 (shl) receive 0.
 __device__ __forceinline__ double dpp_shr1(double v) {  // lane l <- lane l-1

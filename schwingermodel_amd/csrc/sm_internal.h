@@ -135,7 +135,10 @@ CGFusedCfg cg_ra_config(const Geometry &g);
 void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard, const double2 *d1,
                   const double2 *d2, double2 *dn, double2 *x, const double2 *U, const double2 *f1,
                   const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
-                  int tb0, int tbn);
+                  int tb0, int tbn, const double2 *prev_partials = nullptr);
+// prev_partials != null (one shard, fold 2): redundant scalars as in
+// cg_onepass_kernel: every block evaluates pass j-1's scalars from its partials
+// (cg1_redundant); the caller keeps the partials by pass parity and flushes.
 // Pack the k-deep t-faces of a field: lo = columns 0..k-1, hi = columns Wt-k..Wt-1, [col][plane][x].
 void launch_pack_faces_k(hipStream_t s, const Geometry &g, int k, const double2 *field, double2 *lo, double2 *hi);
 // Two-direction form, after the last pass J = sc->k: if J is odd, x += alpha_{J-1} d_{J-1}
