@@ -182,25 +182,28 @@ def test_twodir_stepwise_finish_matches_onepass(sm, passes):
         assert rel <= 1e-13, (fused, rel)
 
 
-@pytest.mark.parametrize("fold", ["2", "1", "0"])
+@pytest.mark.parametrize("fold,red", [("2", "512"), ("2", "0"), ("1", "512"), ("0", "512")])
 @pytest.mark.parametrize("Nx,Nt,xchunk", [(96, 120, 0), (200, 56, 7), (5, 9, 0), (64, 64, 64)])
-def test_recompute_matches_twodir(sm, Nx, Nt, xchunk, fold):
-    """The recompute-Ad pass (folded and exact bracket arithmetic) against the
+def test_recompute_matches_twodir(sm, Nx, Nt, xchunk, fold, red):
+    """The recompute-Ad pass (fused multiply-add, folded and exact bracket
+    arithmetic; in-kernel redundant scalars or the scalar kernel) against the
     two-direction pass that stores Ad: the same iteration count to 1e-10 and
     x within the reduction-order band, including chunks shorter than the
     4-row halo, Nt not a multiple of the 56-column wave and a lattice smaller
     than one wave's halo."""
     import os
     S = Nx * Nt
-    old = os.environ.get("SM_CGRA_FOLD")
-    os.environ["SM_CGRA_FOLD"] = fold  # read when the context is created
+    env = {"SM_CGRA_FOLD": fold, "SM_CGRA_RED_MAX_BLOCKS": red}  # read when the context is created
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         L = sm.init(Nx, Nt)
     finally:
-        if old is None:
-            del os.environ["SM_CGRA_FOLD"]
-        else:
-            os.environ["SM_CGRA_FOLD"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     U, psi = sm.spinor(S), sm.spinor(S)
     P = lambda a: a.ctypes.data  # noqa: E731
     sm.lib.sm_fill_gauge(4321, 0.4242, Nt, 0, Nx, 0, Nt, P(U.mu0), P(U.mu1))
