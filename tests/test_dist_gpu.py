@@ -89,6 +89,7 @@ def test_sharded_md_matches_reference(tmp_path, fixture, world):
 @pytest.mark.parametrize("fixture,world,fused,folded,td", [
     ("gen:32x48:0.4242:0.0", 2, "1", "0", "1"),   # the one-pass eo CG (4-deep faces of d, Ad)
     ("gen:32x48:0.3:-0.1", 4, "1", "0", "1"),
+    ("gen:32x48:0.3:-0.1", 6, "1", "0", "1"),     # Wt = 8: the narrowest shard it takes (faces = a whole neighbour)
     ("gen:32x48:0.3:-0.1", 8, "1", "0", "1"),     # Wt = 6 < 8: falls back to the six-launch iteration
     ("gen:32x48:0.3:-0.1", 4, "1", "0", "0"),     # the six-launch iteration
     ("gen:32x48:0.3:-0.1", 4, "0", "0", "0"),     # the two-launch Dhat (eo_hop with faces)
