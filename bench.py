@@ -2,26 +2,37 @@
 """Benchmark of the hot path: CG on D D^dagger + the Wilson-Dirac apply, fp64.
 
 Metric (BASELINE.json): CG iterations/s and Dirac-apply achieved HBM GB/s on a
-4096 x 4096 lattice (beta = 5 synthetic U(1) field, sigma = 0.2374, m0 = -0.06).
+4096 x 4096 lattice (beta = 5 synthetic U(1) field, sigma = 0.2374, m0 = -0.06),
+at 1/2/4/8 GPUs.
 
 One "step" = one CG iteration (src/conjugate_gradient.cpp:31-63): Ad = D D^dag d,
 <d,Ad>, x += alpha d, r -= alpha Ad, <r,r>, stop test, d = beta d + r -- all on
 device, inputs resident in HBM. The CG runs with tol = 0 so every timed
 iteration does the full work.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
-one process per GPU, the lattice sharded along t with RCCL halos; weak scaling,
-each GPU owns 4096 x 4096 sites (global lattice 4096 x 4096N). `value` is the
-whole-job rate in 4096^2-lattice CG iterations per second (= it/s x N).
-`--strong` instead splits one fixed 4096 x 4096 lattice over the N GPUs
- and reports that lattice's it/s.
-torch.distributed (gloo) is used only for the RCCL unique id, barriers and the
-max-over-ranks timing.
+Workloads (BASELINE.json configs):
+  --config 3  (default for N = 1)  4096^2, beta=5 field, m0=-0.06, one GPU.
+  --config 4  (default for N > 1)  the SAME 4096^2 lattice sharded along t over
+              the N GPUs (strong scaling: N = 1 and N = 8 run one workload).
+              The weak-scaling variant of config 4 (4096 x 512N, so N = 8 is
+              4096^2) is measured too and reported under "weak".
+  --config 5  8192^2, beta=2 field (sigma 0.4242), m0=-0.19 (near m_crit),
+              sharded over N GPUs: CG to 1e-10 from x0 = phi (the reference's
+              start), time to solution, iterations and the true residual.
+
+Multi-GPU: one process per GPU. Launched by the driver as
+`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`
+(WORLD_SIZE must equal --gpus). `python bench.py --gpus N` with no
+WORLD_SIZE spawns the N ranks itself, before anything touches the GPU.
+torch.distributed (gloo) is control plane only: the RCCL unique id, barriers
+and the max-over-ranks timing. `--transport hosted` runs the shards over the
+host-staged transport (several ranks may share one GPU; tests / rehearsal).
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -29,90 +40,171 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-NX = 4096
-NT_PER_GPU = 4096
-SIGMA_B5 = 0.2374      # beta = 5
-M0 = -0.06
 SEED_U, SEED_CHI = 4321, 91011
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_SITE_APPLY = 96  # read psi 32 + U 32, write 32
 # algorithmic HBM bytes per site of one CG iteration, by path
-BYTES_PER_SITE_CG = {"recompute": 160, "twodir": 224, "onepass": 288, "fused": 320, "fused_inkernel": 320,
-                     "sixkernel": 576}
+BYTES_PER_SITE_CG = {"recompute": 160, "twodir": 224, "onepass": 288, "fused": 320, "sixkernel": 576}
+CG_PATH_ID = {"recompute": 5, "twodir": 4, "onepass": 3, "fused": 1, "sixkernel": 0}
+
+# BASELINE.json configs on the GPU (1 and 2 are the CPU-plumbing / 1024^2 parity cases)
+CONFIGS = {
+    3: dict(Nx=4096, Nt=4096, sigma=0.2374, m0=-0.06,
+            name="config 3: 4096x4096 lattice, beta=5 field, m0=-0.06"),
+    4: dict(Nx=4096, Nt=4096, sigma=0.2374, m0=-0.06,
+            name="config 4: 4096x4096 lattice (beta=5 field, m0=-0.06) t-sharded over the GPUs (strong)"),
+    5: dict(Nx=8192, Nt=8192, sigma=0.4242, m0=-0.19,
+            name="config 5: 8192x8192 lattice near m_crit (beta=2 field, m0=-0.19), CG to 1e-10"),
+}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--applies", type=int, default=100, help="timed Dirac applies")
-    ap.add_argument("--nx", type=int, default=NX)
-    ap.add_argument("--nt-per-gpu", type=int, default=NT_PER_GPU)
+    ap.add_argument("--config", type=int, choices=[3, 4, 5], default=None,
+                    help="BASELINE.json config (default: 3 on one GPU, 4 on several)")
+    ap.add_argument("--nx", type=int, default=None, help="override the config's lattice (tests)")
+    ap.add_argument("--nt", type=int, default=None)
+    ap.add_argument("--no-weak", action="store_true", help="skip the weak-scaling extra of config 3/4")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("SM_CPU_THREADS", "16")))
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="host cores for the CPU baseline (default: this process's CPU share)")
+    ap.add_argument("--cpu-iters", type=int, default=50, help="CG iterations of the CPU baseline sample")
     ap.add_argument("--transport", choices=["rccl", "hosted"], default="rccl",
                     help="multi-GPU wire: RCCL (production) or the host-staged test transport")
-    ap.add_argument("--device", type=int, default=None, help="override LOCAL_RANK -> GPU mapping")
-    ap.add_argument("--cg-path", choices=["recompute", "twodir", "onepass", "fused", "fused_inkernel", "sixkernel"],
-                    default="recompute")
-    ap.add_argument("--strong", action="store_true",
-                    help="strong scaling (SURVEY.md §8d config 4): a fixed nx x nt-per-gpu lattice split over the N GPUs")
-    return ap.parse_args()
+    ap.add_argument("--device", type=int, default=None, help="override the rank -> GPU mapping")
+    ap.add_argument("--cg-path", choices=list(CG_PATH_ID), default="recompute")
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(args, threads):
+# --------------------------------------------------------------------------- launch
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N fresh rank processes
+    (nothing in this parent touches the GPU) and exit with the worst code."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        for p in procs:
+            rc = max(rc, p.wait())
+            if rc:
+                break
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+    return rc
+
+
+# --------------------------------------------------------------------------- CPU baseline
+
+def cpu_share():
+    """Host cores this process may use: the affinity mask, capped by
+    OMP_NUM_THREADS (the GPU box sets it to the box's CPU share; nproc there
+    shows the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def decompose(threads):
+    """ranks_x x ranks_t <= threads, both powers of two (they must divide the
+    power-of-two lattice, include/mpi_setup.h:6-23), ranks_x >= 2 (the reference
+    deadlocks for ranks_x = 1), as square as possible."""
+    p = 1 << (max(2, threads).bit_length() - 1)
+    k = p.bit_length() - 1
+    rx = 1 << ((k + 1) // 2)
+    return rx, p // rx
+
+
+def cpu_baseline(cfg, threads, ncg):
     """CPU reference timed on this host on a bounded sample of the same workload.
 
-    Preferred: the unmodified reference (oracle/_ref/sm_ref_4096x4096, built in
-    the dev container) under MPI with a 2D decomposition (ranks_x >= 2; the
-    reference deadlocks for ranks_x = 1). Fallback: the oracle
-    restatement (single thread CG, threaded D)."""
-    exe = os.path.join(REPO, "oracle", "_ref", f"sm_ref_{args.nx}x{args.nt_per_gpu}")
+    Preferred: the unmodified reference (oracle/_ref/sm_ref_<Nx>x<Nt>, built in
+    the dev container from /root/reference) under MPI with a 2D decomposition.
+    Fallback: the bit-exact oracle restatement (one thread)."""
+    Nx, Nt, m0, sigma = cfg["Nx"], cfg["Nt"], cfg["m0"], cfg["sigma"]
+    exe = os.path.join(REPO, "oracle", "_ref", f"sm_ref_{Nx}x{Nt}")
     mpirun = "/opt/conda/bin/mpirun"
-    ncg = 12
-    if os.path.exists(exe) and os.path.exists(mpirun):
-        rx = 4 if threads >= 16 else 2
-        rt = max(1, threads // rx)
+    model = cpu_model()
+    if os.path.exists(exe) and os.path.exists(mpirun) and threads >= 2:
+        rx, rt = decompose(threads)
         cmd = [mpirun, "-n", str(rx * rt), exe, "bench", str(rx), str(rt), str(SEED_U),
-               repr(SIGMA_B5), str(SEED_CHI), repr(M0), "3", str(ncg)]
+               repr(sigma), str(SEED_CHI), repr(m0), "3", str(ncg)]
         try:
-            env = dict(os.environ, HOSTNAME=os.environ.get("HOSTNAME", "localhost"))
-            out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+            env = dict(os.environ, HOSTNAME=os.environ.get("HOSTNAME", "localhost"), OMP_NUM_THREADS="1")
+            out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
             if out.returncode == 0:
                 r = json.loads(out.stdout.strip().splitlines()[-1])
-                return {"value": r["cg_it_per_s"], "unit": "CG iterations/s (4096^2)",
-                        "cores": rx * rt, "kind": "reference",
-                        "sample": f"{r['cg_iters']} CG iterations + 3 D applies at {args.nx}x{args.nt_per_gpu}, "
-                                  f"MPI {rx}x{rt} ranks (unmodified reference via oracle/_ref)",
+                return {"value": r["cg_it_per_s"], "unit": f"CG iterations/s ({Nx}x{Nt})",
+                        "cores": rx * rt, "kind": "reference", "cpu_model": model,
+                        "decomposition": f"MPI ranks_x={rx} x ranks_t={rt}",
+                        "sample": f"{r['cg_iters']} CG iterations (tol 0) + 3 D applies at {Nx}x{Nt}, "
+                                  f"unmodified reference (oracle/_ref) under MPICH, {rx}x{rt} ranks, 1 thread each",
                         "dirac_apply_GBps": r["apply_GBps"]}
+            print(f"[bench] reference CPU baseline rc={out.returncode}: {out.stderr[-400:]}", file=sys.stderr)
         except Exception as e:  # noqa: BLE001 -- fall through to the port
             print(f"[bench] reference CPU baseline failed: {e}", file=sys.stderr)
-    # oracle port: single-threaded CG, a few iterations
+    # oracle port: single-threaded CG, a few iterations (test checker used as the timed baseline)
     import numpy as np
+    import schwingermodel_amd as sm
     o = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
     vp, ci, cd = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
     o.oracle_cg.argtypes = [ci, ci, vp, vp, vp, vp, vp, vp, cd, cd, ci, ctypes.POINTER(ci), ctypes.POINTER(cd)]
-    import schwingermodel_amd as sm
-    Nx, Nt = args.nx, args.nt_per_gpu
     S = Nx * Nt
     U0, U1, p0, p1 = (np.empty(2 * S) for _ in range(4))
-    sm.lib.sm_fill_gauge(SEED_U, SIGMA_B5, Nt, 0, Nx, 0, Nt, U0.ctypes.data, U1.ctypes.data)
+    sm.lib.sm_fill_gauge(SEED_U, sigma, Nt, 0, Nx, 0, Nt, U0.ctypes.data, U1.ctypes.data)
     sm.lib.sm_fill_spinor(SEED_CHI, Nt, 0, Nx, 0, Nt, p0.ctypes.data, p1.ctypes.data)
     x0, x1 = np.empty(2 * S), np.empty(2 * S)
     it, err = ctypes.c_int(), ctypes.c_double()
-    n = 4
+    n = max(2, min(ncg, 8))
     t = time.perf_counter()
     o.oracle_cg(Nx, Nt, U0.ctypes.data, U1.ctypes.data, p0.ctypes.data, p1.ctypes.data,
-                x0.ctypes.data, x1.ctypes.data, M0, 0.0, n, ctypes.byref(it), ctypes.byref(err))
+                x0.ctypes.data, x1.ctypes.data, m0, 0.0, n, ctypes.byref(it), ctypes.byref(err))
     dt = time.perf_counter() - t
-    return {"value": it.value / dt, "unit": "CG iterations/s (4096^2)", "cores": 1, "kind": "port",
+    return {"value": it.value / dt, "unit": f"CG iterations/s ({Nx}x{Nt})", "cores": 1, "kind": "port",
+            "cpu_model": model, "decomposition": "1 thread",
             "sample": f"{it.value} CG iterations (incl. initial DD^dag) at {Nx}x{Nt}, oracle/sm_oracle.c"}
 
 
 def load_traffic(nx, nt):
     """HBM bytes per dslash launch from the committed rocprofv3 PMC summary
-    (profiles/*_dslash_pmc.json, FETCH_SIZE x2 + WRITE_SIZE per the gfx950 rule)."""
+    (profiles/*_dslash_pmc.json, FETCH_SIZE + WRITE_SIZE with the gfx950 rule);
+    the newest file for this local shape wins."""
     best = None
     pdir = os.path.join(REPO, "profiles")
     if os.path.isdir(pdir):
@@ -122,150 +214,307 @@ def load_traffic(nx, nt):
                     with open(os.path.join(pdir, f)) as fh:
                         d = json.load(fh)
                     if d.get("Nx") == nx and d.get("Nt") == nt:
-                        best = d.get("hbm_bytes_per_launch")
+                        best = (f, d.get("hbm_bytes_per_launch"))
                 except Exception:  # noqa: BLE001
                     pass
     return best
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import numpy as np
+# --------------------------------------------------------------------------- GPU side
+
+class Shard:
+    """This rank's t-shard of an Nx x Nt lattice with its fields resident in HBM."""
+
+    def __init__(self, rt, Nx, Nt, sigma):
+        import torch
+        import schwingermodel_amd as sm
+        from schwingermodel_amd import dist as smd
+        self.sm, self.rt = sm, rt
+        world, rank, device = rt["world"], rt["rank"], rt["device"]
+        if Nt % world:
+            raise SystemExit(f"Nt={Nt} is not divisible by {world} GPUs")
+        self.transport = None
+        if world > 1 and rt["transport"] == "hosted":
+            ctx, self.transport = smd.create_hosted_context(Nx, Nt, device=device)
+            L = sm.Lattice.__new__(sm.Lattice)
+            L.ctx, L.Nx, L.Nt, L.Wt, L.t0 = ctx, Nx, Nt, Nt // world, rank * (Nt // world)
+            L.V, L.shard, L.nshard = Nx * L.Wt, rank, world
+        else:
+            uid = smd.broadcast_unique_id() if world > 1 else None
+            L = sm.Lattice(Nx, Nt, nshard=world, shard=rank, device=device, unique_id=uid)
+        self.L, self.Nx, self.Nt, self.Wt, self.V = L, Nx, Nt, L.Wt, L.V
+        sm.check(sm.lib.sm_set_stream(L.ctx, ctypes.c_void_p(rt["stream"].cuda_stream)))
+        # synthetic inputs (counter-based: each shard makes its own slice, no transfer)
+        U = torch.empty(4 * self.V, dtype=torch.float64)
+        chi = torch.empty(4 * self.V, dtype=torch.float64)
+        _fill(sm, Nx, Nt, L.t0, L.Wt, sigma, U.numpy(), chi.numpy())
+        self.U = U.cuda()
+        self.phi = chi.cuda()
+        del U, chi
+        self.x = torch.empty_like(self.phi)
+        self.out = torch.empty_like(self.phi)
+        sm.check(sm.lib.sm_upload_gauge_dev(L.ctx, self.p(self.U)))
+
+    @staticmethod
+    def p(t):
+        return ctypes.c_void_p(t.data_ptr())
+
+    def close(self):
+        self.L.close()
+
+
+def _fill(sm, Nx, Nt, t0, Wt, sigma, U, chi, nthreads=8):
+    """Row blocks of the counter-based generator in threads (it is row-separable)."""
+    from concurrent.futures import ThreadPoolExecutor
+    V = Nx * Wt
+    rows = max(1, -(-Nx // nthreads))
+
+    def job(x0):
+        nx = min(rows, Nx - x0)
+        off = 2 * x0 * Wt
+        sm.lib.sm_fill_gauge(SEED_U, sigma, Nt, x0, nx, t0, Wt, U[off:].ctypes.data, U[2 * V + off:].ctypes.data)
+        sm.lib.sm_fill_spinor(SEED_CHI, Nt, x0, nx, t0, Wt, chi[off:].ctypes.data, chi[2 * V + off:].ctypes.data)
+    with ThreadPoolExecutor(nthreads) as ex:
+        list(ex.map(job, range(0, Nx, rows)))
+
+
+def barrier(rt):
     import torch
     import torch.distributed as dist
-    import schwingermodel_amd as sm
+    torch.cuda.synchronize()
+    if rt["world"] > 1:
+        dist.barrier()
+
+
+def max_over_ranks(rt, vals):
     from schwingermodel_amd import dist as smd
+    return smd.max_over_ranks(vals) if rt["world"] > 1 else list(vals)
 
-    if world > 1:
-        dist.init_process_group("gloo")
-    device = local_rank if args.device is None else args.device
-    torch.cuda.set_device(device)
 
-    def barrier():
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-
-    Nx, Wt = args.nx, args.nt_per_gpu
-    if args.strong:
-        if Wt % world:
-            raise SystemExit(f"--strong: Nt={Wt} is not divisible by {world} GPUs")
-        Wt //= world
-    Nt = Wt * world
-    transport = None
-    if world > 1 and args.transport == "hosted":
-        ctx, transport = smd.create_hosted_context(Nx, Nt, device=device)
-        L = sm.Lattice.__new__(sm.Lattice)
-        L.ctx, L.Nx, L.Nt, L.Wt, L.t0, L.V = ctx, Nx, Nt, Wt, rank * Wt, Nx * Wt
-    else:
-        uid = smd.broadcast_unique_id() if world > 1 else None
-        L = sm.Lattice(Nx, Nt, nshard=world, shard=rank, device=device, unique_id=uid)
-    V = L.V
-    t0 = L.t0
-    # a real (non-null) torch stream: the library launches on it, so the torch
-    # events below bracket exactly the kernels being timed
-    stream = torch.cuda.Stream()
-    torch.cuda.set_stream(stream)
-    sm.check(sm.lib.sm_set_stream(L.ctx, ctypes.c_void_p(stream.cuda_stream)))
-
-    # synthetic inputs of the benchmark shape (counter-based: each shard makes its slice)
-    U = torch.empty(4 * V, dtype=torch.float64)
-    chi = torch.empty(4 * V, dtype=torch.float64)
-    Un, cn = U.numpy(), chi.numpy()
-    sm.lib.sm_fill_gauge(SEED_U, SIGMA_B5, Nt, 0, Nx, t0, Wt, Un.ctypes.data, Un[2 * V:].ctypes.data)
-    sm.lib.sm_fill_spinor(SEED_CHI, Nt, 0, Nx, t0, Wt, cn.ctypes.data, cn[2 * V:].ctypes.data)
-    dU = U.cuda()
-    phi = chi.cuda()
-    x = torch.empty_like(phi)
-    out = torch.empty_like(phi)
-    sm.check(sm.lib.sm_upload_gauge_dev(L.ctx, ctypes.c_void_p(dU.data_ptr())))
-    del U, chi
-
-    # ---- Dirac apply: HIP events on the stream the kernel is launched on ----
+def time_applies(rt, sh, m0, n):
+    """Dirac apply D, HIP events on the stream the kernel is launched on."""
+    import torch
+    sm = sh.sm
     for _ in range(10):
-        sm.check(sm.lib.sm_dirac_dev(L.ctx, ctypes.c_void_p(phi.data_ptr()), ctypes.c_void_p(out.data_ptr()), M0, 0))
-    barrier()
+        sm.check(sm.lib.sm_dirac_dev(sh.L.ctx, sh.p(sh.phi), sh.p(sh.out), m0, 0))
+    barrier(rt)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(args.applies):
-        sm.check(sm.lib.sm_dirac_dev(L.ctx, ctypes.c_void_p(phi.data_ptr()), ctypes.c_void_p(out.data_ptr()), M0, 0))
-    e1.record(stream)
-    barrier()
-    apply_s = e0.elapsed_time(e1) / 1e3 / args.applies
-    apply_GBps = BYTES_PER_SITE_APPLY * V / apply_s / 1e9
+    e0.record(rt["stream"])
+    for _ in range(n):
+        sm.check(sm.lib.sm_dirac_dev(sh.L.ctx, sh.p(sh.phi), sh.p(sh.out), m0, 0))
+    e1.record(rt["stream"])
+    barrier(rt)
+    return e0.elapsed_time(e1) / 1e3 / n
 
-    sm.check(sm.lib.sm_tune_cg(L.ctx, {"recompute": 5, "twodir": 4, "onepass": 3, "fused": 1, "fused_inkernel": 2, "sixkernel": 0}[args.cg_path], 0))
-    # ---- CG iterations (tol = 0: never converges, full work every step) ----
-    sm.check(sm.lib.sm_cg_begin(L.ctx, ctypes.c_void_p(phi.data_ptr()), ctypes.c_void_p(x.data_ptr()), M0, 0.0))
-    sm.check(sm.lib.sm_cg_iterate(L.ctx, args.warmup))
-    barrier()
+
+def time_cg_steps(rt, sh, m0, cg_path, warmup, steps):
+    """K CG iterations (tol = 0: never converges, the full work every step)
+    bracketed by a barrier + device synchronisation on both sides."""
+    import torch
+    sm = sh.sm
+    sm.check(sm.lib.sm_tune_cg(sh.L.ctx, CG_PATH_ID[cg_path], 0))
+    sm.check(sm.lib.sm_cg_begin(sh.L.ctx, sh.p(sh.phi), sh.p(sh.x), m0, 0.0))
+    sm.check(sm.lib.sm_cg_iterate(sh.L.ctx, warmup))
+    barrier(rt)
     c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     w0 = time.perf_counter()
-    c0.record(stream)
-    sm.check(sm.lib.sm_cg_iterate(L.ctx, args.steps))
-    c1.record(stream)
-    barrier()
+    c0.record(rt["stream"])
+    sm.check(sm.lib.sm_cg_iterate(sh.L.ctx, steps))
+    c1.record(rt["stream"])
+    barrier(rt)
     wall = time.perf_counter() - w0
     res = sm.CGResult()
-    sm.check(sm.lib.sm_cg_status(L.ctx, ctypes.byref(res)))
-    # the one-pass iteration's pass 0 (in the warmup) only forms Ad_0: every
+    sm.check(sm.lib.sm_cg_status(sh.L.ctx, ctypes.byref(res)))
+    # the one-pass iterations' pass 0 (in the warmup) only forms Ad_0: every
     # later pass is one full reference iteration
-    setup_passes = 1 if args.cg_path in ("onepass", "twodir", "recompute") else 0
-    assert res.iterations == args.warmup + args.steps - setup_passes and res.converged == 0
-    t_ev = c0.elapsed_time(c1) / 1e3
-    t_local = max(wall, t_ev)
-    if world > 1:
-        t_local, apply_s = smd.max_over_ranks([t_local, apply_s])
-        apply_GBps = BYTES_PER_SITE_APPLY * V / apply_s / 1e9
+    setup_passes = 1 if cg_path in ("onepass", "twodir", "recompute") else 0
+    if res.iterations != warmup + steps - setup_passes or res.converged != 0:
+        raise SystemExit(f"CG ran {res.iterations} iterations (converged={res.converged}), "
+                         f"expected {warmup + steps - setup_passes}")
+    return max(wall, c0.elapsed_time(c1) / 1e3)
 
-    if rank == 0:
-        it_per_s = args.steps / t_local
-        # weak: 4096^2-lattice iterations per second, whole job; strong: the
-        # one fixed lattice's iterations per second
-        value = it_per_s if args.strong else it_per_s * world
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args, args.cpu_threads)
-        traffic = load_traffic(Nx, Wt)
-        line = {
-            "metric": "CG iterations/sec + Dirac-apply achieved HBM GB/s, 4096^2 fp64",
-            "value": round(value, 3),
-            "unit": (f"CG iterations/s (one {Nx}x{Nt} lattice over all GPUs)" if args.strong
-                     else f"CG iterations/s ({Nx}x{Wt} sites per GPU, whole job)"),
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(1e3 * t_local / args.steps, 4),
-            "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (counter-based U(1) field theta~N(0,0.2374^2), complex-Gaussian RHS)",
-            "config": {"workload": f"CG on D D^dag, {Nx}x{Nt} lattice (beta=5 field, m0={M0}), "
-                                   f"t-sharded over {world} GPU(s)",
-                       "transport": args.transport if world > 1 else None,
-                       "Nx": Nx, "Nt": Nt, "sites_per_gpu": V, "m0": M0, "sigma": SIGMA_B5,
-                       "parallelism": f"t-shard x{world}" + (" (RCCL halos)" if world > 1 else "")},
-            "dirac_apply_GBps": round(apply_GBps, 1),
-            "dirac_apply_us": round(apply_s * 1e6, 2),
-            "roofline": {"bound": "hbm", "achieved": round(apply_GBps, 1), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(apply_GBps / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic,
-                         "kernel": "dslash_kernel<D> (96 B/site algorithmic)"},
-            "cpu_baseline": cpu,
-            # the CG iteration's own streaming rate (informational; the graded
-            # roofline is the Dirac apply's): algorithmic bytes / time per step
-            "cg_iteration": {"path": args.cg_path, "bytes_per_site": BYTES_PER_SITE_CG[args.cg_path],
-                             "achieved_GBps": round(BYTES_PER_SITE_CG[args.cg_path] * V * it_per_s / 1e9, 1),
-                             "reference_sequence_bytes_per_site": 576},
-        }
-        print(json.dumps(line), flush=True)
-    L.close()
+
+def true_relres(sh, m0):
+    """||phi - D D^dag x|| / ||phi|| over all shards (sm_dot_dev is global)."""
+    import numpy as np
+    import torch
+    sm = sh.sm
+    Ax = torch.empty_like(sh.phi)
+    sm.check(sm.lib.sm_ddag_dev(sh.L.ctx, sh.p(sh.x), sh.p(Ax), m0))
+    r = sh.phi - Ax
+    rr, pp = np.zeros(2), np.zeros(2)
+    sm.check(sm.lib.sm_dot_dev(sh.L.ctx, sh.p(r), sh.p(r), ctypes.c_void_p(rr.ctypes.data)))
+    sm.check(sm.lib.sm_dot_dev(sh.L.ctx, sh.p(sh.phi), sh.p(sh.phi), ctypes.c_void_p(pp.ctypes.data)))
+    return float(np.sqrt(rr[0] / pp[0]))
+
+
+def base_line(args, rt, cfg, Nx, Nt, sh):
+    world = rt["world"]
+    return {
+        "metric": "CG iterations/sec + Dirac-apply achieved HBM GB/s, 4096^2 fp64, 1/2/4/8 GPU",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "higher_is_better": True,
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": f"synthetic (counter-based U(1) field theta~N(0,{cfg['sigma']}^2) seed {SEED_U}, "
+                f"complex-Gaussian RHS seed {SEED_CHI})",
+        "config": {"workload": cfg["name"] + (f" [overridden: {Nx}x{Nt}]" if (Nx, Nt) != (cfg["Nx"], cfg["Nt"])
+                                                 else ""),
+                   "Nx": Nx, "Nt": Nt, "m0": cfg["m0"], "sigma": cfg["sigma"],
+                   "sites_per_gpu": sh.V, "shard": f"{Nx}x{sh.Wt}",
+                   "transport": args.transport if world > 1 else None,
+                   "parallelism": f"t-shard x{world}" + ((" (RCCL halos over xGMI)" if args.transport == "rccl"
+                                                          else " (host-staged halos)") if world > 1 else "")},
+    }
+
+
+def run_config34(args, rt, cfg_id):
+    import torch  # noqa: F401
+    cfg = CONFIGS[cfg_id]
+    Nx, Nt = args.nx or cfg["Nx"], args.nt or cfg["Nt"]
+    m0, world, rank = cfg["m0"], rt["world"], rt["rank"]
+    sh = Shard(rt, Nx, Nt, cfg["sigma"])
+    apply_s = time_applies(rt, sh, m0, args.applies)
+    t_cg = time_cg_steps(rt, sh, m0, args.cg_path, args.warmup, args.steps)
+    t_cg, apply_s = max_over_ranks(rt, [t_cg, apply_s])
+    V = sh.V
+    sh.close()
+    weak = None
+    if not args.no_weak:
+        # config 4's weak-scaling curve: 4096 x 512N sites, 4096 x 512 per GPU
+        wNt = (Nt // 8) * world
+        shw = Shard(rt, Nx, wNt, cfg["sigma"])
+        tw = time_cg_steps(rt, shw, m0, args.cg_path, args.warmup, args.steps)
+        (tw,) = max_over_ranks(rt, [tw])
+        weak = {"lattice": f"{Nx}x{wNt}", "sites_per_gpu": shw.V, "ms_per_step": round(1e3 * tw / args.steps, 4),
+                "value": round(args.steps / tw * world, 3),
+                "unit": f"CG iterations/s of a {Nx}x{Nt // 8}-site slab per GPU, whole job (it/s x N)",
+                "scaling": "weak"}
+        shw.close()
+    if rank != 0:
+        return
+    it_per_s = args.steps / t_cg
+    apply_GBps = BYTES_PER_SITE_APPLY * V / apply_s / 1e9
+    line = base_line(args, rt, cfg, Nx, Nt, sh)
+    line.update({
+        "value": round(it_per_s, 3),
+        "unit": f"CG iterations/s (one {Nx}x{Nt} lattice over all GPUs)",
+        "ms_per_step": round(1e3 * t_cg / args.steps, 4),
+        "scaling": "strong",
+    })
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(dict(cfg, Nx=Nx, Nt=Nt), args.cpu_threads or cpu_share(), args.cpu_iters)
+    tr = load_traffic(Nx, sh.Wt)
+    line.update({
+        "dirac_apply_GBps": round(apply_GBps, 1),
+        "dirac_apply_us": round(apply_s * 1e6, 2),
+        "roofline": {"bound": "hbm", "achieved": round(apply_GBps, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(apply_GBps / HBM_PEAK_GBPS, 4),
+                     "traffic": tr[1] if tr else None,
+                     "traffic_source": tr[0] if tr else None,
+                     "kernel": f"dslash_kernel<D>, {BYTES_PER_SITE_APPLY} B/site algorithmic x {V} sites per launch"},
+        "cpu_baseline": cpu,
+        # the CG iteration's own streaming rate (informational; the graded
+        # roofline is the Dirac apply's): algorithmic bytes / time per step
+        "cg_iteration": {"path": args.cg_path, "bytes_per_site": BYTES_PER_SITE_CG[args.cg_path],
+                         "achieved_GBps_per_gpu": round(BYTES_PER_SITE_CG[args.cg_path] * V * it_per_s / 1e9, 1),
+                         "reference_sequence_bytes_per_site": 576},
+        "weak": weak,
+    })
+    print(json.dumps(line), flush=True)
+
+
+def run_config5(args, rt):
+    cfg = CONFIGS[5]
+    Nx, Nt = args.nx or cfg["Nx"], args.nt or cfg["Nt"]
+    m0, world, rank = cfg["m0"], rt["world"], rt["rank"]
+    sm = None
+    sh = Shard(rt, Nx, Nt, cfg["sigma"])
+    sm = sh.sm
+    sm.check(sm.lib.sm_tune_cg(sh.L.ctx, CG_PATH_ID[args.cg_path], 0))
+    tol = 1e-10
+    # warm the kernels once on a short solve, then the timed solve from x0 = phi
+    res = sm.CGResult()
+    sm.check(sm.lib.sm_cg_dev(sh.L.ctx, sh.p(sh.phi), sh.p(sh.x), m0, tol, 5, ctypes.byref(res)))
+    barrier(rt)
+    t = time.perf_counter()
+    sm.check(sm.lib.sm_cg_dev(sh.L.ctx, sh.p(sh.phi), sh.p(sh.x), m0, tol, 100000, ctypes.byref(res)))
+    barrier(rt)
+    dt = time.perf_counter() - t
+    (dt,) = max_over_ranks(rt, [dt])
+    rel = true_relres(sh, m0)
+    V = sh.V
+    line = base_line(args, rt, cfg, Nx, Nt, sh)
+    sh.close()
+    if rank != 0:
+        return
+    line.update({
+        "value": round(res.iterations / dt, 3),
+        "unit": f"CG iterations/s (one {Nx}x{Nt} lattice over all GPUs, solve to tol 1e-10)",
+        "ms_per_step": round(1e3 * dt / max(1, res.iterations), 4),
+        "steps": res.iterations, "warmup": 0,
+        "scaling": "strong",
+        "time_to_solution_s": round(dt, 4),
+        "iterations": res.iterations, "converged": res.converged,
+        "cg_residual_rel": res.residual / res.phi_norm if res.phi_norm else None,
+        "true_relres": rel,
+        "cg_iteration": {"path": args.cg_path, "bytes_per_site": BYTES_PER_SITE_CG[args.cg_path],
+                         "achieved_GBps_per_gpu": round(BYTES_PER_SITE_CG[args.cg_path] * V * res.iterations
+                                                        / dt / 1e9, 1)},
+    })
+    print(json.dumps(line), flush=True)
+    if not res.converged or not rel < 1e-9:
+        raise SystemExit(f"config 5: converged={res.converged} true relres {rel:.3e}")
+
+
+def main():
+    args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus is None:
+        args.gpus = int(env_world) if env_world else 1
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: refusing to measure the wrong job")
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    cfg_id = args.config or (3 if world == 1 else 4)
+    if cfg_id == 3 and world > 1:
+        cfg_id = 4
+
+    import torch
+    import torch.distributed as dist
+    ndev = torch.cuda.device_count()  # does not initialise the GPU on this image
+    if args.device is not None:
+        device = args.device
+    elif args.transport == "hosted":
+        device = local_rank % max(1, ndev)
+    else:
+        if world > 1 and ndev < int(os.environ.get("LOCAL_WORLD_SIZE", world)):
+            raise SystemExit(f"{world} RCCL ranks need one GPU each, {ndev} visible (use --transport hosted)")
+        device = local_rank
     if world > 1:
-        dist.destroy_process_group()
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(device)
+    # a real (non-null) torch stream: the library launches on it, so the torch
+    # events bracket exactly the kernels being timed
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    rt = {"world": world, "rank": rank, "device": device, "stream": stream, "transport": args.transport}
+    try:
+        if cfg_id == 5:
+            run_config5(args, rt)
+        else:
+            run_config34(args, rt, cfg_id)
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
 
 
 if __name__ == "__main__":

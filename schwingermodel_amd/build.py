@@ -42,8 +42,29 @@ def build_library(force=False, verbose=True):
         return LIB
     if not os.path.exists(HIPCC):
         raise RuntimeError(f"hipcc not found at {HIPCC}")
+    # one hipcc per translation unit, in parallel (objects under build/, git-ignored),
+    # then one link; a source whose object is newer than it and every header is reused
+    objdir = os.path.join(REPO, "build", "sm_hip")
+    os.makedirs(objdir, exist_ok=True)
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(REPO, "include", "sm_hip.h")]
+    jobs = []
+    for s in SOURCES:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(objdir, s + ".o")
+        if force or _stale(obj, [src] + hdrs):
+            jobs.append([HIPCC] + CFLAGS + ["-c", src, "-o", obj])
+    from concurrent.futures import ThreadPoolExecutor
+    nproc = min(len(jobs) or 1, int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16)
+    with ThreadPoolExecutor(nproc) as ex:
+        procs = list(ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), jobs))
+    for c, p in zip(jobs, procs):
+        if verbose or p.returncode:
+            print(" ".join(c), file=sys.stderr)
+            sys.stderr.write(p.stderr)
+        if p.returncode:
+            raise subprocess.CalledProcessError(p.returncode, c)
     tmp = LIB + ".tmp"
-    cmd = [HIPCC] + CFLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", tmp] + LDFLAGS
+    cmd = [HIPCC, f"--offload-arch={ARCH}"] + [os.path.join(objdir, s + ".o") for s in SOURCES] + ["-o", tmp] + LDFLAGS
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
