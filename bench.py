@@ -32,6 +32,7 @@ import argparse
 import ctypes
 import json
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -208,7 +209,9 @@ def load_traffic(nx, nt):
     best = None
     pdir = os.path.join(REPO, "profiles")
     if os.path.isdir(pdir):
-        for f in sorted(os.listdir(pdir)):
+        def natural(f):
+            return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", f)]
+        for f in sorted(os.listdir(pdir), key=natural):
             if f.endswith("_dslash_pmc.json"):
                 try:
                     with open(os.path.join(pdir, f)) as fh:

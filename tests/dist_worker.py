@@ -272,15 +272,149 @@ def run_eo(name, result_path, dist, rank, world):
     dist.destroy_process_group()
 
 
+def fill_block(sm, Nx, Nt, t0, Wt, sigma, seeds=(4321, 5678, 91011), nthreads=8):
+    """U, psi, chi of the t-block [t0, t0+Wt) of the global synthetic fields
+    (counter-based, row-separable: row blocks are filled in threads)."""
+    from concurrent.futures import ThreadPoolExecutor
+    V = Nx * Wt
+    f = {k: np.empty(4 * V) for k in ("U", "psi", "chi")}
+    rows = max(1, -(-Nx // nthreads))
+
+    def job(x0):
+        nx = min(rows, Nx - x0)
+        o = 2 * x0 * Wt
+        sm.lib.sm_fill_gauge(seeds[0], sigma, Nt, x0, nx, t0, Wt, f["U"][o:].ctypes.data, f["U"][2 * V + o:].ctypes.data)
+        for k, s in (("psi", seeds[1]), ("chi", seeds[2])):
+            sm.lib.sm_fill_spinor(s, Nt, x0, nx, t0, Wt, f[k][o:].ctypes.data, f[k][2 * V + o:].ctypes.data)
+    with ThreadPoolExecutor(nthreads) as ex:
+        list(ex.map(job, range(0, Nx, rows)))
+    return f
+
+
+def big_ops(sm, ctx, V, f, m0, ops):
+    """The operators on one context (host pointers, reference layout): D psi,
+    D^dag chi, force(psi, chi) (ops 'full'), the CG solve of D D^dag x = psi and
+    its true residual terms |psi - D D^dag x|^2, |psi|^2 (local sums)."""
+    P = lambda x: ctypes.c_void_p(x.ctypes.data)  # noqa: E731
+    out = {}
+    if ops == "full":
+        for key, src, dag in (("Dpsi", "psi", 0), ("Ddagchi", "chi", 1)):
+            o = np.empty(4 * V)
+            sm.check(sm.lib.sm_dirac(ctx, P(f[src]), P(f[src][2 * V:]), P(o), P(o[2 * V:]), m0, dag))
+            out[key] = o
+        F = np.empty(2 * V)
+        sm.check(sm.lib.sm_force(ctx, P(f["psi"]), P(f["psi"][2 * V:]), P(f["chi"]), P(f["chi"][2 * V:]),
+                                 P(F), P(F[V:])))
+        out["force"] = F
+    x = np.empty(4 * V)
+    res = sm.CGResult()
+    sm.check(sm.lib.sm_cg(ctx, P(f["psi"]), P(f["psi"][2 * V:]), P(x), P(x[2 * V:]), m0, 1e-10, 20000,
+                          ctypes.byref(res)))
+    out["x"] = x
+    out["cg"] = (int(res.converged), int(res.iterations))
+    Ax = np.empty(4 * V)
+    sm.check(sm.lib.sm_ddag(ctx, P(x), P(x[2 * V:]), P(Ax), P(Ax[2 * V:]), m0))
+    r = f["psi"] - Ax
+    out["res_sq"] = (float(r @ r), float(f["psi"] @ f["psi"]))
+    return out
+
+
+def block_of(a, Nx, Nt, t0, Wt, planes_complex=True):
+    """Columns [t0, t0+Wt) of a global two-plane field (complex planes of Nx*Nt,
+    or real planes for the force), as this shard's flat layout."""
+    S = Nx * Nt
+    if planes_complex:
+        return np.concatenate([np.ascontiguousarray(a[2 * S * p:2 * S * (p + 1)].view(np.complex128)
+                                                    .reshape(Nx, Nt)[:, t0:t0 + Wt]).reshape(-1).view(np.float64)
+                               for p in range(2)])
+    return np.concatenate([np.ascontiguousarray(a[S * p:S * (p + 1)].reshape(Nx, Nt)[:, t0:t0 + Wt]).reshape(-1)
+                           for p in range(2)])
+
+
+def run_big(name, result_path, dist, rank, world):
+    """mode "big": BASELINE configs at their real shard shapes on ONE GPU.
+    name = big:<Nx>x<Nt>:<sigma>:<m0>:<ops>, ops 'full' (D, D^dag, force, CG)
+    or 'cg'. Rank 0 first runs the one-shard reference on the GPU and stores
+    its outputs as .npy next to the result file; then every rank runs its
+    t-shard (hosted transport) and compares its own block: D / D^dag / force
+    bitwise, CG iterations, |x - x_one| and the true residual summed over ranks.
+    No rank ever holds the whole sharded result."""
+    import time
+    import schwingermodel_amd as sm
+    from schwingermodel_amd import dist as smd
+    import torch
+    _, dims, sigma, m0s, ops = name.split(":")
+    Nx, Nt = (int(v) for v in dims.split("x"))
+    sigma, m0 = float(sigma), float(m0s)
+    S = Nx * Nt
+    d = os.path.dirname(result_path)
+    dev = int(os.environ.get("SM_DEVICE", "0"))
+    if rank == 0:
+        t = time.time()
+        g = fill_block(sm, Nx, Nt, 0, Nt, sigma)
+        L = sm.Lattice(Nx, Nt, device=dev)
+        sm.check(sm.lib.sm_upload_gauge(L.ctx, ctypes.c_void_p(g["U"].ctypes.data),
+                                        ctypes.c_void_p(g["U"][2 * S:].ctypes.data)))
+        one = big_ops(sm, L.ctx, S, g, m0, ops)
+        L.close()
+        del g
+        for k in ("Dpsi", "Ddagchi", "force", "x"):
+            if k in one:
+                np.save(os.path.join(d, f"one_{k}.npy"), one.pop(k))
+        with open(os.path.join(d, "one.json"), "w") as fh:
+            json.dump({"cg": one["cg"], "res_sq": one["res_sq"], "seconds": time.time() - t}, fh)
+        del one
+    dist.barrier()
+    t0, Wt = ctypes.c_int(), ctypes.c_int()
+    sm.check(sm.lib.sm_shard_plan(Nt, world, rank, ctypes.byref(t0), ctypes.byref(Wt)))
+    t0, Wt = t0.value, Wt.value
+    V = Nx * Wt
+    f = fill_block(sm, Nx, Nt, t0, Wt, sigma, nthreads=2)
+    ctx, tr = smd.create_hosted_context(Nx, Nt, device=dev)
+    sm.check(sm.lib.sm_upload_gauge(ctx, ctypes.c_void_p(f["U"].ctypes.data),
+                                    ctypes.c_void_p(f["U"][2 * V:].ctypes.data)))
+    ts = time.time()
+    mine = big_ops(sm, ctx, V, f, m0, ops)
+    ts = time.time() - ts
+    sm.lib.sm_destroy(ctx)
+    local = {"cg": mine["cg"], "bitwise": {}}
+    for k in ("Dpsi", "Ddagchi", "force"):
+        if k in mine:
+            ref = np.load(os.path.join(d, f"one_{k}.npy"), mmap_mode="r")
+            local["bitwise"][k] = bool(np.array_equal(block_of(ref, Nx, Nt, t0, Wt, k != "force").view(np.uint64),
+                                                      mine[k].view(np.uint64)))
+    xr = block_of(np.load(os.path.join(d, "one_x.npy"), mmap_mode="r"), Nx, Nt, t0, Wt)
+    dx = mine["x"] - xr
+    sums = torch.tensor([float(dx @ dx), float(xr @ xr), mine["res_sq"][0], mine["res_sq"][1]], dtype=torch.float64)
+    dist.all_reduce(sums)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, local)
+    if rank == 0:
+        with open(os.path.join(d, "one.json")) as fh:
+            one = json.load(fh)
+        rep = {"world": world, "Wt": Wt, "one_cg": one["cg"], "one_relres": (one["res_sq"][0] / one["res_sq"][1]) ** 0.5,
+               "cg": [g["cg"] for g in gathered],
+               "bitwise": {k: all(g["bitwise"][k] for g in gathered) for k in gathered[0]["bitwise"]},
+               "x_rel": float((sums[0] / sums[1]) ** 0.5), "relres": float((sums[2] / sums[3]) ** 0.5),
+               "seconds_one": one["seconds"], "seconds_sharded": ts}
+        with open(result_path, "w") as fh:
+            json.dump(rep, fh)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     mode, name, result_path = sys.argv[1], sys.argv[2], sys.argv[3]
+    import datetime
     import torch.distributed as dist
-    dist.init_process_group("gloo")
+    dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=20))
     rank, world = dist.get_rank(), dist.get_world_size()
     if mode == "md":
         return run_md(name, result_path, dist, rank, world)
     if mode == "eo":
         return run_eo(name, result_path, dist, rank, world)
+    if mode == "big":
+        return run_big(name, result_path, dist, rank, world)
     from conftest import bits_equal, load_fixture
     import schwingermodel_amd as sm
     from schwingermodel_amd import dist as smd
