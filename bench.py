@@ -45,8 +45,8 @@ SEED_U, SEED_CHI = 4321, 91011
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_SITE_APPLY = 96  # read psi 32 + U 32, write 32
 # algorithmic HBM bytes per site of one CG iteration, by path
-BYTES_PER_SITE_CG = {"recompute": 160, "twodir": 224, "onepass": 288, "fused": 320, "sixkernel": 576}
-CG_PATH_ID = {"recompute": 5, "twodir": 4, "onepass": 3, "fused": 1, "sixkernel": 0}
+BYTES_PER_SITE_CG = {"recompute": 160, "twodir": 224, "sixkernel": 576}
+CG_PATH_ID = {"recompute": 5, "twodir": 4, "sixkernel": 0}
 
 # BASELINE.json configs on the GPU (1 and 2 are the CPU-plumbing / 1024^2 parity cases)
 CONFIGS = {
@@ -330,7 +330,7 @@ def time_cg_steps(rt, sh, m0, cg_path, warmup, steps):
     sm.check(sm.lib.sm_cg_status(sh.L.ctx, ctypes.byref(res)))
     # the one-pass iterations' pass 0 (in the warmup) only forms Ad_0: every
     # later pass is one full reference iteration
-    setup_passes = 1 if cg_path in ("onepass", "twodir", "recompute") else 0
+    setup_passes = 1 if cg_path in ("twodir", "recompute") else 0
     if res.iterations != warmup + steps - setup_passes or res.converged != 0:
         raise SystemExit(f"CG ran {res.iterations} iterations (converged={res.converged}), "
                          f"expected {warmup + steps - setup_passes}")

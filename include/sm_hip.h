@@ -103,6 +103,12 @@ typedef struct {
 } sm_host_transport;
 int sm_create_hosted(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device,
                      const sm_host_transport *transport);
+/* RCCL loopback: ONE shard (the whole lattice) driven through the t-shard code
+ * path -- faces packed and exchanged with ncclSend/ncclRecv to itself, scalar
+ * sums through ncclAllReduce -- over a one-rank communicator built from
+ * unique_id (sm_comm_unique_id). The results equal sm_create's one-shard
+ * context; it exists so the RCCL data path can be verified on a single GPU. */
+int sm_create_loopback(sm_ctx **out, int Nx, int Nt_global, int device, const void *unique_id);
 int sm_destroy(sm_ctx *ctx);
 /* Launch on a caller stream (a hipStream_t, e.g. torch's current stream);
  * NULL restores the context's own stream. */
@@ -121,13 +127,10 @@ int sm_tune(sm_ctx *ctx, int bt, int xchunk, int xcd_remap, int variant);
  * two-direction one-pass iteration that stores Ad:
  * no r vector (r_{j-1} = d_{j-1} - beta_{j-2} d_{j-2} is rebuilt from the two
  * stored directions) and x updated on even passes only, 224 B/site.
- * fused = 3 runs an iteration in ONE HBM pass with an r vector: the
- * residual update r -= alpha Ad is folded into the next pass, beta comes from
- * that pass's direct dots (sm_cgfused.hip), 288 B/site. 1 runs two passes each followed
- * by a one-block scalar kernel (alpha, beta), 2 the same two passes with
- * alpha and beta reduced in-kernel by the last block of each pass (one shard
- * only), 0 the six-kernel
- * sequence; xchunk = rows per block of the active fused kernel. < 0 / <= 0 keep. */
+ * fused = 0 is the reference's six-launch sequence (576 B/site). Other
+ * values return SM_ERR_ARG (the two-pass and r-vector iterations of round 1
+ * were dominated at every size and removed). xchunk = rows per block of the
+ * active one-pass kernel. < 0 / <= 0 keep. */
 int sm_tune_cg(sm_ctx *ctx, int fused, int xchunk);
 /* Streaming-bandwidth ceiling on the ctx stream (measured roofline reference):
  * out = a + b (two_reads = 1: the stencil's 2-read/1-write byte mix) or

@@ -19,6 +19,11 @@
 //   bench <ranks_x> <ranks_t> <seed_U> <sigma> <seed_psi> <m0> <napply> <ncg>
 //       generates the synthetic fields per rank (sm_fields.h), times napply
 //       D_phi applies and ncg CG iterations (tol = 0), prints one JSON line.
+//   conf <dir> <ranks_x> <ranks_t>
+//       reads U.bin, stores it with the reference's SaveConf into
+//       <dir>/ref_conf.ctxt (src/gauge_conf.cpp:378-423: MPI_Gatherv to rank 0,
+//       28-byte records), reads that file back with GaugeConf::readBinary
+//       (:495-546, MPI_Scatterv) and writes the field it read as ref_conf_read.bin.
 //   md <dir> <ranks_x> <ranks_t> <m0> <beta> <tau> <md_steps> <tol> <max_iter>
 //       reads U.bin, chi.bin and P.bin (momenta: two real planes) and runs the
 //       reference's gauge / molecular-dynamics code on them: plaquette field,
@@ -237,6 +242,20 @@ static int run_md(const std::string &dir, double m0, double beta, double tau, in
     return 0;
 }
 
+static int run_conf(const std::string &dir) {
+    GaugeConf G;
+    if (!read_block(dir + "/U.bin", G.Conf)) {
+        if (mpi::rank == 0) fprintf(stderr, "cannot read U in %s\n", dir.c_str());
+        return 1;
+    }
+    SaveConf(G, dir + "/ref_conf.ctxt");
+    MPI_Barrier(MPI_COMM_WORLD);
+    GaugeConf H;
+    H.readBinary(dir + "/ref_conf.ctxt");
+    write_spinor(dir + "/ref_conf_read.bin", H.Conf);
+    return 0;
+}
+
 static int run_bench(unsigned long long seedU, double sigma, unsigned long long seedP, double m0,
                      int napply, int ncg) {
     spinor U(mpi::maxSize), psi(mpi::maxSize), out(mpi::maxSize), x(mpi::maxSize);
@@ -320,12 +339,15 @@ int main(int argc, char **argv) {
         setup(atoi(argv[3]), atoi(argv[4]));
         rc = run_md(argv[2], atof(argv[5]), atof(argv[6]), atof(argv[7]), atoi(argv[8]), atof(argv[9]),
                     atoi(argv[10]));
+    } else if (argc >= 5 && !strcmp(argv[1], "conf")) {
+        setup(atoi(argv[3]), atoi(argv[4]));
+        rc = run_conf(argv[2]);
     } else if (argc >= 10 && !strcmp(argv[1], "bench")) {
         setup(atoi(argv[2]), atoi(argv[3]));
         rc = run_bench(strtoull(argv[4], 0, 10), atof(argv[5]), strtoull(argv[6], 0, 10),
                        atof(argv[7]), atoi(argv[8]), atoi(argv[9]));
     } else {
-        fprintf(stderr, "usage: gen <dir> seedU sigma seedP seedC | fixture <dir> rx rt m0 tol max_iter | bench rx rt seedU sigma seedP m0 napply ncg | md <dir> rx rt m0 beta tau md_steps tol max_iter\n");
+        fprintf(stderr, "usage: gen <dir> seedU sigma seedP seedC | fixture <dir> rx rt m0 tol max_iter | bench rx rt seedU sigma seedP m0 napply ncg | md <dir> rx rt m0 beta tau md_steps tol max_iter | conf <dir> rx rt\n");
     }
     MPI_Finalize();
     return rc;

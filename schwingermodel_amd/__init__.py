@@ -81,7 +81,7 @@ class re_field:
 class Lattice:
     """One t-shard of an Nx x Nt lattice on one GPU (owns an sm_ctx)."""
 
-    def __init__(self, Nx, Nt, nshard=1, shard=0, device=0, unique_id=None):
+    def __init__(self, Nx, Nt, nshard=1, shard=0, device=0, unique_id=None, loopback=False):
         self.Nx, self.Nt, self.nshard, self.shard, self.device = Nx, Nt, nshard, shard, device
         t0, Wt = ctypes.c_int(), ctypes.c_int()
         check(lib.sm_shard_plan(Nt, nshard, shard, ctypes.byref(t0), ctypes.byref(Wt)))
@@ -91,7 +91,15 @@ class Lattice:
         uid = None
         if unique_id is not None:
             uid = ctypes.create_string_buffer(bytes(unique_id), len(unique_id))
-        check(lib.sm_create(ctypes.byref(h), Nx, Nt, nshard, shard, device, uid))
+        if loopback:  # one shard through the t-shard path over a one-rank RCCL communicator
+            if nshard != 1:
+                raise ValueError("loopback is one shard")
+            if uid is None:
+                uid = ctypes.create_string_buffer(128)
+                check(lib.sm_comm_unique_id(uid, 128))
+            check(lib.sm_create_loopback(ctypes.byref(h), Nx, Nt, device, uid))
+        else:
+            check(lib.sm_create(ctypes.byref(h), Nx, Nt, nshard, shard, device, uid))
         self.ctx = h
         self.last_cg = CGResult()
 
@@ -121,12 +129,13 @@ class Lattice:
 _LATTICE = None
 
 
-def init(Nx, Nt, nshard=1, shard=0, device=0, unique_id=None):
-    """Set the lattice geometry (the reference's NS/NT + mpi:: setup)."""
+def init(Nx, Nt, nshard=1, shard=0, device=0, unique_id=None, loopback=False):
+    """Set the lattice geometry (the reference's NS/NT + mpi:: setup).
+    loopback=True: one shard driven through the multi-GPU (RCCL) code path."""
     global _LATTICE
     if _LATTICE is not None:
         _LATTICE.close()
-    _LATTICE = Lattice(Nx, Nt, nshard, shard, device, unique_id)
+    _LATTICE = Lattice(Nx, Nt, nshard, shard, device, unique_id, loopback)
     return _LATTICE
 
 

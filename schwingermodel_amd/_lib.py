@@ -64,6 +64,7 @@ def _load():
         "sm_device_count": ([ctypes.POINTER(ci)], ci),
         "sm_create": ([ctypes.POINTER(vp), ci, ci, ci, ci, ci, vp], ci),
         "sm_create_hosted": ([ctypes.POINTER(vp), ci, ci, ci, ci, ci, vp], ci),
+        "sm_create_loopback": ([ctypes.POINTER(vp), ci, ci, ci, vp], ci),
         "sm_destroy": ([vp], ci),
         "sm_set_stream": ([vp, vp], ci),
         "sm_synchronize": ([vp], ci),

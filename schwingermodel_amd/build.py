@@ -1,6 +1,6 @@
 """In-tree build of libsm_hip.so for gfx950 (hipcc; no JIT cache, no pip install).
 
-    python -m schwingermodel_amd.build          # library only
+    python schwingermodel_amd/build.py          # library + sm_hmc (not -m: the package import loads the old .so)
 The .so lands next to this file, so it travels with the repo snapshot to the
 GPU box and is the one the tests / bench / smoke load.
 """

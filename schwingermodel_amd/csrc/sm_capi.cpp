@@ -40,7 +40,7 @@ int fail(int code, const char *fmt, ...) {
 // Neighbour sources for `in`: periodic aliases (1 GPU) or received faces.
 TFaces faces_for(sm_ctx *c, const double2 *in, const double2 *recv_lo, const double2 *recv_hi) {
     TFaces f;
-    if (c->nshard == 1) {
+    if (!c->sharded()) {
         f.lo = in + (c->g.Wt - 1);
         f.lo_xs = c->g.Wt;
         f.lo_ps = c->g.V;
@@ -101,7 +101,7 @@ int exchange_faces(sm_ctx *c, double2 *slo, double2 *shi, double2 *rlo, double2 
 
 // In-place global sum of n doubles resident on the device.
 int allreduce_dev(sm_ctx *c, double *dev, int n) {
-    if (c->nshard == 1) return SM_OK;
+    if (!c->sharded()) return SM_OK;
     if (c->hosted) {
         HIP_TRY(hipMemcpyAsync(c->h_red, dev, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
@@ -116,7 +116,7 @@ int allreduce_dev(sm_ctx *c, double *dev, int n) {
 }
 
 int halo(sm_ctx *c, const double2 *field, int set, TFaces *f) {
-    if (c->nshard == 1) {
+    if (!c->sharded()) {
         *f = faces_for(c, field, nullptr, nullptr);
         return SM_OK;
     }
@@ -128,13 +128,13 @@ int halo(sm_ctx *c, const double2 *field, int set, TFaces *f) {
     return SM_OK;
 }
 
-const double2 *loU(sm_ctx *c) { return c->nshard == 1 ? c->U + (c->g.Wt - 1) : c->ghostU; }
+const double2 *loU(sm_ctx *c) { return !c->sharded() ? c->U + (c->g.Wt - 1) : c->ghostU; }
 
 int apply(sm_ctx *c, const double2 *in, double2 *out, double mass, int dagger, const double2 *aux,
           double2 *partials, const CGScalars *skip) {
     TFaces f;
     const int TB = (c->g.Wt + c->cfg.bt - 1) / c->cfg.bt;
-    const bool one = c->nshard == 1;
+    const bool one = !c->sharded();
     if (TB < 3 || (one && !c->split_test)) {
         TRY(halo(c, in, 0, &f));
         launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip);
@@ -209,7 +209,7 @@ double2 *face2_send(sm_ctx *c, int f, int hi) {  // send buffers of field slot f
 // Pack and exchange the 2-deep faces of nf (<= 2) fields in ONE transport
 // round on stream s (RCCL: a single group of 4*nf p2p ops).
 int halo2_multi(sm_ctx *c, hipStream_t s, const double2 *const *fields, double2 *const *faces, int nf) {
-    if (c->nshard == 1) return SM_OK;
+    if (!c->sharded()) return SM_OK;
     const size_t cnt = (size_t)8 * c->g.Nx;  // doubles: 2 columns x 2 planes x Nx complex
     for (int f = 0; f < nf; ++f) launch_pack_faces2(s, c->g, fields[f], face2_send(c, f, 0), face2_send(c, f, 1));
     if (c->hosted) {
@@ -242,7 +242,7 @@ int halo2(sm_ctx *c, const double2 *field, double2 *face) {
 static double2 *face4_send(sm_ctx *c, int hi) { return c->faces4 + (size_t)(8 * hi) * c->g.Nx; }
 static double2 *face4_recv_d(sm_ctx *c, long pass) { return c->faces4 + (size_t)(16 + 16 * (pass & 1)) * c->g.Nx; }
 double2 *face4_recv_U(sm_ctx *c) { return c->faces4 + (size_t)48 * c->g.Nx; }
-bool cg_ra_ok(const sm_ctx *c) { return c->nshard == 1 || c->g.Wt >= 4; }
+bool cg_ra_ok(const sm_ctx *c) { return !c->sharded() || c->g.Wt >= 4; }
 
 // Pack and exchange the 4-deep t-faces of `field` into `recv` on stream s.
 static int halo4(sm_ctx *c, hipStream_t s, const double2 *field, double2 *recv) {
@@ -252,7 +252,7 @@ static int halo4(sm_ctx *c, hipStream_t s, const double2 *field, double2 *recv) 
 }
 
 int exchange_ghost_U(sm_ctx *c) {
-    if (c->nshard == 1) return SM_OK;
+    if (!c->sharded()) return SM_OK;
     // U_t(x, Wt-1) (plane 0 of my hi face) is the up-neighbour's U_t(x, -1)
     double2 *slo = face_buf(c, 1, 0), *shi = face_buf(c, 1, 1);
     double2 *rlo = face_buf(c, 1, 2), *rhi = face_buf(c, 1, 3);
@@ -268,7 +268,7 @@ int exchange_ghost_U(sm_ctx *c) {
 
 // alpha / beta from per-block partials (local sum, all-reduce over shards, scalar)
 int cg_scalar(sm_ctx *c, int nparts, int which) {
-    if (c->nshard == 1) {
+    if (!c->sharded()) {
         if (which == 0) launch_cg_alpha(c->stream, nparts, c->partials, c->sc);
         else launch_cg_beta(c->stream, nparts, c->partials, c->sc);
         return SM_OK;
@@ -371,7 +371,7 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 }
 
 static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device,
-                         const void *unique_id, const sm_host_transport *tr) {
+                         const void *unique_id, const sm_host_transport *tr, bool loop = false) {
     if (!out) return fail(SM_ERR_ARG, "null out");
     *out = nullptr;
     int t0, Wt;
@@ -385,6 +385,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     HIP_TRY(hipSetDevice(device));
     sm_ctx *c = new sm_ctx();
     c->device = device;
+    c->loop = loop;
     c->nshard = nshard;
     c->shard = shard;
     c->g.Nx = Nx;
@@ -405,12 +406,12 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     if (const char *e = getenv("SM_CG_FUSED")) c->cg_fused = atoi(e);
     if (const char *e = getenv("SM_EDGE_CONCURRENT")) c->edge_concurrent = atoi(e);
     if (const char *e = getenv("SM_SPLIT_TEST")) c->split_test = atoi(e);
-    if (const char *e = getenv("SM_CG_INKERNEL_MAX_BLOCKS")) c->cg_inkernel_max_blocks = atoi(e);
     if (const char *e = getenv("SM_CGRA_RED_MAX_BLOCKS")) c->cg_ra_red_max_blocks = atoi(e);
     if (const char *e = getenv("SM_CG_REDUNDANT")) c->cg_redundant = atoi(e);
     if (const char *e = getenv("SM_EO_FUSED")) c->eo_fused = atoi(e);
     if (const char *e = getenv("SM_EO_CG_FOLDED")) c->eo_cg_folded = atoi(e);
     if (const char *e = getenv("SM_EO_CG_TD")) c->eo_cg_td = atoi(e);
+    if (const char *e = getenv("SM_DEBUG_CG")) c->debug_cg = atoi(e);
     const int np = kMaxPartials;
     const size_t fb = sizeof(double2) * 2 * (size_t)c->g.V;
     hipError_t e = hipSuccess;
@@ -430,13 +431,11 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     chk(hipMalloc(&c->sums, sizeof(double2) * 4));
     chk(hipMalloc(&c->Fbuf, sizeof(double) * 2 * (size_t)c->g.V));
     chk(hipMalloc(&c->sc, sizeof(CGScalars)));
-    chk(hipMalloc(&c->counters, 256));  // two tickets on separate 128-B lines: [0], [32]
     chk(hipHostMalloc(&c->h_sc, sizeof(CGScalars)));
     chk(hipHostMalloc(&c->h_sums, sizeof(double2) * 4));
     chk(hipHostMalloc(&c->h_face, sizeof(double) * 4 * kMaxFaceDoubles * (size_t)Nx));
     chk(hipHostMalloc(&c->h_red, sizeof(double) * 8));
     if (e == hipSuccess) chk(hipMemset(c->sc, 0, sizeof(CGScalars)));
-    if (e == hipSuccess) chk(hipMemset(c->counters, 0, 256));
     if (e != hipSuccess) {
         sm_destroy(c);
         return fail(SM_ERR_HIP, "allocation failed: %s", hipGetErrorString(e));
@@ -444,7 +443,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     if (nshard > 1 && tr) {
         c->hosted = true;
         c->tr = *tr;
-    } else if (nshard > 1) {
+    } else if (c->sharded()) {
         ncclUniqueId id;
         memcpy(&id, unique_id, sizeof id);
         ncclResult_t r = ncclCommInitRank(&c->comm, nshard, id, shard);
@@ -463,6 +462,11 @@ int sm_create(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int de
     return create_common(out, Nx, Nt_global, nshard, shard, device, unique_id, nullptr);
 }
 
+int sm_create_loopback(sm_ctx **out, int Nx, int Nt_global, int device, const void *unique_id) {
+    if (!unique_id) return fail(SM_ERR_ARG, "loopback needs an RCCL unique id (sm_comm_unique_id)");
+    return create_common(out, Nx, Nt_global, 1, 0, device, unique_id, nullptr, true);
+}
+
 int sm_create_hosted(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device,
                      const sm_host_transport *transport) {
     if (!transport) return fail(SM_ERR_ARG, "null transport");
@@ -475,7 +479,7 @@ int sm_destroy(sm_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
     void *dev[] = {c->U, c->ghostU, c->fields, c->faces, c->faces2, c->faces4, c->partials, c->sums, c->Fbuf, c->sc,
-                   c->counters, c->U_alt, c->Pmd, c->Fmd, c->eo, c->Ucb, c->eo_faces, c->eo_faces4};
+                   c->U_alt, c->Pmd, c->Fmd, c->eo, c->Ucb, c->eo_faces, c->eo_faces4};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_sc) (void)hipHostFree(c->h_sc);
@@ -493,11 +497,9 @@ int sm_destroy(sm_ctx *c) {
 
 int sm_tune_cg(sm_ctx *c, int fused, int xchunk) {
     if (!c) return fail(SM_ERR_ARG, "null context");
-    if (fused > 5) return fail(SM_ERR_ARG, "fused must be 0 .. 5");
-    if (fused >= 0) {
-        c->cg_fused = fused >= 3 ? fused : (fused != 0);
-        c->cg_inkernel = fused == 2;
-    }
+    if (fused > 5 || (fused >= 1 && fused <= 3))
+        return fail(SM_ERR_ARG, "CG path must be 0 (reference sequence), 4 (stored Ad) or 5 (recompute Ad)");
+    if (fused >= 0) c->cg_fused = fused;
     if (xchunk > 0) {
         CGFusedCfg &cur = c->cg_fused == 5 ? c->racfg : c->fcfg;  // the active pass's geometry
         CGFusedCfg f = cur;
@@ -621,7 +623,7 @@ int sm_cg_begin(sm_ctx *c, const double *phi, double *x, double m0, double tol) 
     TRY(apply(c, t, Ad, c->cg_mass, 0, nullptr, nullptr, nullptr));
     double2 *prr = c->partials, *ppp = c->partials + c->nparts_red;
     launch_cg_init(c->stream, n, ph, Ad, r, d, prr, ppp);                        // r = phi - Ax; d = r
-    if (c->nshard == 1) {
+    if (!c->sharded()) {
         launch_cg_finalize_init(c->stream, c->nparts_red, prr, ppp, c->sc, tol);
     } else {
         launch_sum_partials(c->stream, c->nparts_red, prr, c->sums);
@@ -638,16 +640,13 @@ int sm_cg_begin(sm_ctx *c, const double *phi, double *x, double m0, double tol) 
 }
 
 
-// One pass of the one-pass CG (sm_cgfused.hip: cg_onepass_kernel): pass j
-// reads the j-1 fields (d, r, Ad), writes the j fields into the other
-// buffers, updates x in place, then the scalar kernel forms err / stop,
-// alpha_j and beta_j.
-//
-// Two-direction form (cg_fused == 4): no r vector. d rotates through three
-// buffers (pass j reads d_{j-1} and d_{j-2}, writes d_j); the `rold` operand
-// is d_{j-2}, and x is updated on even passes only, so after an odd final
-// pass sm_cg_finish adds the pending alpha_{j-1} d_{j-1}.
-static double2 *cg_dbuf(sm_ctx *c, long i) {  // d_i of the two-direction form (d_0 from cg_init in F_D)
+// One pass of the two-direction CG with a stored Ad (cg_fused == 4,
+// sm_cgfused.hip: cg_onepass_kernel): pass j reads d_{j-1}, d_{j-2} and
+// Ad_{j-1}, writes d_j and Ad_j, updates x on even passes (so after an odd
+// final pass sm_cg_finish adds the pending alpha_{j-1} d_{j-1}), then the
+// scalar kernel forms err / stop, alpha_j and beta_j. d rotates through three
+// buffers (cg_dbuf), Ad ping-pongs.
+static double2 *cg_dbuf(sm_ctx *c, long i) {  // d_i (d_0 from cg_init in F_D)
     static const int slot[3] = {F_D2, F_R, F_D};
     return c->field(slot[((i % 3) + 3) % 3]);
 }
@@ -655,43 +654,33 @@ static double2 *cg_dbuf(sm_ctx *c, long i) {  // d_i of the two-direction form (
 static int cg_onepass(sm_ctx *c) {
     const long j = c->cg_issued;
     const bool odd = j & 1, first = j == 0;
-    const bool td = c->cg_fused >= 4;  // mode 5 falls back here where the recompute-Ad pass does not fit
-    double2 *dold = c->field(odd ? F_D2 : F_D), *dnew = c->field(odd ? F_D : F_D2);
-    double2 *rold = c->field(odd ? F_R2 : F_R), *rnew = c->field(odd ? F_R : F_R2);
+    // pass 0 reads d_0 from F_D and stores it to cg_dbuf(0)
+    const double2 *dold = first ? c->field(F_D) : cg_dbuf(c, j - 1);
+    const double2 *d2 = cg_dbuf(c, j - 2);
+    double2 *dnew = cg_dbuf(c, j);
     double2 *aold = c->field(odd ? F_AD2 : F_AD), *anew = c->field(odd ? F_AD : F_AD2);
-    if (td) {
-        // pass 0 reads d_0 from F_D and stores it to cg_dbuf(0); rold = d_{j-2}
-        dold = first ? c->field(F_D) : cg_dbuf(c, j - 1);
-        rold = cg_dbuf(c, j - 2);
-        dnew = cg_dbuf(c, j);
-        rnew = nullptr;
-    }
     const CGFusedCfg &fc = c->fcfg;
     const int nparts = cg_fused_blocks(fc);
-    // small one-shard grids: the pass's last block forms the scalars (saves a
-    // latency-bound launch per iteration); large grids contend on the ticket
-    const bool inkernel = c->nshard == 1 && nparts <= c->cg_inkernel_max_blocks;
-    // redundant scalars (default for those grids): partials by pass parity,
+    // redundant scalars on small one-shard grids: partials by pass parity,
     // evaluated by every block of the next pass; sm_cg_iterate flushes the last
-    const bool redundant = inkernel && c->cg_redundant;
+    const bool redundant = !c->sharded() && c->cg_redundant && nparts <= c->cg_red_max_blocks;
     double2 *part = redundant ? c->partials + (j & 1) * 3 * (size_t)nparts : c->partials;
     const double2 *prev = redundant ? c->partials + ((j + 1) & 1) * 3 * (size_t)nparts : nullptr;
     auto pass = [&](int tb0, int tbn, hipStream_t st) {
-        launch_cg_onepass(st, c->g, fc, c->nshard, dold, rold, aold, dnew, rnew, anew, c->cg_x, c->U,
-                          face2_recv(c, 0), face2_recv(c, 1), face2_recv(c, 3), face2_recv(c, 2), c->cg_mass,
-                          first, c->sc, part, tb0, tbn, inkernel && !redundant ? c->counters : nullptr, prev, j,
-                          td);
+        launch_cg_onepass(st, c->g, fc, c->kshards(), dold, d2, aold, dnew, anew, c->cg_x, c->U, face2_recv(c, 0),
+                          face2_recv(c, 1), face2_recv(c, 3), face2_recv(c, 2), c->cg_mass, first, c->sc, part, tb0,
+                          tbn, prev, j);
     };
-    if (td) c->cg_pending_x = 1;  // sm_cg_finish checks the device's final pass parity
-    if (c->nshard == 1) {
+    c->cg_pending_x = 1;  // sm_cg_finish checks the device's final pass parity
+    if (!c->sharded()) {
         pass(0, fc.TBk, c->stream);
-        if (!inkernel) launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
+        if (!redundant) launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
         c->cg_flush_pass = redundant ? j : -1;
         c->cg_flush_nparts = nparts;
         return SM_OK;
     }
-    // interior t-blocks while the 2-deep faces of d, r, Ad travel (one round)
-    const double2 *flds[3] = {dold, rold, aold};
+    // interior t-blocks while the 2-deep faces of d_{j-1}, d_{j-2}, Ad_{j-1} travel (one round)
+    const double2 *flds[3] = {dold, d2, aold};
     double2 *fcs[3] = {face2_recv(c, 0), face2_recv(c, 1), face2_recv(c, 3)};
     auto interior = [&](int tb) {
         const int g_lo = 4 * tb, g_hi = std::min(4 * tb + 3, fc.NWT - 1);
@@ -739,7 +728,7 @@ static int cg_ra_pass(sm_ctx *c) {
     const int nparts = cg_fused_blocks(fc);
     c->cg_pending_x = 1;  // sm_cg_finish checks the device's final pass parity
     c->cg_flush_pass = -1;
-    const bool one = c->nshard == 1;
+    const bool one = !c->sharded();
     if (one && !c->split_test) {
         // redundant scalars on small grids (partials by pass parity; every block
         // of the next pass evaluates them; sm_cg_iterate flushes the last pass)
@@ -758,7 +747,7 @@ static int cg_ra_pass(sm_ctx *c) {
     }
     double2 *f1 = one ? nullptr : face4_recv_d(c, j), *f2 = one ? nullptr : face4_recv_d(c, j - 1);
     auto pass = [&](int tb0, int tbn, hipStream_t st) {
-        launch_cg_ra(st, c->g, fc, c->nshard, d1, d2, dn, c->cg_x, c->U, f1, f2, one ? nullptr : face4_recv_U(c),
+        launch_cg_ra(st, c->g, fc, c->kshards(), d1, d2, dn, c->cg_x, c->U, f1, f2, one ? nullptr : face4_recv_U(c),
                      c->cg_mass, j, c->sc, c->partials, tb0, tbn);
     };
     // interior t-blocks: every lane's column (56g-4 .. 56g+59) inside [0, Wt)
@@ -807,65 +796,12 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
     for (int i = 0; i < niter; ++i) {
         if (c->cg_fused == 5 && cg_ra_ok(c)) {
             TRY(cg_ra_pass(c));
-        } else if (c->cg_fused >= 3) {
+        } else if (c->cg_fused >= 4) {
             TRY(cg_onepass(c));
-        } else if (c->cg_fused) {
-            // pass 1: d_k, deferred x update, Ad = D D^dag d_k, <d_k, Ad>
-            double2 *dold = c->field((c->cg_issued & 1) ? F_D2 : F_D);
-            double2 *dnew = c->field((c->cg_issued & 1) ? F_D : F_D2);
-            const CGFusedCfg &fc = c->fcfg;
-            const bool one = c->nshard == 1 && c->cg_inkernel;  // scalars reduced in-kernel (last block)
-            auto pass1 = [&](int tb0, int tbn) {
-                launch_cg_fused(c->stream, c->g, fc, c->nshard, dold, dnew, r, x, Ad, c->U,
-                                face2_recv(c, 0), face2_recv(c, 1), face2_recv(c, 2), c->cg_mass,
-                                c->cg_issued == 0, c->sc, c->partials, tb0, tbn,
-                                one ? c->counters : nullptr);
-            };
-            if (c->nshard == 1) {
-                pass1(0, fc.TBk);
-            } else {
-                // Only the first and last t-blocks read the faces: exchange them
-                // (d_{k-1} and r in one round) on the comm stream while the
-                // interior blocks run, then finish the two edge block-columns.
-                const double2 *flds[2] = {dold, r};
-                double2 *fcs[2] = {face2_recv(c, 0), face2_recv(c, 1)};
-                // interior t-blocks: every valid tile's lanes (columns 60g-2 .. 60g+61)
-                // stay inside [0, Wt): they never read a face
-                auto interior = [&](int tb) {
-                    const int g_lo = 4 * tb, g_hi = std::min(4 * tb + 3, fc.NWT - 1);
-                    return kFusedWaveCols * g_lo - 2 >= 0 &&
-                           kFusedWaveCols * g_hi + kFusedWaveCols + 1 <= c->g.Wt - 1;
-                };
-                int tb_lo = 0, tb_hi = -1;
-                for (int tb = 0; tb < fc.TBk; ++tb)
-                    if (interior(tb)) {
-                        if (tb_hi < 0) tb_lo = tb;
-                        tb_hi = tb;
-                    }
-                const bool split = tb_hi >= tb_lo && tb_hi >= 0;
-                // (the host transport runs the same stream/event sequence; its
-                // exchange blocks the host, so it just does not overlap)
-                HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
-                HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
-                TRY(halo2_multi(c, c->comm_stream, flds, fcs, 2));
-                HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
-                if (split) pass1(tb_lo, tb_hi - tb_lo + 1);
-                HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
-                if (split) {
-                    pass1(0, tb_lo);
-                    pass1(tb_hi + 1, fc.TBk - tb_hi - 1);
-                } else {
-                    pass1(0, fc.TBk);
-                }
-            }
-            if (!one) TRY(cg_scalar(c, cg_fused_blocks(c->fcfg), 0));
-            // pass 2: r -= alpha Ad, <r, r>; stop test and beta
-            launch_cg_update_r(c->stream, n, r, Ad, c->sc, c->partials, one ? c->counters + 32 : nullptr);
-            if (!one) TRY(cg_scalar(c, c->nparts_red, 1));
-            c->cg_pending_x = 1;
         } else {
+            // the reference's sequence, six launches (src/conjugate_gradient.cpp:31-63):
+            // Ad = D D^dag d with fused partials of <d, Ad>; alpha; x, r; beta; d
             double2 *d = c->field(F_D);
-            // Ad = D D^dag d, fused partials of <d, Ad>
             TRY(apply(c, d, t, c->cg_mass, 1, nullptr, nullptr, c->sc));
             TRY(apply(c, t, Ad, c->cg_mass, 0, d, c->partials, c->sc));
             TRY(cg_scalar(c, c->nparts_dslash, 0));
@@ -875,7 +811,7 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
         }
         c->cg_issued++;
     }
-    if (c->cg_fused >= 3 && c->cg_flush_pass >= 0) {  // redundant scalars: evaluate the last pass for the host
+    if (c->cg_fused >= 4 && c->cg_flush_pass >= 0) {  // redundant scalars: evaluate the last pass for the host
         const long J = c->cg_flush_pass;
         const int nparts = c->cg_flush_nparts;
         launch_cg1_flush(c->stream, nparts, c->partials + (J & 1) * 3 * (size_t)nparts, c->sc, J);
@@ -887,12 +823,8 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
 
 int sm_cg_finish(sm_ctx *c, sm_cg_result *res) {
     if (!c || !res) return fail(SM_ERR_ARG, "null argument");
-    if (c->cg_active && c->cg_pending_x && c->cg_fused >= 4) {
+    if (c->cg_active && c->cg_pending_x) {
         launch_cg_td_finish_x(c->stream, 2 * c->g.V, c->cg_x, cg_dbuf(c, 0), cg_dbuf(c, 1), cg_dbuf(c, 2), c->sc);
-        HIP_TRY(hipGetLastError());
-        c->cg_pending_x = 0;
-    } else if (c->cg_active && c->cg_pending_x) {
-        launch_cg_finish_x(c->stream, 2 * c->g.V, c->cg_x, c->field(F_D), c->field(F_D2), c->sc);
         HIP_TRY(hipGetLastError());
         c->cg_pending_x = 0;
     }
@@ -917,10 +849,10 @@ int sm_cg_dev(sm_ctx *c, const double *phi, double *x, double m0, double tol, in
     TRY(sm_cg_begin(c, phi, x, m0, tol));
     // Enqueue iterations in chunks; each CG kernel is a no-op once the device
     // flag `done` is set, so overshooting a chunk costs only empty launches.
-    // The one-pass path runs max_iter + 1 passes (pass 0 forms Ad_0) and stops
-    // itself at k == max_iter.
+    // The one-pass paths run max_iter + 1 passes (pass 0 forms Ad_0) and stop
+    // themselves at k == max_iter.
     int passes = max_iter;
-    if (c->cg_fused >= 3) {
+    if (c->cg_fused >= 4) {
         HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)&c->sc->max_iter, max_iter, 1, c->stream));
         passes = max_iter + 1;
     }
@@ -931,6 +863,9 @@ int sm_cg_dev(sm_ctx *c, const double *phi, double *x, double m0, double tol, in
         TRY(sm_cg_iterate(c, nb));
         issued += nb;
         TRY(sm_cg_status(c, res));
+        if (c->debug_cg)
+            fprintf(stderr, "[sm cg shard %d/%d] passes %d k %d err %.3e\n", c->shard, c->nshard, issued,
+                    res->iterations, res->residual);
         if (res->converged) break;
         chunk = plan.next(res->iterations, res->residual, tol * res->phi_norm);
     }

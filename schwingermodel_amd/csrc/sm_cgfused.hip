@@ -1,23 +1,30 @@
-// sm_cgfused.hip -- one CG iteration on D D^dagger in two HBM passes (gfx950).
+// sm_cgfused.hip -- the two-direction one-pass CG iteration with a stored Ad
+// (gfx950), the default below 256^2 sites per shard (mode 4 of sm_tune_cg),
+// plus the CG scalar kernels shared with the recompute-Ad pass (sm_cgra.hip).
 //
 // Reference loop body (src/conjugate_gradient.cpp:31-63), iteration k:
 //     Ad = D D^dag d_k ; alpha_k = rn / <d_k, Ad> ; x += alpha_k d_k ;
 //     r -= alpha_k Ad ; err = |r| ; stop? ; beta_k = err^2 / rn ; d_{k+1} = d_k beta_k + r
-// Pass 1 (cg_fused_kernel), iteration k:
-//     d_k = d_{k-1} beta_{k-1} + r_k          (on the fly, stored once)
-//     x  += alpha_{k-1} d_{k-1}               (deferred x update of iteration k-1)
-//     T   = D^dag d_k   (registers only)      Ad = D T ; partials of <d_k, Ad>
-// Pass 2 (cg_update_r_kernel): r -= alpha_k Ad ; partials of <r, r>.
-// Every per-element operation is the reference's (same complex arithmetic,
-// same order), only the dot-product reduction order differs.
-//
-// HBM bytes per site: pass 1 reads d_{k-1}, r, x, U (128) and writes d_k, x, Ad
-// (96); pass 2 reads r, Ad and writes r (96): 320 B/site against 576 for the
-// reference's sequence.
+// Pass j (j >= 1), every per-element operation the reference's:
+//     r_{j-1} = d_{j-1} - d_{j-2} beta_{j-2}         (the reference's d *= beta; d += r, :55-58)
+//     r_j     = r_{j-1} - alpha_{j-1} Ad_{j-1}       (:38-39)
+//     d_j     = d_{j-1} beta_{j-1} + r_j             (:55-58)
+//     x      <- (x + alpha_{j-2} d_{j-2}) + alpha_{j-1} d_{j-1}   on even j (:36-37)
+//     Ad_j    = D D^dag d_j ; partials of <d_j,Ad_j>, <r_j,Ad_j>, |r_j|^2, |Ad_j|^2
+// Then (cg1_scalar_kernel): err = sqrt|r_j|^2 (direct, as the reference) and its
+// stop test; alpha_j = |r_j|^2 / <d_j,Ad_j>; and beta_j from the expansion
+//     |r_{j+1}|^2 = |r_j|^2 - 2 Re(conj(alpha_j) <r_j,Ad_j>) + |alpha_j|^2 |Ad_j|^2
+// of the pass's own direct dots (no conjugacy assumed), so r_{j+1} never has
+// to be written before d_{j+1} is formed. Pass 0 only forms Ad_0 (d_0 = r_0).
+// No r vector is stored: d rotates through three buffers, Ad ping-pongs (halo
+// lanes / rows of neighbouring tiles read the j-1 fields while owners write
+// the j fields). HBM bytes per site: read d_{j-1}, d_{j-2}, Ad_{j-1}, U (128),
+// write d_j, Ad_j (64), plus read and write x on even passes: 224 mean,
+// against 576 for the reference's sequence.
 //
 // Geometry: a wave owns 60 consecutive t-columns; its 64 lanes cover columns
 // T0-2 .. T0+61 (2 halo lanes per side) and march along x. The t-neighbours of
-// the intermediates (d_k, T, U_t) come from adjacent lanes through DPP
+// the intermediates (d_j, T, U_t) come from adjacent lanes through DPP
 // wave-shifts; the x-neighbours are register rows. Halo lanes compute and are
 // discarded, so waves are independent (no LDS, no barrier in the loop).
 #include "sm_device.h"
@@ -29,241 +36,34 @@ namespace sm {
 
 constexpr int FW = kFusedWaveCols;  // output t-columns per wave
 
-struct CGFArgs {
-    const double2 *dold;
-    double2 *dnew;
-    const double2 *r;
-    double2 *x;
-    double2 *Ad;
-    const double2 *U;
-    const double2 *fd, *fr, *fU;  // nshard > 1: 4-column faces [-2,-1,Wt,Wt+1][plane][x]
-    CGScalars *sc;
-    double2 *partials;
-    long V;
-    int Nx, Wt, t0, Ntg, nshard;
-    int xchunk, NWT, TBk, XB, remap, first;
-    int tb0, tbn, part0;  // launch covers t-blocks [tb0, tb0+tbn); partials at part0 + blockIdx
-    unsigned *counter;    // finalize: last block sums the partials and computes alpha
-    int finalize;
-    double mass;
-};
-
 struct CSrc {
     const double2 *p;
     long xs, ps;
 };
 
-// Where column c of a field lives: in-domain, periodic wrap (one shard), or
-// the received face (t-shard). Clamped so every lane's address is valid.
-__device__ __forceinline__ CSrc csrc(const double2 *base, const double2 *face, int c, const CGFArgs &a) {
-    CSrc s;
-    if (c >= 0 && c < a.Wt) {
-        s.p = base + c;
-        s.xs = a.Wt;
-        s.ps = a.V;
-    } else if (a.nshard == 1) {
-        int cw = c % a.Wt;
-        if (cw < 0) cw += a.Wt;
-        s.p = base + cw;
-        s.xs = a.Wt;
-        s.ps = a.V;
-    } else {
-        int fc = c < 0 ? c + 2 : c - a.Wt + 2;
-        fc = fc < 0 ? 0 : (fc > 3 ? 3 : fc);
-        s.p = face + (long)fc * 2 * a.Nx;
-        s.xs = 1;
-        s.ps = a.Nx;
-    }
-    return s;
-}
-
-struct Raw {
-    double2 d0, d1, r0, r1, ut, ux, x0, x1;
-};
-
-
-__global__ void __launch_bounds__(256) cg_fused_kernel(CGFArgs a) {
-    __shared__ double2 sh[4];
-    CGScalars *sc = a.sc;
-    if (sc->done) return;  // grid-uniform: converged in an earlier iteration
-    const double2 alpha = sc->alpha, beta = sc->beta;  // alpha_{k-1}, beta_{k-1}
-    int tb, xc;
-    {
-        int w = blockIdx.x;
-        if (a.remap) {
-            const int n = a.tbn * a.XB, q = n >> 3, rr = n & 7, xcd = w & 7;
-            w = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (w >> 3);
-        }
-        tb = a.tb0 + w % a.tbn;
-        xc = w / a.tbn;
-    }
-    const int lane = threadIdx.x & 63;
-    const int g = tb * 4 + (threadIdx.x >> 6);  // wave tile along t
-    const int x0 = xc * a.xchunk;
-    const int xe = min(a.Nx, x0 + a.xchunk);
-    double2 acc = make_double2(0.0, 0.0);
-    if (g < a.NWT && x0 < xe) {
-        const int Nx = a.Nx, Wt = a.Wt;
-        const int c = g * FW - 2 + lane;                 // this lane's t-column
-        const bool own = lane >= 2 && lane < FW + 2 && c < Wt;
-        int tg = (a.t0 + c) % a.Ntg;
-        if (tg < 0) tg += a.Ntg;
-        const double sr0 = tg == a.Ntg - 1 ? -1.0 : 1.0;  // SignR[2n], include/dirac_operator.h:53-55
-        const double sl0 = tg == 0 ? -1.0 : 1.0;          // SignL[2n], :56-58
-        const CSrc Sd = csrc(a.dold, a.fd, c, a), Sr = csrc(a.r, a.fr, c, a), Su = csrc(a.U, a.fU, c, a);
-        const int cx = c < 0 ? 0 : (c >= Wt ? Wt - 1 : c);  // in-domain column for x / stores
-        const bool first = a.first != 0;
-        auto wrap = [Nx](int x) { int w = x % Nx; return w < 0 ? w + Nx : w; };
-        // raw loads of logical row xr: d_{k-1}, r (rows x0-2 .. xe+1), U (clamped
-        // to x0-2 .. xe), x (clamped to owned rows; re-reads are cache hits)
-        auto load = [&](int xr, Raw &R) {
-            const long pr = (long)wrap(xr);
-            const double2 *pd = Sd.p + pr * Sd.xs, *pq = Sr.p + pr * Sr.xs;
-            R.d0 = pd[0];
-            R.d1 = pd[Sd.ps];
-            R.r0 = pq[0];
-            R.r1 = pq[Sr.ps];
-            const double2 *pu = Su.p + (long)wrap(min(xr, xe)) * Su.xs;
-            R.ut = pu[0];
-            R.ux = pu[Su.ps];
-            const long nx = (long)wrap(min(max(xr, x0), xe - 1)) * Wt + cx;
-            R.x0 = a.x[nx];
-            R.x1 = a.x[nx + a.V];
-        };
-        // d_k = d_{k-1} * beta + r (src/conjugate_gradient.cpp:55-58); on owned
-        // rows also store it and apply the deferred x += alpha d_{k-1} (:36-37)
-        auto dnew = [&](int xr, const Raw &R) {
-            Sp d;
-            d.a = first ? R.d0 : cadd(cmul(R.d0, beta), R.r0);
-            d.b = first ? R.d1 : cadd(cmul(R.d1, beta), R.r1);
-            if (xr >= x0 && xr < xe && own) {
-                const long n = (long)xr * Wt + c;
-                st_nt(a.dnew + n, d.a);
-                st_nt(a.dnew + n + a.V, d.b);
-                if (!first) {
-                    st_nt(a.x + n, cadd(R.x0, cmul(alpha, R.d0)));
-                    st_nt(a.x + n + a.V, cadd(R.x1, cmul(alpha, R.d1)));
-                }
-            }
-            return d;
-        };
-        // D^dag at this lane's column of row xr (centre p, x-neighbours pxm/pxp)
-        auto ddag = [&](const Sp &p, const Sp &pxm, const Sp &pxp, double2 ut, double2 ux,
-                        double2 uxm, double2 &utm_out) {
-            const Sp pm = shr(p), pp = shl(p);
-            utm_out = dpp_shr1(ut);
-            Sp o;
-            dirac_site<1>(a.mass, sr0, sl0, p.a, p.b, pp.a, pp.b, pxp.a, pxp.b, pm.a, pm.b, pxm.a,
-                          pxm.b, ut, ux, utm_out, uxm, o.a, o.b);
-            return o;
-        };
-        // prologue: rows x0-2 .. x0+1
-        Raw R;
-        load(x0 - 2, R);
-        Sp dm2 = dnew(x0 - 2, R);
-        double2 uxm2 = R.ux;
-        load(x0 - 1, R);
-        Sp dm1 = dnew(x0 - 1, R);
-        double2 utm1 = R.ut, uxm1 = R.ux;
-        load(x0, R);
-        Sp dc = dnew(x0, R);
-        double2 utc = R.ut, uxc = R.ux;
-        load(x0 + 1, R);
-        Sp dn = dnew(x0 + 1, R);
-        double2 utn = R.ut, uxn = R.ux;
-        load(x0 + 2, R);
-        double2 dummy;
-        Sp Tp = ddag(dm1, dm2, dc, utm1, uxm1, uxm2, dummy);  // T(x0-1)
-        double2 utmc;
-        Sp Tc = ddag(dc, dm1, dn, utc, uxc, uxm1, utmc);      // T(x0), U_t(x0, t-1)
-        double2 uxp = uxm1;                                   // U_x(x-1)
-        for (int x = x0; x < xe; ++x) {
-            // A: row x+2 -> d_{k}(x+2); then immediately reuse R for row x+3
-            const Sp d2 = dnew(x + 2, R);
-            const double2 ut2 = R.ut, ux2 = R.ux;
-            load(min(x + 3, xe + 1), R);
-            __builtin_amdgcn_sched_barrier(0);  // keep the next row's loads issued here
-            // B: T(x+1) = D^dag d at row x+1
-            double2 utmn;
-            const Sp Tn = ddag(dn, dc, d2, utn, uxn, uxc, utmn);
-            // C: Ad(x) = D T at row x; dot <d_k, Ad> on owned sites
-            const Sp Tm = shr(Tc), Tq = shl(Tc);
-            Sp o;
-            dirac_site<0>(a.mass, sr0, sl0, Tc.a, Tc.b, Tq.a, Tq.b, Tn.a, Tn.b, Tm.a, Tm.b, Tp.a, Tp.b,
-                          utc, uxc, utmc, uxp, o.a, o.b);
-            if (own) {
-                const long n = (long)x * Wt + c;
-                st_nt(a.Ad + n, o.a);
-                st_nt(a.Ad + n + a.V, o.b);
-                acc = cadd(acc, cmul(dc.a, cconj(o.a)));  // dot(d, Ad), include/variables.h:185-188
-                acc = cadd(acc, cmul(dc.b, cconj(o.b)));
-            }
-            // rotate (all ready values: no load is waited on here)
-            Tp = Tc;
-            Tc = Tn;
-            dc = dn;
-            dn = d2;
-            uxp = uxc;
-            utc = utn;
-            uxc = uxn;
-            utmc = utmn;
-            utn = ut2;
-            uxn = ux2;
-        }
-    }
-    const double2 bs = block_sum(acc, sh);
-    if (!a.finalize) {
-        if (threadIdx.x == 0) a.partials[a.part0 + blockIdx.x] = bs;
-    } else {  // single launch over the whole shard: alpha in-kernel
-        if (threadIdx.x == 0) publish_partial(a.partials + blockIdx.x, bs);
-        __shared__ int last;
-        if (last_block_arrive(a.counter, gridDim.x, &last)) {
-            const double2 tot = sum_published_block(gridDim.x, a.partials, sh);
-            if (threadIdx.x == 0) cg_alpha_scalar(sc, tot);  // alpha = rn / <d, Ad>
-        }
-    }
-}
-
-// ---- one-pass CG iteration (pass 2 folded into the next pass 1) ----------------
-// Pass j (j >= 1), every per-element operation the reference's:
-//     r_j  = r_{j-1} - alpha_{j-1} Ad_{j-1}          (src/conjugate_gradient.cpp:38-39)
-//     d_j  = d_{j-1} beta_{j-1} + r_j                (:55-58)
-//     x_j  = x_{j-1} + alpha_{j-1} d_{j-1}           (:36-37)
-//     Ad_j = D D^dag d_j ; partials of <d_j,Ad_j>, <r_j,Ad_j>, |r_j|^2, |Ad_j|^2
-// Then (cg1_scalar_kernel): err = sqrt|r_j|^2 (direct, as the reference) and its
-// stop test; alpha_j = |r_j|^2 / <d_j,Ad_j>; and beta_j from the expansion
-//     |r_{j+1}|^2 = |r_j|^2 - 2 Re(conj(alpha_j) <r_j,Ad_j>) + |alpha_j|^2 |Ad_j|^2
-// of the pass's own direct dots (no conjugacy assumed), so r_{j+1} never has
-// to be written before d_{j+1} is formed. Pass 0 only forms Ad_0 (d_0 = r_0).
-// r, d and Ad ping-pong (halo lanes / rows of neighbouring tiles read the
-// j-1 fields while owners write the j fields).
-// HBM bytes per site and iteration: read d, r, Ad, x, U (160), write d, r, Ad,
-// x (128) = 288, against 320 for the two-pass iteration and 576 for the
-// reference's sequence.
 struct CG1Args {
-    const double2 *dold, *rold, *aold;
-    double2 *dnew, *rnew, *anew;
+    const double2 *dold, *rold, *aold;  // d_{j-1}, d_{j-2}, Ad_{j-1}
+    double2 *dnew, *anew;               // d_j, Ad_j
     double2 *x;
     const double2 *U;
-    const double2 *fd, *fr, *fa, *fU;  // nshard > 1: 4-column faces
+    const double2 *fd, *fr, *fa, *fU;  // t-shards: 2-deep faces [-2,-1,Wt,Wt+1][plane][x]
     CGScalars *sc;
     double2 *partials;                 // 3 per block: <d,Ad>, <r,Ad>, (|r|^2, |Ad|^2)
-    unsigned *counter;                 // small one-shard grids: the last block forms the scalars
     const double2 *prev;               // != null: redundant scalars from pass j-1's partials
-    long pass;                         // j (redundant scalars)
+    long pass;                         // j
     long V;
     int Nx, Wt, t0, Ntg, nshard;
     int xchunk, NWT, TBk, XB, remap, first;
-    int tb0, tbn, part0;
+    int tb0, tbn;
     double mass;
 };
-
-__device__ void cg1_scalars(CGScalars *sc, int first, double2 dA, double2 rA, double2 nn);
 
 struct Raw3 {
     double2 d0, d1, r0, r1, a0, a1, ut, ux, x0, x1;
 };
 
+// Where column c of a field lives: in-domain, periodic wrap (one shard), or
+// the received face (t-shard). Clamped so every lane's address is valid.
 __device__ __forceinline__ CSrc csrc1(const double2 *base, const double2 *face, int c, const CG1Args &a) {
     CSrc s;
     if (c >= 0 && c < a.Wt) {
@@ -286,16 +86,15 @@ __device__ __forceinline__ CSrc csrc1(const double2 *base, const double2 *face, 
     return s;
 }
 
-// RED: redundant scalars (a.prev != null); its own instance keeps the call out of the large-grid kernel.
-// TD: two-direction recurrence (no r vector): the `rold` fields hold d_{j-2},
-// r_{j-1} is rebuilt as d_{j-1} - d_{j-2} beta_{j-2}, and x takes the updates of
-// passes j-1 and j together on even passes (XP = 1); 224 instead of 288 B/site.
-template <int RED, int TD, int XP>
+// RED: redundant scalars (a.prev != null): every block evaluates pass j-1's
+// scalars itself; its own instance keeps that code out of the large-grid kernel.
+// XP: x takes the updates of passes j-1 and j together (even passes).
+template <int RED, int XP>
 __global__ void __launch_bounds__(256) cg_onepass_kernel(CG1Args a) {
     __shared__ double2 sh[4];
     CGScalars *sc = a.sc;
     double2 alpha, beta;                               // alpha_{j-1}, beta_{j-1}
-    double2 alpha2, beta2;                             // alpha_{j-2}, beta_{j-2} (TD)
+    double2 alpha2, beta2;                             // alpha_{j-2}, beta_{j-2}
     if (RED) {
         __shared__ double2 s_ab[4];
         __shared__ int s_stop;
@@ -347,8 +146,8 @@ __global__ void __launch_bounds__(256) cg_onepass_kernel(CG1Args a) {
         const bool own = lane >= 2 && lane < FW + 2 && c < Wt;
         int tg = (a.t0 + c) % a.Ntg;
         if (tg < 0) tg += a.Ntg;
-        const double sr0 = tg == a.Ntg - 1 ? -1.0 : 1.0;
-        const double sl0 = tg == 0 ? -1.0 : 1.0;
+        const double sr0 = tg == a.Ntg - 1 ? -1.0 : 1.0;  // SignR[2n], include/dirac_operator.h:53-55
+        const double sl0 = tg == 0 ? -1.0 : 1.0;          // SignL[2n], :56-58
         const CSrc Sd = csrc1(a.dold, a.fd, c, a), Sr = csrc1(a.rold, a.fr, c, a);
         const CSrc Sa = csrc1(a.aold, a.fa, c, a), Su = csrc1(a.U, a.fU, c, a);
         const int cx = c < 0 ? 0 : (c >= Wt ? Wt - 1 : c);
@@ -366,24 +165,18 @@ __global__ void __launch_bounds__(256) cg_onepass_kernel(CG1Args a) {
             const double2 *pu = Su.p + (long)wrap(min(xr, xe)) * Su.xs;
             R.ut = pu[0];
             R.ux = pu[Su.ps];
-            if (!TD || XP) {
+            if (XP) {
                 const long nx = (long)wrap(min(max(xr, x0), xe - 1)) * Wt + cx;
                 R.x0 = a.x[nx];
                 R.x1 = a.x[nx + a.V];
             }
         };
-        const bool rebuild = TD && a.pass >= 2;  // pass 1 has r_0 = d_0 (no d_{-1})
-        // r_j and d_j of row xr; on owned rows store r_j (not TD), d_j, x_j, add |r_j|^2
+        const bool rebuild = a.pass >= 2;  // pass 1 has r_0 = d_0 (no d_{-1})
+        // r_j and d_j of row xr; on owned rows store d_j, x_j, add |r_j|^2
         auto form = [&](int xr, const Raw3 &R, Sp &rj) {
-            Sp rp;  // r_{j-1}
-            if (TD) {
-                // d_{j-1} = d_{j-2} beta_{j-2} + r_{j-1} (the reference's d *= beta; d += r)
-                rp.a = rebuild ? csub(R.d0, cmul(R.r0, beta2)) : R.d0;
-                rp.b = rebuild ? csub(R.d1, cmul(R.r1, beta2)) : R.d1;
-            } else {
-                rp.a = R.r0;
-                rp.b = R.r1;
-            }
+            Sp rp;  // r_{j-1}: d_{j-1} = d_{j-2} beta_{j-2} + r_{j-1}
+            rp.a = rebuild ? csub(R.d0, cmul(R.r0, beta2)) : R.d0;
+            rp.b = rebuild ? csub(R.d1, cmul(R.r1, beta2)) : R.d1;
             rj.a = first ? rp.a : csub(rp.a, cmul(alpha, R.a0));
             rj.b = first ? rp.b : csub(rp.b, cmul(alpha, R.a1));
             Sp d;
@@ -391,17 +184,9 @@ __global__ void __launch_bounds__(256) cg_onepass_kernel(CG1Args a) {
             d.b = first ? R.d1 : cadd(cmul(R.d1, beta), rj.b);
             if (xr >= x0 && xr < xe && own) {
                 const long n = (long)xr * Wt + c;
-                if (!TD) {
-                    st_nt(a.rnew + n, rj.a);
-                    st_nt(a.rnew + n + a.V, rj.b);
-                }
                 st_nt(a.dnew + n, d.a);
                 st_nt(a.dnew + n + a.V, d.b);
-                if (!TD && !first) {
-                    st_nt(a.x + n, cadd(R.x0, cmul(alpha, R.d0)));
-                    st_nt(a.x + n + a.V, cadd(R.x1, cmul(alpha, R.d1)));
-                }
-                if (TD && XP) {  // x_j = (x_{j-2} + alpha_{j-2} d_{j-2}) + alpha_{j-1} d_{j-1}
+                if (XP) {  // x_j = (x_{j-2} + alpha_{j-2} d_{j-2}) + alpha_{j-1} d_{j-1}
                     st_nt(a.x + n, cadd(cadd(R.x0, cmul(alpha2, R.r0)), cmul(alpha, R.d0)));
                     st_nt(a.x + n + a.V, cadd(cadd(R.x1, cmul(alpha2, R.r1)), cmul(alpha, R.d1)));
                 }
@@ -483,37 +268,11 @@ __global__ void __launch_bounds__(256) cg_onepass_kernel(CG1Args a) {
     const double2 s1 = block_sum(acc_rA, sh);
     __syncthreads();
     const double2 s2 = block_sum(acc_n, sh);
-    double2 *p = a.partials + 3 * ((long)tb * a.XB + xc);  // one slot per tile
-    if (!a.counter) {  // (also the redundant-scalar path: plain stores, read by the next launch)
-        if (threadIdx.x == 0) {
-            p[0] = s0;
-            p[1] = s1;
-            p[2] = s2;
-        }
-        return;
-    }
-    // small grid, one shard: write-through publish + ticket; the last block
-    // sums all partials (sc1 loads, fixed order) and forms the scalars
-    if (threadIdx.x == 0) {
-        publish_partial(p, s0);
-        publish_partial(p + 1, s1);
-        publish_partial(p + 2, s2);
-    }
-    __shared__ int last;
-    if (last_block_arrive(a.counter, gridDim.x, &last)) {
-        double2 t[3];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            __syncthreads();
-            double2 acc = make_double2(0.0, 0.0);
-            for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) {
-                const double2 *pi = a.partials + 3 * (long)i + q;
-                acc = cadd(acc, make_double2(__hip_atomic_load(&pi->x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                             __hip_atomic_load(&pi->y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-            }
-            t[q] = block_sum(acc, sh);
-        }
-        if (threadIdx.x == 0) cg1_scalars(sc, a.first, t[0], t[1], t[2]);
+    if (threadIdx.x == 0) {  // one slot per tile (also the redundant path: read by the next launch)
+        double2 *p = a.partials + 3 * ((long)tb * a.XB + xc);
+        p[0] = s0;
+        p[1] = s1;
+        p[2] = s2;
     }
 }
 
@@ -632,14 +391,13 @@ __global__ void cg1_from_sums_kernel(CGScalars *sc, int first) {
 
 void launch_cg_onepass(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard,
                        const double2 *dold, const double2 *rold, const double2 *aold, double2 *dnew,
-                       double2 *rnew, double2 *anew, double2 *x, const double2 *U, const double2 *fd,
-                       const double2 *fr, const double2 *fa, const double2 *fU, double mass, int first,
-                       CGScalars *sc, double2 *partials, int tb0, int tbn, unsigned *counter,
-                       const double2 *prev_partials, long pass, int twodir) {
+                       double2 *anew, double2 *x, const double2 *U, const double2 *fd, const double2 *fr,
+                       const double2 *fa, const double2 *fU, double mass, int first, CGScalars *sc,
+                       double2 *partials, int tb0, int tbn, const double2 *prev_partials, long pass) {
     if (tbn <= 0) return;
     CG1Args a;
     a.dold = dold; a.rold = rold; a.aold = aold;
-    a.dnew = dnew; a.rnew = rnew; a.anew = anew;
+    a.dnew = dnew; a.anew = anew;
     a.x = x; a.U = U;
     a.fd = fd; a.fr = fr; a.fa = fa; a.fU = fU;
     a.sc = sc; a.partials = partials;
@@ -649,23 +407,16 @@ void launch_cg_onepass(hipStream_t s, const Geometry &g, const CGFusedCfg &c, in
     a.mass = mass;
     a.tb0 = tb0;
     a.tbn = tbn;
-    a.part0 = tb0 * c.XB;
-    a.counter = counter;
     a.prev = prev_partials;
     a.pass = pass;
     const dim3 grid(tbn * c.XB), block(256);
-    if (!twodir) {
-        if (prev_partials) hipLaunchKernelGGL((cg_onepass_kernel<1, 0, 0>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((cg_onepass_kernel<0, 0, 0>), grid, block, 0, s, a);
-        return;
-    }
     const bool xp = pass >= 2 && (pass & 1) == 0;  // x takes passes j-1 and j together
     if (prev_partials) {
-        if (xp) hipLaunchKernelGGL((cg_onepass_kernel<1, 1, 1>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((cg_onepass_kernel<1, 1, 0>), grid, block, 0, s, a);
+        if (xp) hipLaunchKernelGGL((cg_onepass_kernel<1, 1>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((cg_onepass_kernel<1, 0>), grid, block, 0, s, a);
     } else {
-        if (xp) hipLaunchKernelGGL((cg_onepass_kernel<0, 1, 1>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((cg_onepass_kernel<0, 1, 0>), grid, block, 0, s, a);
+        if (xp) hipLaunchKernelGGL((cg_onepass_kernel<0, 1>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((cg_onepass_kernel<0, 0>), grid, block, 0, s, a);
     }
 }
 
@@ -708,85 +459,7 @@ CGFusedCfg cg_fused_config(const Geometry &g) {
 
 int cg_fused_blocks(const CGFusedCfg &c) { return c.TBk * c.XB; }
 
-void launch_cg_fused(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard,
-                     const double2 *dold, double2 *dnew, const double2 *r, double2 *x, double2 *Ad,
-                     const double2 *U, const double2 *fd, const double2 *fr, const double2 *fU,
-                     double mass, int first, CGScalars *sc, double2 *partials, int tb0, int tbn,
-                     unsigned *counter) {
-    if (tbn <= 0) return;
-    CGFArgs a;
-    a.dold = dold; a.dnew = dnew; a.r = r; a.x = x; a.Ad = Ad; a.U = U;
-    a.fd = fd; a.fr = fr; a.fU = fU;
-    a.sc = sc; a.partials = partials;
-    a.V = g.V; a.Nx = g.Nx; a.Wt = g.Wt; a.t0 = g.t0; a.Ntg = g.Ntg; a.nshard = nshard;
-    a.xchunk = c.xchunk; a.NWT = c.NWT; a.TBk = c.TBk; a.XB = c.XB; a.remap = c.remap;
-    a.first = first;
-    a.mass = mass;
-    a.tb0 = tb0;
-    a.tbn = tbn;
-    a.part0 = tb0 * c.XB;  // disjoint partial slots per t-block range
-    a.counter = counter;
-    a.finalize = counter != nullptr;
-    hipLaunchKernelGGL(cg_fused_kernel, dim3(tbn * c.XB), dim3(256), 0, s, a);
-}
-
-// ---- pass 2: r -= alpha Ad ; partials <r, r>  (src/conjugate_gradient.cpp:39-43)
 constexpr int RB2 = 256;
-__global__ void __launch_bounds__(RB2) cg_update_r_kernel(long n, double2 *r, const double2 *Ad,
-                                                          CGScalars *sc, double2 *part, unsigned *counter) {
-    __shared__ double2 sh[RB2 / 64];
-    if (sc->done) return;
-    const double2 alpha = sc->alpha;
-    double2 acc = make_double2(0.0, 0.0);
-    const Chunk ch = block_chunk(n);
-    auto f = [&](long i) {
-        const double2 ri = csub(ld_nt(r + i), cmul(alpha, ld_nt(Ad + i)));
-        st_nt(r + i, ri);
-        acc = cadd(acc, cmul(ri, cconj(ri)));
-    };
-    long i = ch.beg + threadIdx.x;
-    for (; i + 3 * RB2 < ch.end; i += 4 * RB2) {
-        f(i);
-        f(i + RB2);
-        f(i + 2 * RB2);
-        f(i + 3 * RB2);
-    }
-    for (; i < ch.end; i += RB2) f(i);
-    const double2 s = block_sum(acc, sh);
-    if (!counter) {
-        if (threadIdx.x == 0) part[blockIdx.x] = s;
-    } else {  // last block: err, stop test, beta (src/conjugate_gradient.cpp:43-61)
-        if (threadIdx.x == 0) publish_partial(part + blockIdx.x, s);
-        __shared__ int last;
-        if (last_block_arrive(counter, gridDim.x, &last)) {
-            const double2 tot = sum_published_block(gridDim.x, part, sh);
-            if (threadIdx.x == 0) cg_beta_scalar(sc, tot);
-        }
-    }
-}
-
-void launch_cg_update_r(hipStream_t s, long n, double2 *r, const double2 *Ad, CGScalars *sc,
-                        double2 *part, unsigned *counter) {
-    hipLaunchKernelGGL(cg_update_r_kernel, dim3(reduce_blocks(n)), dim3(RB2), 0, s, n, r, Ad, sc, part,
-                       counter);
-}
-
-// ---- the deferred x update of the last executed iteration --------------------
-// x += alpha_{k-1} d_{k-1}, d_{k-1} in dbuf[k & 1] (k = iterations executed).
-__global__ void __launch_bounds__(RB2) cg_finish_x_kernel(long n, double2 *x, const double2 *d0,
-                                                          const double2 *d1, const CGScalars *sc) {
-    const int k = sc->k;
-    if (k < 1) return;
-    const double2 alpha = sc->alpha;
-    const double2 *d = (k & 1) ? d1 : d0;
-    const Chunk ch = block_chunk(n);
-    for (long i = ch.beg + threadIdx.x; i < ch.end; i += RB2) x[i] = cadd(x[i], cmul(alpha, d[i]));
-}
-
-void launch_cg_finish_x(hipStream_t s, long n, double2 *x, const double2 *d0, const double2 *d1,
-                        const CGScalars *sc) {
-    hipLaunchKernelGGL(cg_finish_x_kernel, dim3(reduce_blocks(n)), dim3(RB2), 0, s, n, x, d0, d1, sc);
-}
 
 // Two-direction form: after the last pass J = k (pass J evaluated into sc), an
 // odd J left alpha_{J-1} d_{J-1} out of x. A stopping evaluation keeps alpha =

@@ -42,30 +42,31 @@ int fail(int code, const char *fmt, ...);
 
 
 // Work fields, each 2*V complex (plane mu0 then mu1).
-// F_R2 / F_AD2: the second r / Ad buffers of the one-pass CG (ping-pong with F_R / F_AD).
-enum { F_IN, F_OUT, F_TMP, F_X, F_R, F_D, F_D2, F_T, F_AD, F_PHI, F_L, F_RR, F_R2, F_AD2, NFIELDS };
+// F_D, F_D2, F_R: the three d buffers of the one-pass CG paths (F_R is r in the
+// six-launch path); F_AD2: the second Ad buffer of the stored-Ad pass (ping-pong with F_AD).
+enum { F_IN, F_OUT, F_TMP, F_X, F_R, F_D, F_D2, F_T, F_AD, F_PHI, F_L, F_RR, F_AD2, NFIELDS };
 
 struct sm_ctx {
     int device = 0;
     int nshard = 1, shard = 0;
+    // RCCL loopback (sm_create_loopback): one shard driven through the t-shard
+    // code path, faces and scalar sums over a one-rank communicator (self
+    // send/recv). Tests the RCCL data path on a single GPU.
+    bool loop = false;
+    int debug_cg = 0;  // SM_DEBUG_CG=1: the CG host loops print their status at each check (stderr)
+    bool sharded() const { return nshard > 1 || loop; }  // faces + collectives (else periodic wrap)
+    int kshards() const { return sharded() ? 2 : 1; }    // the kernels' view: > 1 reads faces
     sm::Geometry g{};
     sm::LaunchCfg cfg{};
     sm::CGFusedCfg fcfg{};
     sm::CGFusedCfg racfg{};        // recompute-Ad CG pass (sm_cgra.hip)
-    // CG iteration: 0 six kernels, 1 two-pass fused (scalar kernels), 2 two-pass
-    // fused with in-kernel scalars, 3 one-pass (sm_cgfused.hip: 288 B/site,
-    // 0.979 vs 1.040 ms per iteration at 4096^2, tools/tune_cg.py), 4 the
-    // two-direction one-pass form (no r vector, x every other pass, 224
-    // B/site; 0.776 vs 1.013 ms per iteration at 4096^2), 5 the two-direction
-    // pass that recomputes Ad instead of storing it (sm_cgra.hip, 160 B/site).
-    // Chosen at creation: 5 where the grid is large or sharded, 4 on small
-    // one-shard grids (redundant in-kernel scalars, latency-bound).
+    // CG iteration: 0 the reference's six-launch sequence (576 B/site), 4 the
+    // two-direction one-pass form with a stored Ad (sm_cgfused.hip: no r
+    // vector, x every other pass, 224 B/site), 5 the two-direction pass that
+    // recomputes Ad instead of storing it (sm_cgra.hip, 160 B/site). Chosen at
+    // creation: 5 from 256^2 sites per shard, 4 below (latency-bound grids).
     int cg_fused = 4;
-    // one shard: alpha/beta by the last block of each pass instead of two
-    // one-block kernels. Measured equal at 4096^2 and 19 % slower at 1024^2
-    // (every block of a one-wave grid hits the ticket at once), so off by default.
-    int cg_inkernel = 0;
-    int cg_inkernel_max_blocks = sm::kInKernelScalarMaxBlocks;  // one-pass path (sm_cgfused.hip)
+    int cg_red_max_blocks = sm::kRedundantMaxBlocks;  // stored-Ad pass: redundant scalars up to this grid
     int cg_redundant = 1;           // those grids: every block evaluates the previous pass's scalars
     long cg_flush_pass = -1;        // last one-pass pass whose scalars still await evaluation
     int cg_flush_nparts = 0;        // its partial count (the one-pass or the recompute-Ad grid)
@@ -95,7 +96,6 @@ struct sm_ctx {
     double2 *sums = nullptr;       // 4 complex scratch (allreduce)
     double *Fbuf = nullptr;        // 2V doubles (force)
     sm::CGScalars *sc = nullptr;       // device
-    unsigned *counters = nullptr;  // device: last-block tickets (fused pass 1, pass 2)
     sm::CGScalars *h_sc = nullptr;     // pinned host mirror
     double2 *h_sums = nullptr;     // pinned host
     int nparts_dslash = 0, nparts_red = 0;

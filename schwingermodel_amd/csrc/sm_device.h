@@ -317,40 +317,4 @@ __device__ __forceinline__ void cg_beta_scalar(CGScalars *sc, double2 rr) {
     sc->rn = make_double2(err_sqr, 0.0);
 }
 
-// In-launch "last block reduces" hand-off (cdna_hip_programming.md §5 item 2,
-// its write-through form): every block publishes its partial with sc1
-// (write-through, agent-scope atomic) stores -- no release fence, which would
-// write back the XCD's whole dirty L2 in every block -- waits for them, then
-// takes a relaxed agent-scope ticket. The block drawing nblocks-1 reads all
-// partials with sc1 (agent atomic) loads and re-arms the counter (zeroed once
-// at context creation).
-__device__ __forceinline__ void publish_partial(double2 *slot, double2 v) {
-    __hip_atomic_store(&slot->x, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&slot->y, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ bool last_block_arrive(unsigned *counter, unsigned nblocks, int *sh_flag) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its sc1 stores are done
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = t == nblocks - 1;
-        if (last) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *sh_flag = last;
-    }
-    __syncthreads();
-    return *sh_flag != 0;
-}
-
-// Fixed-order sum of published partials, every load sc1 (agent atomic).
-__device__ __forceinline__ double2 sum_published_block(int nparts, double2 *part, double2 *sh) {
-    double2 acc = make_double2(0.0, 0.0);
-    for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
-        const double re = __hip_atomic_load(&part[i].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const double im = __hip_atomic_load(&part[i].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        acc = cadd(acc, make_double2(re, im));
-    }
-    return block_sum(acc, sh);
-}
-
 }  // namespace sm

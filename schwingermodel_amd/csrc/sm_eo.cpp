@@ -22,6 +22,8 @@
 // of both link parities) with the t +- 1 shards; dots are all-reduced.
 #include <cmath>
 
+#include <cstdio>
+
 #include "sm_ctx.h"
 #include "sm_fields.h"
 #include "sm_internal.h"
@@ -48,7 +50,7 @@ static double2 *eo_face(sm_ctx *c, int slot) { return c->eo_faces + (size_t)slot
 // holds d_{j-2}'s), 5 Ad_{j-1}.
 enum { EOF4_SEND, EOF4_UE, EOF4_UO, EOF4_D0, EOF4_D1, EOF4_AD, EOF4_N };
 static double2 *eo_face4(sm_ctx *c, int slot) { return c->eo_faces4 + (size_t)slot * 16 * c->g.Nx; }
-static bool eo_td_sharded_ok(const sm_ctx *c) { return c->nshard > 1 && c->g.Wt >= 8; }
+static bool eo_td_sharded_ok(const sm_ctx *c) { return c->sharded() && c->g.Wt >= 8; }
 
 static int eo_halo4(sm_ctx *c, const double2 *f, int slot) {
     double2 *snd = eo_face4(c, EOF4_SEND), *rcv = eo_face4(c, slot);
@@ -61,7 +63,7 @@ static int eo_halo4(sm_ctx *c, const double2 *f, int slot) {
 // received faces (null on one shard: the kernels wrap periodically).
 static int eo_halo(sm_ctx *c, const double2 *f, int slot, const double2 **out) {
     *out = nullptr;
-    if (c->nshard == 1) return SM_OK;
+    if (!c->sharded()) return SM_OK;
     double2 *snd = eo_face(c, EOF_SEND), *rcv = eo_face(c, slot);
     const size_t half = (size_t)4 * c->g.Nx;  // complex per side
     launch_pack_cb_faces(c->stream, c->g, f, snd);
@@ -72,7 +74,7 @@ static int eo_halo(sm_ctx *c, const double2 *f, int slot, const double2 **out) {
 
 static EoFaces u_faces(sm_ctx *c) {
     EoFaces f;
-    if (c->nshard > 1) {
+    if (c->sharded()) {
         f.ue = eo_face(c, EOF_UE);
         f.uo = eo_face(c, EOF_UO);
     }
@@ -85,12 +87,12 @@ int eo_ready(sm_ctx *c) {
     if (c->g.Wt % 2 || c->g.Nx % 2)
         return fail(SM_ERR_ARG, "even-odd preconditioning needs even Nx and shard width (%d x %d)", c->g.Nx,
                     c->g.Wt);
-    if (c->nshard > 1 && c->g.Wt < 4)
+    if (c->sharded() && c->g.Wt < 4)
         return fail(SM_ERR_ARG, "even-odd preconditioning needs t-shards at least 4 wide (Wt = %d)", c->g.Wt);
     if (!c->eo) {
         HIP_TRY(hipMalloc(&c->eo, sizeof(double2) * (size_t)EO_N * c->g.V));
         HIP_TRY(hipMalloc(&c->Ucb, sizeof(double2) * 2 * (size_t)c->g.V));
-        if (c->nshard > 1) HIP_TRY(hipMalloc(&c->eo_faces, sizeof(double2) * (size_t)EOF_N * 8 * c->g.Nx));
+        if (c->sharded()) HIP_TRY(hipMalloc(&c->eo_faces, sizeof(double2) * (size_t)EOF_N * 8 * c->g.Nx));
         if (eo_td_sharded_ok(c))
             HIP_TRY(hipMalloc(&c->eo_faces4, sizeof(double2) * (size_t)EOF4_N * 16 * c->g.Nx));
     }
@@ -158,7 +160,7 @@ static int eo_cg_folded(sm_ctx *c, const double2 *b, double2 *x, double mass, do
     TRY(eo_M(c, x, Ad, mass, &np));
     double2 *prr = c->partials, *ppp = c->partials + nred;
     launch_cg_init(c->stream, n, b, Ad, rb[0], db[0], prr, ppp);                // r_0 = b - M x_0; d_0 = r_0
-    if (c->nshard == 1) {
+    if (!c->sharded()) {
         launch_cg_finalize_init(c->stream, nred, prr, ppp, c->sc, tol);
     } else {
         launch_sum_partials(c->stream, nred, prr, c->sums);
@@ -189,7 +191,7 @@ static int eo_cg_folded(sm_ctx *c, const double2 *b, double2 *x, double mass, do
         launch_eo_cg_pass(c->stream, c->g, cfg, 0, q, ucb(c, 0), ucb(c, 1), mass, f, c->sc, c->partials);
         TRY(eo_halo(c, W, EOF_W, &q.wf));
         launch_eo_cg_pass(c->stream, c->g, cfg, 1, q, ucb(c, 0), ucb(c, 1), mass, f, c->sc, c->partials);
-        if (c->nshard == 1) {
+        if (!c->sharded()) {
             launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, q.first);
         } else {
             launch_cg1_local_sum(c->stream, nparts, c->partials, c->sc);
@@ -238,7 +240,7 @@ static int eo_cg_twodir(sm_ctx *c, const double2 *b, double2 *x, double mass, do
     TRY(eo_M(c, x, eo_vec(c, EO_AD), mass, &np));
     double2 *prr = c->partials, *ppp = c->partials + nred;
     launch_cg_init(c->stream, n, b, eo_vec(c, EO_AD), eo_vec(c, EO_R), eo_vec(c, EO_D), prr, ppp);  // r_0, d_0
-    if (c->nshard == 1) {
+    if (!c->sharded()) {
         launch_cg_finalize_init(c->stream, nred, prr, ppp, c->sc, tol);
     } else {
         launch_sum_partials(c->stream, nred, prr, c->sums);
@@ -259,7 +261,7 @@ static int eo_cg_twodir(sm_ctx *c, const double2 *b, double2 *x, double mass, do
         const double2 *d2 = j >= 2 ? dbuf(j - 2) : d1;
         const double2 *aold = first ? d1 : abuf[(j - 1) & 1];
         EoTdFaces f;
-        if (c->nshard > 1) {  // faces of d_{j-1} (d_{j-2}'s are the previous pass's) and Ad_{j-1}
+        if (c->sharded()) {  // faces of d_{j-1} (d_{j-2}'s are the previous pass's) and Ad_{j-1}
             const int sd = (j & 1) ? EOF4_D1 : EOF4_D0, sp = (j & 1) ? EOF4_D0 : EOF4_D1;
             TRY(eo_halo4(c, d1, sd));
             f.d1 = eo_face4(c, sd);
@@ -271,7 +273,7 @@ static int eo_cg_twodir(sm_ctx *c, const double2 *b, double2 *x, double mass, do
         }
         launch_eo_td(c->stream, c->g, cfg, d1, d2, aold, dbuf(j), abuf[j & 1], x, ucb(c, 0), ucb(c, 1), mass, j,
                      c->sc, c->partials, f);
-        if (c->nshard == 1) {
+        if (!c->sharded()) {
             launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
         } else {
             launch_cg1_local_sum(c->stream, nparts, c->partials, c->sc);
@@ -290,6 +292,9 @@ static int eo_cg_twodir(sm_ctx *c, const double2 *b, double2 *x, double mass, do
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(c->h_sc, c->sc, sizeof(CGScalars), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
+        if (c->debug_cg)
+            fprintf(stderr, "[sm eo_cg shard %d/%d] pass %ld k %d err %.3e target %.3e done %d\n", c->shard, c->nshard, j,
+                    c->h_sc->k, c->h_sc->err, tol * c->h_sc->phi_norm, c->h_sc->done);
         if (c->h_sc->done) break;
         chunk = plan.next(c->h_sc->k, c->h_sc->err, tol * c->h_sc->phi_norm);
     }
@@ -307,7 +312,7 @@ static int eo_cg_twodir(sm_ctx *c, const double2 *b, double2 *x, double mass, do
 // CG on Dhat Dhat^dag x = b (x0 = b, the reference's convention), the
 // reference's recurrence and stop test on half-lattice vectors.
 int eo_cg(sm_ctx *c, const double2 *b, double2 *x, double mass, double tol, int max_iter, sm_cg_result *res) {
-    if (c->eo_cg_td && (c->nshard == 1 || eo_td_sharded_ok(c))) return eo_cg_twodir(c, b, x, mass, tol, max_iter, res);
+    if (c->eo_cg_td && (!c->sharded() || eo_td_sharded_ok(c))) return eo_cg_twodir(c, b, x, mass, tol, max_iter, res);
     if (c->eo_cg_folded && c->eo_fused) return eo_cg_folded(c, b, x, mass, tol, max_iter, res);
     const long n = c->g.V;  // complex entries of an even vector
     const int nparts = reduce_blocks(n);
@@ -317,7 +322,7 @@ int eo_cg(sm_ctx *c, const double2 *b, double2 *x, double mass, double tol, int 
     TRY(eo_M(c, x, Ad, mass, &np));                          // (its dot partials are not used)
     double2 *prr = c->partials, *ppp = c->partials + nparts;
     launch_cg_init(c->stream, n, b, Ad, r, d, prr, ppp);
-    if (c->nshard == 1) {
+    if (!c->sharded()) {
         launch_cg_finalize_init(c->stream, nparts, prr, ppp, c->sc, tol);
     } else {
         launch_sum_partials(c->stream, nparts, prr, c->sums);

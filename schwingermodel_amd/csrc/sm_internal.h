@@ -111,21 +111,15 @@ struct CGFusedCfg {
 };
 CGFusedCfg cg_fused_config(const Geometry &g);
 int cg_fused_blocks(const CGFusedCfg &c);
-void launch_cg_fused(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard,
-                     const double2 *dold, double2 *dnew, const double2 *r, double2 *x, double2 *Ad,
-                     const double2 *U, const double2 *fd, const double2 *fr, const double2 *fU,
-                     double mass, int first, CGScalars *sc, double2 *partials, int tb0, int tbn,
-                     unsigned *counter);  // counter != null: last block computes alpha
-// One-pass iteration (pass 2 folded into the next pass): partials are 3 per block.
+// The two-direction one-pass iteration with a stored Ad (mode 4): partials are
+// 3 per block; d_{j-1} in dold, d_{j-2} in rold (faces fd / fr), Ad_{j-1} in aold.
 void launch_cg_onepass(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard,
                        const double2 *dold, const double2 *rold, const double2 *aold, double2 *dnew,
-                       double2 *rnew, double2 *anew, double2 *x, const double2 *U, const double2 *fd,
-                       const double2 *fr, const double2 *fa, const double2 *fU, double mass, int first,
-                       CGScalars *sc, double2 *partials, int tb0, int tbn,
-                       unsigned *counter,   // counter != null: the last block forms the scalars
+                       double2 *anew, double2 *x, const double2 *U, const double2 *fd, const double2 *fr,
+                       const double2 *fa, const double2 *fU, double mass, int first, CGScalars *sc,
+                       double2 *partials, int tb0, int tbn,
                        const double2 *prev_partials = nullptr,  // != null: redundant scalars (see below)
-                       long pass = 0,
-                       int twodir = 0);  // two-direction form: rold/fr = d_{j-2}, rnew unused
+                       long pass = 0);
 // Two-direction pass that recomputes Ad_{j-1} = D D^dag d_{j-1} in-kernel
 // instead of storing Ad (sm_cgra.hip): 160 B/site; d_i in d[i % 3] as below.
 // Faces (t-shard, 4-deep [col -4..-1, Wt..Wt+3][plane][x]): f1 = d_{j-1},
@@ -151,16 +145,12 @@ void launch_cg_td_finish_x(hipStream_t s, long n, double2 *x, const double2 *d0,
 // launch_cg1_flush evaluates the last issued pass's partials into sc for the
 // host (idempotent: the next pass recomputes the same state).
 void launch_cg1_flush(hipStream_t s, int nparts, const double2 *partials, CGScalars *sc, long pass);
-// one-pass: in-kernel scalars up to this grid size (64^2: 64 blocks, 12.2 vs 14.2 us per
-// iteration; 256^2: 512 blocks, 18.9 vs 17.0 us -- the ticket contends; tools/tune_cg.py)
-constexpr int kInKernelScalarMaxBlocks = 128;
+// stored-Ad pass: redundant scalars up to this grid size (64^2: 64 blocks, 11.2 vs 12.0 us per
+// iteration with a scalar ticket; 128^2 11.6 vs 12.9 us)
+constexpr int kRedundantMaxBlocks = 128;
 void launch_cg1_scalars(hipStream_t s, int nparts, const double2 *partials, CGScalars *sc, int first);
 void launch_cg1_local_sum(hipStream_t s, int nparts, const double2 *partials, CGScalars *sc);
 void launch_cg1_from_sums(hipStream_t s, CGScalars *sc, int first);
-void launch_cg_update_r(hipStream_t s, long n, double2 *r, const double2 *Ad, CGScalars *sc,
-                        double2 *part, unsigned *counter);  // counter != null: last block: beta
-void launch_cg_finish_x(hipStream_t s, long n, double2 *x, const double2 *d0, const double2 *d1,
-                        const CGScalars *sc);
 void launch_pack_faces2(hipStream_t s, const Geometry &g, const double2 *field, double2 *lo,
                         double2 *hi);
 

@@ -30,7 +30,7 @@ int ensure_md(sm_ctx *c) {
     return SM_OK;
 }
 
-const double2 *ufaces(sm_ctx *c) { return c->nshard == 1 ? nullptr : face2_recv(c, 2); }
+const double2 *ufaces(sm_ctx *c) { return !c->sharded() ? nullptr : face2_recv(c, 2); }
 
 int check_params(const sm_hmc_params *p) {
     if (!p) return fail(SM_ERR_ARG, "null params");
@@ -51,7 +51,7 @@ int gauge_sum(sm_ctx *c, int nparts, double2 *out) {
 }
 
 int plaquette_sums(sm_ctx *c, double beta, double *sp, double *action, double2 *field) {
-    launch_plaquette(c->stream, c->g, c->nshard, c->U, ufaces(c), beta, field, c->partials);
+    launch_plaquette(c->stream, c->g, c->kshards(), c->U, ufaces(c), beta, field, c->partials);
     HIP_TRY(hipGetLastError());
     double2 s;
     TRY(gauge_sum(c, gauge_reduce_blocks(c->g), &s));
@@ -122,7 +122,7 @@ int sm_staples(sm_ctx *c, double *S0, double *S1) {
     if (!S0 || !S1) return fail(SM_ERR_ARG, "null argument");
     HIP_TRY(hipSetDevice(c->device));
     double2 *S = c->field(F_OUT);
-    launch_staple_force(c->stream, c->g, c->nshard, c->U, ufaces(c), 0.0, nullptr, S);
+    launch_staple_force(c->stream, c->g, c->kshards(), c->U, ufaces(c), 0.0, nullptr, S);
     HIP_TRY(hipGetLastError());
     return download_plane_pair(c, S, S0, S1);
 }
@@ -133,7 +133,7 @@ int sm_gauge_force(sm_ctx *c, double beta, double *F0, double *F1) {
     HIP_TRY(hipSetDevice(c->device));
     TRY(ensure_md(c));
     TRY(upload_real_pair(c, c->Fmd, F0, F1));
-    launch_staple_force(c->stream, c->g, c->nshard, c->U, ufaces(c), beta, c->Fmd, nullptr);
+    launch_staple_force(c->stream, c->g, c->kshards(), c->U, ufaces(c), beta, c->Fmd, nullptr);
     HIP_TRY(hipGetLastError());
     return download_real_pair(c, c->Fmd, F0, F1);
 }
@@ -151,7 +151,7 @@ int sm_md_force_dev(sm_ctx *c, const sm_hmc_params *p, const double *phi, double
         TRY(apply(c, psi, T, p->m0 + 2, 1, nullptr, nullptr, nullptr));                 // TEMP = D^dag psi
         TRY(sm_force_dev(c, (const double *)psi, (const double *)T, F));                 // fermion bilinear
     }
-    launch_staple_force(c->stream, c->g, c->nshard, c->U, ufaces(c), p->beta, F, nullptr);  // Force_G
+    launch_staple_force(c->stream, c->g, c->kshards(), c->U, ufaces(c), p->beta, F, nullptr);  // Force_G
     HIP_TRY(hipGetLastError());
     return SM_OK;
 }

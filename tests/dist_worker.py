@@ -198,18 +198,23 @@ def eo_ops(sm, ctx, V, fields, m0, prm):
     P_ = lambda x: ctypes.c_void_p(x.ctypes.data)  # noqa: E731
     (U0, U1), (p0, p1), (f0, f1) = fields
     out = {}
+    step = lambda m: print(f"[eo_ops V={V}] {m}", file=sys.stderr, flush=True)  # noqa: E731
+    step("dhat")
     for key, dag in (("dhat", 0), ("dhatdag", 1)):
         o0, o1 = np.empty(V, complex), np.empty(V, complex)
         sm.check(sm.lib.sm_eo_dhat(ctx, dag, P_(p0), P_(p1), P_(o0), P_(o1), m0))
         out[key] = (o0, o1)
     x0, x1 = np.empty(V, complex), np.empty(V, complex)
     res = sm.CGResult()
+    step("eo_cg")
     sm.check(sm.lib.sm_eo_cg(ctx, P_(p0), P_(p1), P_(x0), P_(x1), m0, 1e-10, 10000, ctypes.byref(res)))
+    step(f"eo_cg done {res.converged} {res.iterations}")
     out["cgx"] = (x0, x1)
     out["cg"] = (res.converged, res.iterations)
     G0, G1 = np.empty(V), np.empty(V)
     sm.check(sm.lib.sm_md_force(ctx, ctypes.byref(prm), P_(f0), P_(f1), P_(G0), P_(G1), ctypes.byref(res)))
     out["force"] = (G0, G1)
+    step("trajectory")
     r = sm.HMCResult()
     sm.check(sm.lib.sm_hmc_trajectory(ctx, ctypes.byref(prm), 5, ctypes.byref(r)))
     Ua, Ub = np.empty(V, complex), np.empty(V, complex)
@@ -407,8 +412,10 @@ def main():
     mode, name, result_path = sys.argv[1], sys.argv[2], sys.argv[3]
     import datetime
     import torch.distributed as dist
+    print(f"[worker {os.environ.get('RANK')}] init_process_group", file=sys.stderr, flush=True)
     dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=20))
     rank, world = dist.get_rank(), dist.get_world_size()
+    print(f"[worker {rank}/{world}] {mode} {name}", file=sys.stderr, flush=True)
     if mode == "md":
         return run_md(name, result_path, dist, rank, world)
     if mode == "eo":
@@ -510,4 +517,9 @@ def main():
 
 
 if __name__ == "__main__":
+    import faulthandler
+    import signal
+    faulthandler.register(signal.SIGUSR1, all_threads=True)  # distutil.run_world: stack dump on a timeout
+    if os.environ.get("SM_WORKER_WATCHDOG"):  # thread-based dump, works whatever the main thread is doing
+        faulthandler.dump_traceback_later(float(os.environ["SM_WORKER_WATCHDOG"]), exit=False)
     main()

@@ -195,6 +195,31 @@ def make_md(name, nx, nt, sigma, m0, beta, tau, steps, mpi=None):
     return meta
 
 
+# Gauge-configuration files written by the reference's SaveConf (28-byte
+# records) on a 1-rank and a 2x2 decomposition (MPI_Gatherv displacements),
+# plus the field its readBinary reads back: name, Nx, Nt, sigma, ranks (rx, rt)
+CONF_FIXTURES = [("conf8x8_hot", 8, 8, -1.0, (1, 1)), ("conf32x48_b3", 32, 48, 0.3246, (2, 2))]
+
+
+def make_conf(name, nx, nt, sigma, ranks, mpirun):
+    exe = os.path.join(REF_DIR, f"sm_ref_{nx}x{nt}")
+    rx, rt = ranks
+    with tempfile.TemporaryDirectory() as d:
+        run([exe, "gen", d, str(SEED_U), repr(sigma), str(SEED_PSI), str(SEED_CHI)])
+        cmd = [exe, "conf", d, str(rx), str(rt)]
+        run(cmd if rx * rt == 1 else [mpirun, "-n", str(rx * rt)] + cmd, timeout=300)
+        U = np.fromfile(os.path.join(d, "U.bin"), dtype=np.float64)
+        with open(os.path.join(d, "ref_conf.ctxt"), "rb") as f:
+            raw = f.read()
+        with open(os.path.join(HERE, name + ".ctxt"), "wb") as f:
+            f.write(raw)
+        back = np.fromfile(os.path.join(d, "ref_conf_read.bin"), dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), U=U, ref_conf_read=back)
+    return {"Nx": nx, "Nt": nt, "sigma": sigma, "ranks_x": rx, "ranks_t": rt, "file": name + ".npz",
+            "ctxt": name + ".ctxt", "bytes": len(raw), "sha256": hashlib.sha256(raw).hexdigest(),
+            "program": "reference SaveConf then GaugeConf::readBinary (src/gauge_conf.cpp:378-423, 495-546)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mpi", action="store_true", help="also run 2x2 ranks (mpirun)")
@@ -204,7 +229,19 @@ def main():
     ap.add_argument("--md-only", action="store_true", help="regenerate only the MD fixtures")
     ap.add_argument("--hmc-stat", action="store_true", help="(re)run the reference HMC program (~2 min)")
     ap.add_argument("--hmc-log-dir", default=None, help="reuse a finished reference HMC run directory")
+    ap.add_argument("--conf-only", action="store_true", help="regenerate only the SaveConf fixtures")
     args = ap.parse_args()
+    if args.conf_only:
+        sizes = sorted({f"{nx}x{nt}" for _, nx, nt, *_ in CONF_FIXTURES})
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref", "REF_SIZES=" + " ".join(sizes)],
+                       check=True)
+        path = os.path.join(HERE, "manifest.json")
+        with open(path) as f:
+            manifest = json.load(f)
+        manifest["conf"] = {n: make_conf(n, nx, nt, sg, rk, args.mpirun) for n, nx, nt, sg, rk in CONF_FIXTURES}
+        with open(path, "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+        return
     if args.hmc_stat:
         path = os.path.join(HERE, "manifest.json")
         with open(path) as f:
@@ -273,6 +310,7 @@ def main():
     manifest["md_params"] = {"seed_P": SEED_P, "P": "numpy default_rng(seed_P).standard_normal(2S)",
                              "cg": {"tol": 1e-10, "max_iter": 10000}}
     manifest["jackknife"] = make_jackknife()
+    manifest["conf"] = {n: make_conf(n, nx, nt, sg, rk, args.mpirun) for n, nx, nt, sg, rk in CONF_FIXTURES}
     if args.large:
         subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref", "REF_SIZES=1024x1024"], check=True)
         manifest["large"] = {}

@@ -101,6 +101,34 @@ def test_gauge_conf_binary_format(tmp_path):
     assert lib.sm_conf_read(str(tmp_path / "missing").encode(), Nx, Nt, b0.ctypes.data, b1.ctypes.data) != 0
 
 
+@pytest.mark.parametrize("name", ["conf8x8_hot", "conf32x48_b3"])
+def test_conf_io_matches_reference_saveconf(tmp_path, name):
+    """Pinned to the reference itself: tests/golden/<name>.ctxt was written by
+    the reference's SaveConf (src/gauge_conf.cpp:378-423; conf32x48 on 2x2 MPI
+    ranks, through its MPI_Gatherv displacements) from the fixture's U, and
+    ref_conf_read is what its GaugeConf::readBinary (:495-546) read back.
+    sm_conf_write must produce the same bytes, sm_conf_read the same field."""
+    import hashlib
+    import json
+    from conftest import GOLDEN
+    meta = json.load(open(os.path.join(GOLDEN, "manifest.json")))["conf"][name]
+    Nx, Nt = meta["Nx"], meta["Nt"]
+    S = Nx * Nt
+    with np.load(os.path.join(GOLDEN, meta["file"]), allow_pickle=False) as z:
+        U, read_back = z["U"].copy(), z["ref_conf_read"].copy()
+    ref_bytes = open(os.path.join(GOLDEN, meta["ctxt"]), "rb").read()
+    assert hashlib.sha256(ref_bytes).hexdigest() == meta["sha256"]
+    u0, u1 = planes(U, S)
+    path = str(tmp_path / "conf.ctxt")
+    assert lib.sm_conf_write(path.encode(), Nx, Nt, u0.ctypes.data, u1.ctypes.data) == 0
+    assert open(path, "rb").read() == ref_bytes
+    back = np.empty(4 * S)
+    b0, b1 = planes(back, S)
+    assert lib.sm_conf_read(os.path.join(GOLDEN, meta["ctxt"]).encode(), Nx, Nt, b0.ctypes.data,
+                            b1.ctypes.data) == 0
+    assert bits_equal(back, read_back) and bits_equal(back, U)
+
+
 def test_no_gpu_fails_loudly():
     try:
         import torch

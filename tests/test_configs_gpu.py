@@ -75,12 +75,13 @@ def test_config_single_gpu_cg(oracle, N, sigma, m0, modes):
         L.close()
 
 
+@pytest.mark.multiproc
 @pytest.mark.parametrize("case,world,xtol", [
     ("big:4096x4096:0.2374:-0.06:full", 8, 1e-12),   # config 4: Wt = 512 per shard
     ("big:8192x8192:0.4242:-0.19:cg", 8, 1e-10),     # config 5: 8192 x 1024 per shard
 ])
 def test_config_sharded_vs_one_shard(tmp_path, case, world, xtol):
-    rep = run_world("big", case, world, tmp_path, timeout=1500)
+    rep = run_world("big", case, world, tmp_path, timeout=160)
     for k, ok in rep["bitwise"].items():
         assert ok is True, (k, rep)
     one_conv, one_it = rep["one_cg"]

@@ -10,7 +10,7 @@ import pytest
 
 from distutil import run_world
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.multiproc]
 
 
 @pytest.mark.parametrize("fixture,world", [("l64x64_b2_m0", 2), ("l32x48_b3_m-0p10", 4),
@@ -23,7 +23,7 @@ def test_sharded_gpu_path_matches_reference(tmp_path, fixture, world):
     # bt = 64 so the Dirac apply of the larger shards also splits into interior
     # and edge t-blocks (the overlapped halo path)
     env = {"SM_BT": "64"} if fixture.startswith("gen:") else None
-    rep = run_world("gpu", fixture, world, tmp_path, timeout=600, extra_env=env)
+    rep = run_world("gpu", fixture, world, tmp_path, timeout=140, extra_env=env)
     c = rep["checks"]
     for k in ("ref_Dpsi", "ref_Ddagchi", "ref_DDdagpsi", "ref_force"):
         assert c[k] is True, (k, c)
@@ -38,7 +38,7 @@ def test_sharded_gpu_path_matches_reference(tmp_path, fixture, world):
 def test_sharded_twodir_cg_matches_reference(tmp_path, fixture, world):
     """The two-direction CG (SM_CG_FUSED=4: d_{j-2} faces instead of r faces)
     on t-shards: the reference's iteration count and solution."""
-    rep = run_world("gpu", fixture, world, tmp_path, timeout=600, extra_env={"SM_CG_FUSED": "4"})
+    rep = run_world("gpu", fixture, world, tmp_path, timeout=140, extra_env={"SM_CG_FUSED": "4"})
     assert rep["checks"]["ref_cgx"] <= 1e-12
     ref = rep["ref_cg_iters"]
     assert len(set(rep["cg_iters"])) == 1 and abs(rep["cg_iters"][0] - ref) <= max(1, ref // 100)
@@ -54,7 +54,7 @@ def test_sharded_recompute_cg_matches_reference(tmp_path, fixture, world):
     interior/edge split of Wt = 512 / 240, the narrowest shard it takes (Wt = 4)
     and the fall-back to the stored-Ad pass below it (Wt = 2): the reference's
     iteration count and solution."""
-    rep = run_world("gpu", fixture, world, tmp_path, timeout=600, extra_env={"SM_CG_FUSED": "5"})
+    rep = run_world("gpu", fixture, world, tmp_path, timeout=140, extra_env={"SM_CG_FUSED": "5"})
     assert rep["checks"]["ref_cgx"] <= 1e-12
     ref = rep["ref_cg_iters"]
     assert len(set(rep["cg_iters"])) == 1 and abs(rep["cg_iters"][0] - ref) <= max(1, ref // 100)
@@ -66,7 +66,7 @@ def test_sharded_md_matches_reference(tmp_path, fixture, world):
     """MD layer on t-shards: bitwise plaquette / staples / gauge force, the
     CG-dependent MD force, leapfrog and Hamiltonians within the test_md_gpu
     tolerances, and an HMC trajectory equal to the one-shard trajectory."""
-    rep = run_world("md", fixture, world, tmp_path, timeout=900)
+    rep = run_world("md", fixture, world, tmp_path, timeout=140)
     c = rep["checks"]
     for k in ("ref_plaq", "ref_staple", "ref_gforce"):
         assert c[k] is True, (k, c)
@@ -101,7 +101,7 @@ def test_sharded_even_odd_matches_one_shard(tmp_path, fixture, world, fused, fol
     vs one shard: Dhat / Dhat^dag bitwise (same per-element arithmetic), the
     half-lattice CG to 1e-10 in the same iteration count (+-1 %), the MD force
     to 1e-10, and an HMC trajectory with the same accept decision."""
-    rep = run_world("eo", fixture, world, tmp_path, timeout=600,
+    rep = run_world("eo", fixture, world, tmp_path, timeout=140,
                     extra_env={"SM_EO_FUSED": fused, "SM_EO_CG_FOLDED": folded, "SM_EO_CG_TD": td})
     c = rep["checks"]
     assert c["dhat"] is True and c["dhatdag"] is True, c

@@ -3,7 +3,7 @@ export TMPDIR=/tmp
 T=${1:-cur}
 mkdir -p gpurun_out
 rm -rf gpurun_out/prof_stats_$T gpurun_out/prof_fetch_$T gpurun_out/prof_write_$T
-timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gputests_$T.log 2>&1 &&
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 170 --timeout-method thread > gpurun_out/gputests_$T.log 2>&1 &&
 timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke_$T.log 2>&1 &&
 timeout -k 10 400 python3 bench.py > gpurun_out/bench_$T.log 2>&1 &&
 timeout -k 10 200 python tools/tune_cg.py --n 4096 --paths twodir,recompute --xchunk 0 --iters 40 --rounds 3 > gpurun_out/tune4096_$T.log 2>&1 &&

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Small-lattice CG latency probe (the HMC config-1 regime, 32^2 .. 512^2).
 
-    python tools/small_cg.py [--sizes 32,64,128,256] [--paths onepass,fused,sixkernel,small]
+    python tools/small_cg.py [--sizes 32,64,128,256] [--paths twodir,recompute,sixkernel]
 
 Per size and CG path: a full solve through sm_cg_dev (tol 1e-10, host status
 polling included: wall-clock us per iteration) and a fixed-length device
@@ -18,13 +18,13 @@ import time
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-PATHS = {"sixkernel": 0, "fused": 1, "fused_inkernel": 2, "onepass": 3, "twodir": 4, "recompute": 5}
+PATHS = {"sixkernel": 0, "twodir": 4, "recompute": 5}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", default="32,64,128,256")
-    ap.add_argument("--paths", default="onepass,fused,sixkernel")
+    ap.add_argument("--paths", default="twodir,recompute,sixkernel")
     ap.add_argument("--m0", type=float, default=0.0)
     ap.add_argument("--sigma", type=float, default=0.4242)
     ap.add_argument("--iters", type=int, default=200)

@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--sixkernel", action="store_true")
-    ap.add_argument("--paths", default="fused", help="comma list of fused (two-pass), fused2 (in-kernel scalars), onepass, twodir, recompute")
+    ap.add_argument("--paths", default="recompute", help="comma list of twodir (stored Ad), recompute, sixkernel")
     a = ap.parse_args()
     import torch
     import schwingermodel_amd as sm
@@ -47,7 +47,7 @@ def main():
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(a.rounds):
         for c in configs:
-            sm.check(sm.lib.sm_tune_cg(L.ctx, {"fused": 1, "fused2": 2, "onepass": 3, "twodir": 4, "recompute": 5, "sixkernel": 0}[c[0]], c[1]))
+            sm.check(sm.lib.sm_tune_cg(L.ctx, {"twodir": 4, "recompute": 5, "sixkernel": 0}[c[0]], c[1]))
             sm.check(sm.lib.sm_cg_begin(L.ctx, vp(dp.data_ptr()), vp(x.data_ptr()), -0.06, 0.0))
             sm.check(sm.lib.sm_cg_iterate(L.ctx, 3))
             e0.record(s)
