@@ -52,6 +52,60 @@ def test_dropin_harness_matches_reference(tmp_path, name, size):
     assert '"cg_converged": 1' in r.stdout
 
 
+MPIEXEC = "/opt/conda/bin/mpiexec"
+
+
+@pytest.mark.multiproc
+@pytest.mark.parametrize("rx,rt", [(1, 2), (2, 1), (2, 2), (2, 4)])
+def test_dropin_multirank_matches_reference(tmp_path, rx, rt):
+    """The reference's own fixture driver on rx x rt MPI ranks (MPICH) over the
+    shim: each t-column's ranks gather to their leader, the rt leaders run the
+    t-shards of the GPU path (several leaders share this one GPU, so the shim
+    picks its MPI host-staged transport), results scattered back. Bitwise
+    against the 1-rank reference for D, D^dag, D D^dag and the force (the
+    reference itself is decomposition-invariant there), 1e-12 for CG."""
+    exe = os.path.join(REF, "sm_dropin_32x48")
+    if not os.path.exists(exe) or not os.path.exists(MPIEXEC):
+        pytest.skip("drop-in binary or MPICH not available")
+    meta, a = load_fixture("l32x48_b3_m-0p10")
+    for k in ("U", "psi", "chi"):
+        a[k].tofile(tmp_path / f"{k}.bin")
+    r = subprocess.run([MPIEXEC, "-n", str(rx * rt), exe, "fixture", str(tmp_path), str(rx), str(rt),
+                        repr(meta["m0"]), "1e-10", "10000"], capture_output=True, text=True, env=env(), timeout=150)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    out = {k: np.fromfile(tmp_path / f"{k}.bin", dtype=np.float64)
+           for k in ("ref_Dpsi", "ref_Ddagchi", "ref_DDdagpsi", "ref_force", "ref_cgx")}
+    for k in ("ref_Dpsi", "ref_Ddagchi", "ref_DDdagpsi", "ref_force"):
+        assert bits_equal(out[k], a[k]), k
+    x, xr = out["ref_cgx"], a["ref_cgx"]
+    assert np.linalg.norm(x - xr) / np.linalg.norm(xr) <= 1e-12
+    assert '"cg_converged": 1' in r.stdout
+
+
+@pytest.mark.multiproc
+def test_reference_hmc_program_multirank(tmp_path):
+    """The reference HMC program (src/main.cpp) on 2 x 2 MPI ranks over the
+    shim: two t-column leaders drive two t-shards on this GPU (MPI host-staged
+    transport), the reference's gauge/MD code runs its own 2 x 2 halo
+    exchanges. Statistical check against the CPU reference's 1-rank numbers
+    (its RNG is clock-seeded, src/main.cpp:17)."""
+    exe = os.path.join(REF, "SM_64x64_hip")
+    if not os.path.exists(exe) or not os.path.exists(MPIEXEC):
+        pytest.skip("drop-in HMC binary or MPICH not available")
+    params = "2\n2\n0\n10\n0.3\n2\n30\n20\n1\n0\n"
+    r = subprocess.run([MPIEXEC, "-n", "4", exe], input=params, capture_output=True, text=True, env=env(),
+                       cwd=tmp_path, timeout=150)
+    assert r.returncode == 0, r.stderr[-2000:]
+    sim = [f for f in os.listdir(tmp_path) if f.endswith("_SimData.txt")]
+    assert sim, r.stdout[-2000:]
+    lines = open(tmp_path / sim[0]).read().split("\n")
+    ep = float(lines[lines.index("#Ep                           #dEp") + 1].split()[0])
+    acc = float(lines[lines.index("#Acceptance rate") + 1].split()[0])
+    assert 0.69 < ep < 0.75, (ep, acc)
+    assert 0.5 < acc <= 1.0, acc
+    assert "did not converge" not in r.stdout
+
+
 def test_reference_hmc_program_on_gpu(tmp_path):
     exe = os.path.join(REF, "SM_64x64_hip")
     if not os.path.exists(exe):
