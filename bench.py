@@ -46,6 +46,9 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_SITE_APPLY = 96  # read psi 32 + U 32, write 32
 # algorithmic HBM bytes per site of one CG iteration, by path
 BYTES_PER_SITE_CG = {"recompute": 160, "twodir": 224, "sixkernel": 576}
+# the recompute-Ad pass reading the links as angles (sm_cg_link_angles): U is
+# 16 instead of 32 B/site of every pass
+BYTES_PER_SITE_CG_ANGLES = 144
 CG_PATH_ID = {"recompute": 5, "twodir": 4, "sixkernel": 0}
 
 # BASELINE.json configs on the GPU (1 and 2 are the CPU-plumbing / 1024^2 parity cases)
@@ -78,6 +81,8 @@ def parse(argv=None):
                     help="multi-GPU wire: RCCL (production) or the host-staged test transport")
     ap.add_argument("--device", type=int, default=None, help="override the rank -> GPU mapping")
     ap.add_argument("--cg-path", choices=list(CG_PATH_ID), default="recompute")
+    ap.add_argument("--no-link-angles", action="store_true",
+                    help="recompute-Ad CG reads the complex links (160 B/site) instead of their angles (144)")
     return ap.parse_args(argv)
 
 
@@ -310,12 +315,21 @@ def time_applies(rt, sh, m0, n):
     return e0.elapsed_time(e1) / 1e3 / n
 
 
-def time_cg_steps(rt, sh, m0, cg_path, warmup, steps):
+def cg_bytes_per_site(sh, cg_path):
+    """Algorithmic bytes per site of the CG iteration the last solve ran."""
+    sm = sh.sm
+    u = ctypes.c_int(0)
+    sm.check(sm.lib.sm_cg_link_angles(sh.L.ctx, -1, ctypes.byref(u)))
+    return BYTES_PER_SITE_CG_ANGLES if (cg_path == "recompute" and u.value) else BYTES_PER_SITE_CG[cg_path]
+
+
+def time_cg_steps(rt, sh, m0, cg_path, warmup, steps, link_angles_off=False):
     """K CG iterations (tol = 0: never converges, the full work every step)
     bracketed by a barrier + device synchronisation on both sides."""
     import torch
     sm = sh.sm
     sm.check(sm.lib.sm_tune_cg(sh.L.ctx, CG_PATH_ID[cg_path], 0))
+    sm.check(sm.lib.sm_cg_link_angles(sh.L.ctx, 0 if link_angles_off else 1, None))
     sm.check(sm.lib.sm_cg_begin(sh.L.ctx, sh.p(sh.phi), sh.p(sh.x), m0, 0.0))
     sm.check(sm.lib.sm_cg_iterate(sh.L.ctx, warmup))
     barrier(rt)
@@ -334,7 +348,7 @@ def time_cg_steps(rt, sh, m0, cg_path, warmup, steps):
     if res.iterations != warmup + steps - setup_passes or res.converged != 0:
         raise SystemExit(f"CG ran {res.iterations} iterations (converged={res.converged}), "
                          f"expected {warmup + steps - setup_passes}")
-    return max(wall, c0.elapsed_time(c1) / 1e3)
+    return max(wall, c0.elapsed_time(c1) / 1e3), cg_bytes_per_site(sh, cg_path)
 
 
 def true_relres(sh, m0):
@@ -380,7 +394,7 @@ def run_config34(args, rt, cfg_id):
     m0, world, rank = cfg["m0"], rt["world"], rt["rank"]
     sh = Shard(rt, Nx, Nt, cfg["sigma"])
     apply_s = time_applies(rt, sh, m0, args.applies)
-    t_cg = time_cg_steps(rt, sh, m0, args.cg_path, args.warmup, args.steps)
+    t_cg, cg_bps = time_cg_steps(rt, sh, m0, args.cg_path, args.warmup, args.steps, args.no_link_angles)
     t_cg, apply_s = max_over_ranks(rt, [t_cg, apply_s])
     V = sh.V
     sh.close()
@@ -389,7 +403,7 @@ def run_config34(args, rt, cfg_id):
         # config 4's weak-scaling curve: 4096 x 512N sites, 4096 x 512 per GPU
         wNt = (Nt // 8) * world
         shw = Shard(rt, Nx, wNt, cfg["sigma"])
-        tw = time_cg_steps(rt, shw, m0, args.cg_path, args.warmup, args.steps)
+        tw, _ = time_cg_steps(rt, shw, m0, args.cg_path, args.warmup, args.steps, args.no_link_angles)
         (tw,) = max_over_ranks(rt, [tw])
         weak = {"lattice": f"{Nx}x{wNt}", "sites_per_gpu": shw.V, "ms_per_step": round(1e3 * tw / args.steps, 4),
                 "value": round(args.steps / tw * world, 3),
@@ -422,8 +436,9 @@ def run_config34(args, rt, cfg_id):
         "cpu_baseline": cpu,
         # the CG iteration's own streaming rate (informational; the graded
         # roofline is the Dirac apply's): algorithmic bytes / time per step
-        "cg_iteration": {"path": args.cg_path, "bytes_per_site": BYTES_PER_SITE_CG[args.cg_path],
-                         "achieved_GBps_per_gpu": round(BYTES_PER_SITE_CG[args.cg_path] * V * it_per_s / 1e9, 1),
+        "cg_iteration": {"path": args.cg_path, "link_angles": cg_bps == BYTES_PER_SITE_CG_ANGLES,
+                         "bytes_per_site": cg_bps,
+                         "achieved_GBps_per_gpu": round(cg_bps * V * it_per_s / 1e9, 1),
                          "reference_sequence_bytes_per_site": 576},
         "weak": weak,
     })
@@ -438,6 +453,7 @@ def run_config5(args, rt):
     sh = Shard(rt, Nx, Nt, cfg["sigma"])
     sm = sh.sm
     sm.check(sm.lib.sm_tune_cg(sh.L.ctx, CG_PATH_ID[args.cg_path], 0))
+    sm.check(sm.lib.sm_cg_link_angles(sh.L.ctx, 0 if args.no_link_angles else 1, None))
     tol = 1e-10
     # warm the kernels once on a short solve, then the timed solve from x0 = phi
     res = sm.CGResult()
@@ -449,6 +465,7 @@ def run_config5(args, rt):
     dt = time.perf_counter() - t
     (dt,) = max_over_ranks(rt, [dt])
     rel = true_relres(sh, m0)
+    cg_bps = cg_bytes_per_site(sh, args.cg_path)
     V = sh.V
     line = base_line(args, rt, cfg, Nx, Nt, sh)
     sh.close()
@@ -464,9 +481,9 @@ def run_config5(args, rt):
         "iterations": res.iterations, "converged": res.converged,
         "cg_residual_rel": res.residual / res.phi_norm if res.phi_norm else None,
         "true_relres": rel,
-        "cg_iteration": {"path": args.cg_path, "bytes_per_site": BYTES_PER_SITE_CG[args.cg_path],
-                         "achieved_GBps_per_gpu": round(BYTES_PER_SITE_CG[args.cg_path] * V * res.iterations
-                                                        / dt / 1e9, 1)},
+        "cg_iteration": {"path": args.cg_path, "link_angles": cg_bps == BYTES_PER_SITE_CG_ANGLES,
+                         "bytes_per_site": cg_bps,
+                         "achieved_GBps_per_gpu": round(cg_bps * V * res.iterations / dt / 1e9, 1)},
     })
     print(json.dumps(line), flush=True)
     if not res.converged or not rel < 1e-9:

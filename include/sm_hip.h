@@ -132,6 +132,17 @@ int sm_tune(sm_ctx *ctx, int bt, int xchunk, int xcd_remap, int variant);
  * were dominated at every size and removed). xchunk = rows per block of the
  * active one-pass kernel. < 0 / <= 0 keep. */
 int sm_tune_cg(sm_ctx *ctx, int fused, int xchunk);
+/* Link angles in the recompute-Ad CG pass (fused = 5, on by default): the
+ * pass reads each link as its angle theta = atan2(Im U, Re U) (16 instead of
+ * 32 B/site; 144 instead of 160 B/site per iteration) and rebuilds
+ * U = (cos theta, sin theta) in registers, within ~1 ulp per component of the
+ * stored link. The angles are rebuilt at the first solve after U changes, and
+ * only used when every link satisfies | |U|^2 - 1 | <= 1e-14 (the reference's
+ * links are exp(i theta), src/gauge_conf.cpp); otherwise the pass reads the
+ * complex links. D, D^dag and the force always use the stored links bitwise.
+ * on: 1 / 0 enable / disable, < 0 keep; *in_use (may be NULL): 1 if the last
+ * sm_cg_begin / sm_cg set the angles up for the active path. */
+int sm_cg_link_angles(sm_ctx *ctx, int on, int *in_use);
 /* Streaming-bandwidth ceiling on the ctx stream (measured roofline reference):
  * out = a + b (two_reads = 1: the stencil's 2-read/1-write byte mix) or
  * out = a, over n complex<double> device elements. */

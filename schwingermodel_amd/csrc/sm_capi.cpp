@@ -252,6 +252,7 @@ static int halo4(sm_ctx *c, hipStream_t s, const double2 *field, double2 *recv) 
 }
 
 int exchange_ghost_U(sm_ctx *c) {
+    c->uang_state = 0;  // every change of U comes through here: the link angles are stale
     if (!c->sharded()) return SM_OK;
     // U_t(x, Wt-1) (plane 0 of my hi face) is the up-neighbour's U_t(x, -1)
     double2 *slo = face_buf(c, 1, 0), *shi = face_buf(c, 1, 1);
@@ -265,6 +266,25 @@ int exchange_ghost_U(sm_ctx *c) {
     return SM_OK;
 }
 
+
+// Link angles for the recompute-Ad pass (cg_ra_kernel UC), rebuilt at the
+// first solve after U changed. Collective on t-shards (a global count of links
+// off the unit circle decides for every shard alike).
+int ensure_link_angles(sm_ctx *c) {
+    if (!c->link_angles || c->cg_fused != 5 || c->racfg.fold < 2 || !cg_ra_ok(c) || c->uang_state != 0)
+        return SM_OK;
+    if (!c->Uang) HIP_TRY(hipMalloc(&c->Uang, sizeof(double) * 2 * (size_t)c->g.V));
+    if (c->sharded() && !c->Uang_face) HIP_TRY(hipMalloc(&c->Uang_face, sizeof(double) * 16 * (size_t)c->g.Nx));
+    const long n = 2 * c->g.V;
+    const int nb = launch_link_angles(c->stream, n, c->U, c->Uang, c->partials);
+    TRY(global_sum(c, nb, c->partials, 0));
+    HIP_TRY(hipMemcpyAsync(c->h_sums, c->sums, sizeof(double2), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->uang_state = c->h_sums[0].x == 0.0 ? 1 : 2;
+    if (c->uang_state == 1 && c->sharded()) launch_angles_of(c->stream, 16 * (long)c->g.Nx, face4_recv_U(c), c->Uang_face);
+    HIP_TRY(hipGetLastError());
+    return SM_OK;
+}
 
 // alpha / beta from per-block partials (local sum, all-reduce over shards, scalar)
 int cg_scalar(sm_ctx *c, int nparts, int which) {
@@ -412,6 +432,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     if (const char *e = getenv("SM_EO_CG_FOLDED")) c->eo_cg_folded = atoi(e);
     if (const char *e = getenv("SM_EO_CG_TD")) c->eo_cg_td = atoi(e);
     if (const char *e = getenv("SM_DEBUG_CG")) c->debug_cg = atoi(e);
+    if (const char *e = getenv("SM_CG_LINK_ANGLES")) c->link_angles = atoi(e);
     const int np = kMaxPartials;
     const size_t fb = sizeof(double2) * 2 * (size_t)c->g.V;
     hipError_t e = hipSuccess;
@@ -479,7 +500,7 @@ int sm_destroy(sm_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
     void *dev[] = {c->U, c->ghostU, c->fields, c->faces, c->faces2, c->faces4, c->partials, c->sums, c->Fbuf, c->sc,
-                   c->U_alt, c->Pmd, c->Fmd, c->eo, c->Ucb, c->eo_faces, c->eo_faces4};
+                   c->U_alt, c->Pmd, c->Fmd, c->eo, c->Ucb, c->eo_faces, c->eo_faces4, c->Uang, c->Uang_face};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_sc) (void)hipHostFree(c->h_sc);
@@ -508,6 +529,13 @@ int sm_tune_cg(sm_ctx *c, int fused, int xchunk) {
         if (3 * cg_fused_blocks(f) > 2 * kMaxPartials) return fail(SM_ERR_ARG, "too many blocks");
         cur = f;
     }
+    return SM_OK;
+}
+
+int sm_cg_link_angles(sm_ctx *c, int on, int *in_use) {
+    if (!c) return fail(SM_ERR_ARG, "null context");
+    if (on >= 0) c->link_angles = on ? 1 : 0;
+    if (in_use) *in_use = c->link_angles && c->cg_fused == 5 && c->uang_state == 1 ? 1 : 0;
     return SM_OK;
 }
 
@@ -611,6 +639,7 @@ int sm_dot_dev(sm_ctx *c, const double *a, const double *b, double *out) {
 // ---- CG on D D^dagger (src/conjugate_gradient.cpp:4-66) ---------------------
 int sm_cg_begin(sm_ctx *c, const double *phi, double *x, double m0, double tol) {
     TRY(check_ready(c));
+    TRY(ensure_link_angles(c));
     const long n = 2 * c->g.V;
     const double2 *ph = (const double2 *)phi;
     double2 *xx = (double2 *)x;
@@ -729,6 +758,8 @@ static int cg_ra_pass(sm_ctx *c) {
     c->cg_pending_x = 1;  // sm_cg_finish checks the device's final pass parity
     c->cg_flush_pass = -1;
     const bool one = !c->sharded();
+    const bool angles = c->link_angles && c->uang_state == 1;
+    const double *ua = angles ? c->Uang : nullptr;
     if (one && !c->split_test) {
         // redundant scalars on small grids (partials by pass parity; every block
         // of the next pass evaluates them; sm_cg_iterate flushes the last pass)
@@ -736,7 +767,7 @@ static int cg_ra_pass(sm_ctx *c) {
         double2 *part = red ? c->partials + (j & 1) * 3 * (size_t)nparts : c->partials;
         const double2 *prev = red ? c->partials + ((j + 1) & 1) * 3 * (size_t)nparts : nullptr;
         launch_cg_ra(c->stream, c->g, fc, 1, d1, d2, dn, c->cg_x, c->U, nullptr, nullptr, nullptr, c->cg_mass, j,
-                     c->sc, part, 0, fc.TBk, prev);
+                     c->sc, part, 0, fc.TBk, prev, ua);
         if (red) {
             c->cg_flush_pass = j;
             c->cg_flush_nparts = nparts;
@@ -748,7 +779,7 @@ static int cg_ra_pass(sm_ctx *c) {
     double2 *f1 = one ? nullptr : face4_recv_d(c, j), *f2 = one ? nullptr : face4_recv_d(c, j - 1);
     auto pass = [&](int tb0, int tbn, hipStream_t st) {
         launch_cg_ra(st, c->g, fc, c->kshards(), d1, d2, dn, c->cg_x, c->U, f1, f2, one ? nullptr : face4_recv_U(c),
-                     c->cg_mass, j, c->sc, c->partials, tb0, tbn);
+                     c->cg_mass, j, c->sc, c->partials, tb0, tbn, nullptr, ua, one ? nullptr : c->Uang_face);
     };
     // interior t-blocks: every lane's column (56g-4 .. 56g+59) inside [0, Wt)
     auto interior = [&](int tb) {

@@ -65,19 +65,28 @@ struct RAArgs {
     double mass;
     const double2 *prev;  // RED: pass j-1's partials
     long pass;
+    const double *Ua, *fUa;  // UC: link angles theta_t, theta_x (plane stride V) and their 4-deep faces
 };
 
+// U(1) link from its angle (UC): one sincos in place of a 16-B load.
+__device__ __forceinline__ double2 u_of(double th) {
+    double sn, cs;
+    sincos(th, &sn, &cs);
+    return make_double2(cs, sn);
+}
+
+template <typename T>
 struct RSrc {
-    const double2 *p;
+    const T *p;
     long xs, ps;
 };
 
 // Column c of a field: periodic wrap (one shard), in-domain, or the received
 // 4-deep face (t-shard). Clamped so every lane's address is valid; lanes
 // beyond the face depth only feed halo lanes.
-template <int SH>
-__device__ __forceinline__ RSrc rsrc(const double2 *base, const double2 *face, int c, const RAArgs &a) {
-    RSrc s;
+template <int SH, typename T>
+__device__ __forceinline__ RSrc<T> rsrc(const T *base, const T *face, int c, const RAArgs &a) {
+    RSrc<T> s;
     if (!SH) {
         int cw = c % a.Wt;
         if (cw < 0) cw += a.Wt;
@@ -148,7 +157,7 @@ __device__ __forceinline__ Sp ra_site(double mass, double sr0, double sl0, const
     return o;
 }
 
-template <int SH, int XP, int FOLD, int RED = 0>
+template <int SH, int XP, int FOLD, int RED = 0, int UC = 0>
 __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
     __shared__ double2 sh[4];
     __shared__ double2 rlds[3][2][256];
@@ -214,9 +223,13 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
         const double sr0 = tg == a.Ntg - 1 ? -1.0 : 1.0;  // SignR[2n], include/dirac_operator.h:53-55
         const double sl0 = tg == 0 ? -1.0 : 1.0;          // SignL[2n], :56-58
         const double mass = a.mass;
-        const RSrc S1 = rsrc<SH>(a.d1, a.f1, c, a);
-        const RSrc S2 = rsrc<SH>(a.d2, a.f2, c, a);
-        const RSrc SU = rsrc<SH>(a.U, a.fU, c, a);
+        const RSrc<double2> S1 = rsrc<SH>(a.d1, a.f1, c, a);
+        const RSrc<double2> S2 = rsrc<SH>(a.d2, a.f2, c, a);
+        using LU = std::conditional_t<UC != 0, double, double2>;  // a link as loaded: angle or complex
+        const RSrc<LU> SU = [&] {
+            if constexpr (UC != 0) return rsrc<SH>(a.Ua, a.fUa, c, a);
+            else return rsrc<SH>(a.U, a.fU, c, a);
+        }();
         const int cx = c < 0 ? 0 : (c >= Wt ? Wt - 1 : c);
         auto wrap = [Nx](int x) { int w = x % Nx; return w < 0 ? w + Nx : w; };
         // d_{j-1}: rows x0-4 .. xe+3; U: x0-4 .. xe+2; d_{j-2}: x0-2 .. xe+1; x: owned rows
@@ -225,10 +238,14 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
             d.a = p[0];
             d.b = p[S1.ps];
         };
-        auto ldu = [&](int xr, double2 &ut, double2 &ux) {
-            const double2 *p = SU.p + (long)wrap(min(xr, xe + 2)) * SU.xs;
+        auto ldu = [&](int xr, LU &ut, LU &ux) {
+            const LU *p = SU.p + (long)wrap(min(xr, xe + 2)) * SU.xs;
             ut = p[0];
             ux = p[SU.ps];
+        };
+        auto cvu = [](LU v) -> double2 {
+            if constexpr (UC != 0) return u_of(v);
+            else return v;
         };
         auto ld2 = [&](int xr, Sp &q, Sp &xv) {
             const double2 *p = S2.p + (long)wrap(min(max(xr, x0 - 2), xe + 1)) * S2.xs;
@@ -244,7 +261,7 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
         const Sp zs = Sp{z, z};
         // state at the top of iteration y (see the header)
         Sp D2, D3, Ld;                                   // d_{j-1}(y+2), (y+3); in flight (y+4)
-        double2 Lut, Lux;                                // in flight U(y+3)
+        LU Lut, Lux;                                     // in flight U(y+3)
         Sp Mq, Mx = zs;                                  // in flight d_{j-2}(y+2), x(y+2)
         double2 Ut0 = z, Ut1 = z, Ut2, Ux0 = z, Ux1 = z, Ux2, Uxm = z;  // U_t(y..y+2), U_x(y-1..y+2)
         Sp P1 = zs, P2 = zs;                             // T'(y+1), T'(y+2)
@@ -253,7 +270,12 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
         const int y0 = x0 - 6;
         ld1(y0 + 2, D2);
         ld1(y0 + 3, D3);
-        ldu(y0 + 2, Ut2, Ux2);
+        {
+            LU t2, x2;
+            ldu(y0 + 2, t2, x2);
+            Ut2 = cvu(t2);
+            Ux2 = cvu(x2);
+        }
         ld1(y0 + 4, Ld);
         ldu(y0 + 3, Lut, Lux);
         ld2(y0 + 2, Mq, Mx);
@@ -262,7 +284,7 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
         auto step = [&](int y, auto mtag) {
             constexpr int M = decltype(mtag)::value;
             const Sp D4 = Ld;
-            const double2 Ut3 = Lut, Ux3 = Lux;
+            const double2 Ut3 = cvu(Lut), Ux3 = cvu(Lux);
             ld1(y + 5, Ld);
             ldu(y + 4, Lut, Lux);
             __builtin_amdgcn_sched_barrier(0);  // keep the next rows' loads issued here
@@ -389,7 +411,7 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
 void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard, const double2 *d1,
                   const double2 *d2, double2 *dn, double2 *x, const double2 *U, const double2 *f1,
                   const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
-                  int tb0, int tbn, const double2 *prev_partials) {
+                  int tb0, int tbn, const double2 *prev_partials, const double *Uang, const double *fUang) {
     if (tbn <= 0) return;
     RAArgs a;
     a.d1 = d1; a.d2 = d2; a.dn = dn; a.x = x; a.U = U;
@@ -404,13 +426,31 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
     a.mass = mass;
     a.prev = prev_partials;
     a.pass = pass;
+    a.Ua = Uang;
+    a.fUa = fUang;
     const dim3 grid(tbn * c.XB), block(64 * c.wpb);
     const int xp = pass >= 2 && (pass & 1) == 0;  // x takes passes j-1 and j together
     // one kernel per (shards, x pass, fold) combination
     const int f = c.fold >= 2 ? 2 : (c.fold ? 1 : 0);
+    const int uc = Uang && f == 2;  // link angles: with the fused multiply-add fold only
     if (prev_partials && nshard == 1 && f == 2 && tb0 == 0 && tbn == c.TBk) {
-        if (xp) hipLaunchKernelGGL((cg_ra_kernel<0, 1, 2, 1>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((cg_ra_kernel<0, 0, 2, 1>), grid, block, 0, s, a);
+        if (uc) {
+            if (xp) hipLaunchKernelGGL((cg_ra_kernel<0, 1, 2, 1, 1>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((cg_ra_kernel<0, 0, 2, 1, 1>), grid, block, 0, s, a);
+        } else {
+            if (xp) hipLaunchKernelGGL((cg_ra_kernel<0, 1, 2, 1>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((cg_ra_kernel<0, 0, 2, 1>), grid, block, 0, s, a);
+        }
+        return;
+    }
+    if (uc) {
+        const int sel = (nshard > 1 ? 2 : 0) + (xp ? 1 : 0);
+        switch (sel) {
+            case 0: hipLaunchKernelGGL((cg_ra_kernel<0, 0, 2, 0, 1>), grid, block, 0, s, a); break;
+            case 1: hipLaunchKernelGGL((cg_ra_kernel<0, 1, 2, 0, 1>), grid, block, 0, s, a); break;
+            case 2: hipLaunchKernelGGL((cg_ra_kernel<1, 0, 2, 0, 1>), grid, block, 0, s, a); break;
+            case 3: hipLaunchKernelGGL((cg_ra_kernel<1, 1, 2, 0, 1>), grid, block, 0, s, a); break;
+        }
         return;
     }
     const int sel = (nshard > 1 ? 6 : 0) + (xp ? 3 : 0) + f;
@@ -423,6 +463,38 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
         SM_RA_CASE(1, 1, 0) SM_RA_CASE(1, 1, 1) SM_RA_CASE(1, 1, 2)
     }
 #undef SM_RA_CASE
+}
+
+// Link angles for the UC passes: theta = atan2(Im U, Re U) for each of the n
+// links (both planes), and per block the count of links whose |U|^2 is off 1
+// by more than 1e-14 (such fields keep the complex-link passes, sm_capi.cpp).
+// cos/sin of the angle give back a unit link within ~1 ulp per component.
+__global__ void __launch_bounds__(256) link_angle_kernel(long n, const double2 *U, double *Ua, double2 *part) {
+    __shared__ double2 sh[4];
+    double bad = 0.0;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const double2 u = U[i];
+        Ua[i] = atan2(u.y, u.x);
+        const double m = u.x * u.x + u.y * u.y - 1.0;
+        if (!(fabs(m) <= 1e-14)) bad += 1.0;  // NaN counts as off the circle
+    }
+    const double2 b = block_sum(make_double2(bad, 0.0), sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = b;
+}
+
+int launch_link_angles(hipStream_t s, long n, const double2 *U, double *Ua, double2 *partials) {
+    const int nb = reduce_blocks(n);
+    hipLaunchKernelGGL(link_angle_kernel, dim3(nb), dim3(256), 0, s, n, U, Ua, partials);
+    return nb;
+}
+
+__global__ void __launch_bounds__(256) angles_of_kernel(long n, const double2 *U, double *Ua) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        Ua[i] = atan2(U[i].y, U[i].x);
+}
+
+void launch_angles_of(hipStream_t s, long n, const double2 *U, double *Ua) {
+    hipLaunchKernelGGL(angles_of_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, U, Ua);
 }
 
 // k-deep t-faces: columns 0..k-1 go down (arrive as Wt..Wt+k-1), columns

@@ -129,7 +129,13 @@ CGFusedCfg cg_ra_config(const Geometry &g);
 void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard, const double2 *d1,
                   const double2 *d2, double2 *dn, double2 *x, const double2 *U, const double2 *f1,
                   const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
-                  int tb0, int tbn, const double2 *prev_partials = nullptr);
+                  int tb0, int tbn, const double2 *prev_partials = nullptr, const double *Uang = nullptr,
+                  const double *fUang = nullptr);
+// Link angles of U for the passes above (Uang: 16 instead of 32 B/site of
+// links): writes theta = atan2(Im, Re) of n links and, per block, the count of
+// links off the unit circle (> 1e-14 in |U|^2) to partials; returns the block count.
+int launch_link_angles(hipStream_t s, long n, const double2 *U, double *Ua, double2 *partials);
+void launch_angles_of(hipStream_t s, long n, const double2 *U, double *Ua);  // faces: angles only
 // prev_partials != null (one shard, fold 2): redundant scalars as in
 // cg_onepass_kernel: every block evaluates pass j-1's scalars from its partials
 // (cg1_redundant); the caller keeps the partials by pass parity and flushes.

@@ -272,3 +272,78 @@ def test_large_lattice_properties(sm, oracle, Nx, Nt):
                                ptr(ref.mu0), ptr(ref.mu1), m0, 0, 8)
         assert bits_equal(flat(Dpsi), flat(ref))
     L.close()
+
+
+def _angles_in_use(sm, L):
+    u = ctypes.c_int(-1)
+    sm.check(sm.lib.sm_cg_link_angles(L.ctx, -1, ctypes.byref(u)))
+    return u.value
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_link_angles_vs_complex_links(sm, name):
+    """The recompute-Ad pass reading each link as its angle (16 instead of 32
+    B/site, the default) against the same pass reading the complex links: the
+    angle form rebuilds U = (cos, sin) within ~1 ulp, so the iteration counts
+    agree (+-1) and x to 1e-12; both meet the reference's solution to 1e-12
+    (test_cg_vs_reference runs the default)."""
+    meta, a = load_fixture(name)
+    Nx, Nt, m0 = meta["Nx"], meta["Nt"], meta["m0"]
+    S = Nx * Nt
+    L = sm.init(Nx, Nt)
+    sm.check(sm.lib.sm_tune_cg(L.ctx, 5, 0))
+    U, psi = as_spinor(sm, a["U"], S), as_spinor(sm, a["psi"], S)
+    out = {}
+    try:
+        for on in (0, 1):
+            sm.check(sm.lib.sm_cg_link_angles(L.ctx, on, None))
+            x = sm.spinor(S)
+            assert sm.conjugate_gradient(U, psi, x, m0) == 1
+            assert _angles_in_use(sm, L) == on
+            out[on] = (flat(x), L.last_cg.iterations)
+    finally:
+        sm.check(sm.lib.sm_cg_link_angles(L.ctx, 1, None))
+    assert abs(out[1][1] - out[0][1]) <= 1, (out[1][1], out[0][1])
+    rel = np.linalg.norm(out[1][0] - out[0][0]) / np.linalg.norm(out[0][0])
+    assert rel <= CG_REL_TOL, rel
+    xr = a["ref_cgx"]
+    assert np.linalg.norm(out[1][0] - xr) / np.linalg.norm(xr) <= CG_REL_TOL
+
+
+def test_link_angles_follow_gauge_updates(sm):
+    """Angles are rebuilt after every change of U (upload, MD update), never
+    reused stale, and a field with a link off the unit circle keeps the
+    complex-link pass: its x is bitwise the angles-off solve's."""
+    Nx, Nt = 96, 64
+    S = Nx * Nt
+    L = sm.init(Nx, Nt)
+    sm.check(sm.lib.sm_tune_cg(L.ctx, 5, 0))  # the recompute-Ad pass (default from 256^2 sites)
+    P = lambda a: a.ctypes.data  # noqa: E731
+    U1, U2, psi = sm.spinor(S), sm.spinor(S), sm.spinor(S)
+    sm.lib.sm_fill_gauge(11, 0.4, Nt, 0, Nx, 0, Nt, P(U1.mu0), P(U1.mu1))
+    sm.lib.sm_fill_gauge(12, 0.9, Nt, 0, Nx, 0, Nt, P(U2.mu0), P(U2.mu1))
+    sm.lib.sm_fill_spinor(13, Nt, 0, Nx, 0, Nt, P(psi.mu0), P(psi.mu1))
+
+    def solve(U, on):
+        sm.check(sm.lib.sm_cg_link_angles(L.ctx, on, None))
+        x = sm.spinor(S)
+        assert sm.conjugate_gradient(U, psi, x, -0.1) == 1
+        return flat(x), _angles_in_use(sm, L)
+
+    try:
+        x1, u1 = solve(U1, 1)
+        x2, u2 = solve(U2, 1)       # new U: angles rebuilt
+        x2c, _ = solve(U2, 0)
+        x1c, _ = solve(U1, 0)
+        assert u1 == 1 and u2 == 1
+        assert np.linalg.norm(x2 - x2c) / np.linalg.norm(x2c) <= 1e-12
+        assert np.linalg.norm(x1 - x1c) / np.linalg.norm(x1c) <= 1e-12
+        assert np.linalg.norm(x1 - x2) / np.linalg.norm(x1) > 1e-3  # the solves did see different fields
+        bad = U2.copy()
+        bad.mu1[17] *= 1.0 + 1e-9  # one link off the unit circle
+        xb, ub = solve(bad, 1)
+        xbc, _ = solve(bad, 0)
+        assert ub == 0
+        assert bits_equal(xb.view(np.float64), xbc.view(np.float64))
+    finally:
+        sm.check(sm.lib.sm_cg_link_angles(L.ctx, 1, None))
