@@ -48,12 +48,14 @@ TFaces faces_for(sm_ctx *c, const double2 *in, const double2 *recv_lo, const dou
         f.hi_xs = c->g.Wt;
         f.hi_ps = c->g.V;
     } else {
+        // spin-projected faces (launch_pack_faces_proj): one complex per x
         f.lo = recv_lo;
         f.lo_xs = 1;
-        f.lo_ps = c->g.Nx;
+        f.lo_ps = 0;
         f.hi = recv_hi;
         f.hi_xs = 1;
-        f.hi_ps = c->g.Nx;
+        f.hi_ps = 0;
+        f.proj = 1;
     }
     return f;
 }
@@ -115,15 +117,17 @@ int allreduce_dev(sm_ctx *c, double *dev, int n) {
     return SM_OK;
 }
 
-int halo(sm_ctx *c, const double2 *field, int set, TFaces *f) {
+// 1-deep t-faces of `field` for the operator `kind` (FaceKind): spin-projected,
+// one complex per x and side (2 Nx doubles per message instead of 4 Nx).
+int halo(sm_ctx *c, const double2 *field, int set, int kind, TFaces *f) {
     if (!c->sharded()) {
         *f = faces_for(c, field, nullptr, nullptr);
         return SM_OK;
     }
     double2 *slo = face_buf(c, set, 0), *shi = face_buf(c, set, 1);
     double2 *rlo = face_buf(c, set, 2), *rhi = face_buf(c, set, 3);
-    launch_pack_faces(c->stream, c->g, field, slo, shi);
-    TRY(exchange_faces(c, slo, shi, rlo, rhi, (size_t)4 * c->g.Nx));
+    launch_pack_faces_proj(c->stream, c->g, field, c->U, kind, slo, shi);
+    TRY(exchange_faces(c, slo, shi, rlo, rhi, (size_t)2 * c->g.Nx));
     *f = faces_for(c, field, rlo, rhi);
     return SM_OK;
 }
@@ -136,7 +140,7 @@ int apply(sm_ctx *c, const double2 *in, double2 *out, double mass, int dagger, c
     const int TB = (c->g.Wt + c->cfg.bt - 1) / c->cfg.bt;
     const bool one = !c->sharded();
     if (TB < 3 || (one && !c->split_test)) {
-        TRY(halo(c, in, 0, &f));
+        TRY(halo(c, in, 0, dagger ? FACE_DDAG : FACE_D, &f));
         launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip);
     } else {
         // t-blocks 1..TB-2 never touch t = 0 / Wt-1: they run on the main
@@ -148,8 +152,8 @@ int apply(sm_ctx *c, const double2 *in, double2 *out, double mass, int dagger, c
         HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
         HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
         if (!one) {
-            launch_pack_faces(c->comm_stream, c->g, in, slo, shi);
-            TRY(exchange_faces_on(c, c->comm_stream, slo, shi, rlo, rhi, (size_t)4 * c->g.Nx));
+            launch_pack_faces_proj(c->comm_stream, c->g, in, c->U, dagger ? FACE_DDAG : FACE_D, slo, shi);
+            TRY(exchange_faces_on(c, c->comm_stream, slo, shi, rlo, rhi, (size_t)2 * c->g.Nx));
         }
         f = one ? faces_for(c, in, nullptr, nullptr) : faces_for(c, in, rlo, rhi);
         // both edge block-columns (TB-1, then 0 by wrap-around) in one launch
@@ -618,8 +622,8 @@ int sm_ddag_dev(sm_ctx *c, const double *in, double *out, double m0) {
 int sm_force_dev(sm_ctx *c, const double *l, const double *r, double *F) {
     TRY(check_ready(c));
     TFaces fl, fr;
-    TRY(halo(c, (const double2 *)l, 0, &fl));
-    TRY(halo(c, (const double2 *)r, 1, &fr));
+    TRY(halo(c, (const double2 *)l, 0, FACE_FORCE_L, &fl));
+    TRY(halo(c, (const double2 *)r, 1, FACE_FORCE_R, &fr));
     launch_force(c->stream, c->g, c->U, (const double2 *)l, (const double2 *)r, fl, fr, F);
     HIP_TRY(hipGetLastError());
     return SM_OK;

@@ -171,7 +171,7 @@ int exchange_faces_on(sm_ctx *c, hipStream_t s, double2 *slo, double2 *shi, doub
                       size_t cnt);
 int exchange_faces(sm_ctx *c, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi, size_t cnt);
 int allreduce_dev(sm_ctx *c, double *dev, int n);
-int halo(sm_ctx *c, const double2 *field, int set, TFaces *f);
+int halo(sm_ctx *c, const double2 *field, int set, int kind, TFaces *f);  // kind: FaceKind
 const double2 *loU(sm_ctx *c);
 int apply(sm_ctx *c, const double2 *in, double2 *out, double mass, int dagger, const double2 *aux,
           double2 *partials, const CGScalars *skip);

@@ -19,7 +19,14 @@ struct TFaces {
     const double2 *lo;   // psi at local t = -1   : lo[x*lo_xs] (+ lo_ps for plane 1)
     const double2 *hi;   // psi at local t = Wt   : hi[x*hi_xs] (+ hi_ps for plane 1)
     long lo_xs, lo_ps, hi_xs, hi_ps;
+    // proj = 1: spin-projected t-faces (t-shards), ONE complex per x and side:
+    // hi = the forward hop's spin combination at t = Wt (D: p0 - p1, D^dag:
+    // p0 + p1; force: l0 + l1 / r0 - r1), lo = the backward hop's whole product
+    // conj(U_t(t = -1)) * combination (D: p0 + p1, D^dag: p0 - p1), formed by
+    // the sending shard with its own link (launch_pack_faces_proj).
+    int proj = 0;
 };
+enum FaceKind { FACE_D = 0, FACE_DDAG = 1, FACE_FORCE_L = 2, FACE_FORCE_R = 3 };
 
 struct Geometry {
     int Nx, Wt;          // local block (all x, Wt t-values)
@@ -238,5 +245,10 @@ void launch_pack_cb_faces4(hipStream_t s, const Geometry &g, const double2 *f, d
 // Pack the t = 0 and t = Wt-1 columns (both planes) into contiguous faces.
 void launch_pack_faces(hipStream_t s, const Geometry &g, const double2 *field, double2 *lo_face,
                        double2 *hi_face);
+// Spin-projected faces (TFaces::proj) of `field` for the operator `kind`:
+// lo_face (my t = 0, sent down) = the forward combination, hi_face (my
+// t = Wt-1, sent up) = conj(U_t) * the backward combination; Nx complex each.
+void launch_pack_faces_proj(hipStream_t s, const Geometry &g, const double2 *field, const double2 *U, int kind,
+                            double2 *lo_face, double2 *hi_face);
 
 }  // namespace sm

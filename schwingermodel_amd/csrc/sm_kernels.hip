@@ -99,11 +99,67 @@ __device__ __forceinline__ void load_row(const DArgs &a, const LaneSrc &L, int x
     r.utm = L.um[(long)xs * L.xs_m];
 }
 
+// dirac_site with spin-projected t-faces (TFaces::proj, t-shards): on the
+// edge lanes the t-hop operands arrive pre-combined. elo: pm0 holds
+// conj(U_t(t-1)) * (backward combination), formed by the sending shard, and
+// the hop is sl0 times it; ehi: pt0 holds the forward combination. The
+// reference's second-spin terms (D: a(-pt0+pt1); D^dag: c(-pm0+pm1)) are the
+// exact negations of the first's, so every value equals dirac_site's up to
+// the sign of an exact zero; off the edges it IS dirac_site's arithmetic.
+template <int DAG>
+__device__ __forceinline__ void dirac_site_proj(double mass, double sr0, double sl0, bool elo, bool ehi, double2 p0,
+                                                double2 p1, double2 pt0, double2 pt1, double2 px0, double2 px1,
+                                                double2 pm0, double2 pm1, double2 pxm0, double2 pxm1, double2 Ut,
+                                                double2 Ux, double2 Utm, double2 Uxm, double2 &s0, double2 &s1) {
+    const double2 one = make_double2(1.0, 0.0);
+    const double2 a = cmul(Ut, make_double2(sr0, 0.0));
+    const double2 b = cmul(Ux, one);
+    const double2 c = cmul(cconj(Utm), make_double2(sl0, 0.0));
+    const double2 e = cmul(cconj(Uxm), one);
+    const double2 Ce = make_double2(sl0 * pm0.x, sl0 * pm0.y);  // edge: sl0 * conj(U_t(t-1)) combo
+    double2 h0, h1;
+    if (!DAG) {
+        double2 A = cmul(a, ehi ? pt0 : csub(pt0, pt1));
+        double2 B = cmul(b, cadd(px0, cmul(I_NUM, px1)));
+        const double2 C = elo ? Ce : cmul(c, cadd(pm0, pm1));
+        double2 E = cmul(e, csub(pxm0, cmul(I_NUM, pxm1)));
+        h0 = cadd(cadd(cadd(A, B), C), E);
+        A = ehi ? cneg(A) : cmul(a, cadd(cneg(pt0), pt1));
+        B = cmul(b, cadd(cmul(MI_NUM, px0), px1));
+        E = cmul(e, cadd(cmul(I_NUM, pxm0), pxm1));
+        h1 = cadd(cadd(cadd(A, B), C), E);
+    } else {
+        double2 C = elo ? Ce : cmul(c, csub(pm0, pm1));
+        double2 E = cmul(e, cadd(pxm0, cmul(I_NUM, pxm1)));
+        const double2 A = cmul(a, ehi ? pt0 : cadd(pt0, pt1));
+        double2 B = cmul(b, csub(px0, cmul(I_NUM, px1)));
+        h0 = cadd(cadd(cadd(C, E), A), B);
+        C = elo ? cneg(C) : cmul(c, cadd(cneg(pm0), pm1));
+        E = cmul(e, cadd(cmul(MI_NUM, pxm0), pxm1));
+        B = cmul(b, cadd(cmul(I_NUM, px0), px1));
+        h1 = cadd(cadd(cadd(C, E), A), B);
+    }
+    s0 = csub(rmul(mass, p0), rmul(0.5, h0));
+    s1 = csub(rmul(mass, p1), rmul(0.5, h1));
+}
+
+template <int DAG, int PROJ>
+__device__ __forceinline__ void dslash_site(const DArgs &a, double sr0, double sl0, bool elo, bool ehi, const Row &cur,
+                                            const Row &nx1, double2 pxm0, double2 pxm1, double2 uxm, double2 &s0,
+                                            double2 &s1) {
+    if (PROJ)
+        dirac_site_proj<DAG>(a.mass, sr0, sl0, elo, ehi, cur.c0, cur.c1, cur.p0, cur.p1, nx1.c0, nx1.c1, cur.m0,
+                             cur.m1, pxm0, pxm1, cur.ut, cur.ux, cur.utm, uxm, s0, s1);
+    else
+        dirac_site<DAG>(a.mass, sr0, sl0, cur.c0, cur.c1, cur.p0, cur.p1, nx1.c0, nx1.c1, cur.m0, cur.m1, pxm0, pxm1,
+                        cur.ut, cur.ux, cur.utm, uxm, s0, s1);
+}
+
 // Marching loop with a two-row prefetch: at step x the loads of row x+2 are
 // issued while row x is computed from rows x-1 (centre), x and x+1, which
 // were loaded one and two steps earlier. xn/xs clamp at the chunk end so no
 // load is ever conditional (re-reads there are cache hits).
-template <int DAG, int EPI, int PREF>
+template <int DAG, int EPI, int PREF, int PROJ = 0>
 __device__ __forceinline__ void dslash_body(const DArgs &a) {
     __shared__ double2 sh[4];
     if (a.sc && a.sc->done) return;  // grid-uniform early exit after CG convergence
@@ -119,6 +175,7 @@ __device__ __forceinline__ void dslash_body(const DArgs &a) {
         const double sr0 = (a.t0 + t == a.Ntg - 1) ? -1.0 : 1.0;
         const double sl0 = (a.t0 + t == 0) ? -1.0 : 1.0;
         const LaneSrc L = lane_src(a, t);
+        const bool elo = PROJ && t == 0, ehi = PROJ && t + 1 == Wt;  // lanes reading projected faces
         auto wrap = [Nx](int x) { return x >= Nx ? x - Nx : x; };
         const int xm = (xbeg == 0) ? Nx - 1 : xbeg - 1;
         const long nm = (long)xm * Wt + t;
@@ -139,8 +196,7 @@ __device__ __forceinline__ void dslash_body(const DArgs &a) {
                     ax1 = a.aux[n + V];
                 }
                 double2 s0, s1;
-                dirac_site<DAG>(a.mass, sr0, sl0, cur.c0, cur.c1, cur.p0, cur.p1, nxt.c0, nxt.c1,
-                                cur.m0, cur.m1, pxm0, pxm1, cur.ut, cur.ux, cur.utm, uxm, s0, s1);
+                dslash_site<DAG, PROJ>(a, sr0, sl0, elo, ehi, cur, nxt, pxm0, pxm1, uxm, s0, s1);
                 st_nt(a.out + n, s0);
                 st_nt(a.out + n + V, s1);
                 if (EPI == EPI_DOT) {
@@ -168,8 +224,7 @@ __device__ __forceinline__ void dslash_body(const DArgs &a) {
                 ax1 = a.aux[n + V];
             }
             double2 s0, s1;
-            dirac_site<DAG>(a.mass, sr0, sl0, cur.c0, cur.c1, cur.p0, cur.p1, nx1.c0, nx1.c1,
-                            cur.m0, cur.m1, pxm0, pxm1, cur.ut, cur.ux, cur.utm, uxm, s0, s1);
+            dslash_site<DAG, PROJ>(a, sr0, sl0, elo, ehi, cur, nx1, pxm0, pxm1, uxm, s0, s1);
             st_nt(a.out + n, s0);
             st_nt(a.out + n + V, s1);
             if (EPI == EPI_DOT) {
@@ -206,6 +261,9 @@ template <int DAG, int EPI>
 __global__ void __launch_bounds__(256) dslash_kernel_v1(DArgs a) { dslash_body<DAG, EPI, 2>(a); }
 template <int DAG, int EPI>
 __global__ void __launch_bounds__(256, 3) dslash_kernel_v2(DArgs a) { dslash_body<DAG, EPI, 2>(a); }
+// t-shards with spin-projected faces (the two-row lookahead body of v1)
+template <int DAG, int EPI>
+__global__ void __launch_bounds__(256) dslash_kernel_proj(DArgs a) { dslash_body<DAG, EPI, 2, 1>(a); }
 
 LaunchCfg dslash_config(const Geometry &g) {
     LaunchCfg c;
@@ -276,7 +334,8 @@ void launch_dslash(hipStream_t s, const Geometry &g, const LaunchCfg &c, int dag
             else hipLaunchKernelGGL((K<1, EPI_NONE>), grid, block, 0, s, a);            \
         }                                                                               \
     } while (0)
-    if (c.variant == 1) SM_LAUNCH(dslash_kernel_v1);
+    if (f.proj) SM_LAUNCH(dslash_kernel_proj);
+    else if (c.variant == 1) SM_LAUNCH(dslash_kernel_v1);
     else if (c.variant == 2) SM_LAUNCH(dslash_kernel_v2);
     else SM_LAUNCH(dslash_kernel_v0);
 #undef SM_LAUNCH
@@ -300,18 +359,19 @@ __global__ void __launch_bounds__(256) force_kernel(FArgs a) {
         const double2 SR1 = make_double2(1.0, 0.0);
         const double2 U = a.U[n], W = a.U[n + V];
         const double2 L0 = a.l[n], L1 = a.l[n + V], R0 = a.r[n], R1 = a.r[n + V];
-        double2 lt0, lt1, rt0, rt1;   // left/right at n + t^
+        double2 lsum, rdif;   // l0 + l1 and r0 - r1 at n + t^
         if (t + 1 < a.Wt) {
-            lt0 = a.l[n + 1]; lt1 = a.l[n + 1 + V];
-            rt0 = a.r[n + 1]; rt1 = a.r[n + 1 + V];
+            lsum = cadd(a.l[n + 1], a.l[n + 1 + V]);
+            rdif = csub(a.r[n + 1], a.r[n + 1 + V]);
         } else {
             const double2 *pl = a.fl.hi + (long)x * a.fl.hi_xs, *pr = a.fr.hi + (long)x * a.fr.hi_xs;
-            lt0 = pl[0]; lt1 = pl[a.fl.hi_ps];
-            rt0 = pr[0]; rt1 = pr[a.fr.hi_ps];
+            // projected faces (t-shards) carry the combinations themselves
+            lsum = a.fl.proj ? pl[0] : cadd(pl[0], pl[a.fl.hi_ps]);
+            rdif = a.fr.proj ? pr[0] : csub(pr[0], pr[a.fr.hi_ps]);
         }
         // mu = 0
-        double2 P = cmul(cmul(cmul(U, SR0), cconj(csub(L0, L1))), csub(rt0, rt1));
-        double2 Q = cmul(cmul(cmul(cconj(U), SR0), cconj(cadd(lt0, lt1))), cadd(R0, R1));
+        double2 P = cmul(cmul(cmul(U, SR0), cconj(csub(L0, L1))), rdif);
+        double2 Q = cmul(cmul(cmul(cconj(U), SR0), cconj(lsum)), cadd(R0, R1));
         a.F[n] = csub(P, Q).y;
         // mu = 1
         const double2 lx0 = a.l[nx], lx1 = a.l[nx + V], rx0 = a.r[nx], rx1 = a.r[nx + V];
@@ -585,6 +645,43 @@ void launch_pack_faces(hipStream_t s, const Geometry &g, const double2 *field, d
                        double2 *hi_face) {
     hipLaunchKernelGGL(pack_faces_kernel, dim3((g.Nx + 255) / 256), dim3(256), 0, s, g.Nx, g.Wt, g.V,
                        field, lo_face, hi_face);
+}
+
+// Spin-projected faces (TFaces::proj): lo = my t = 0 column's forward-hop
+// combination (it is the down-neighbour's t = Wt), hi = conj(U_t(t = Wt-1))
+// times my t = Wt-1 column's backward-hop combination (the up-neighbour's
+// t = -1 hop, without its antiperiodic sign). The sums and the product are the
+// reference's own (src/dirac_operator.cpp:31-43, 255-267; force :493-506).
+__global__ void pack_faces_proj_kernel(int Nx, int Wt, long V, const double2 *f, const double2 *U, int kind,
+                                       double2 *lo, double2 *hi) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= Nx) return;
+    const long a = (long)x * Wt, b = (long)x * Wt + Wt - 1;
+    const double2 a0 = f[a], a1 = f[a + V], b0 = f[b], b1 = f[b + V];
+    switch (kind) {
+        case FACE_D:
+            lo[x] = csub(a0, a1);
+            hi[x] = cmul(cconj(U[b]), cadd(b0, b1));
+            break;
+        case FACE_DDAG:
+            lo[x] = cadd(a0, a1);
+            hi[x] = cmul(cconj(U[b]), csub(b0, b1));
+            break;
+        case FACE_FORCE_L:  // the force reads only its t+1 neighbours (hi faces)
+            lo[x] = cadd(a0, a1);
+            hi[x] = make_double2(0.0, 0.0);
+            break;
+        default:            // FACE_FORCE_R
+            lo[x] = csub(a0, a1);
+            hi[x] = make_double2(0.0, 0.0);
+            break;
+    }
+}
+
+void launch_pack_faces_proj(hipStream_t s, const Geometry &g, const double2 *field, const double2 *U, int kind,
+                            double2 *lo_face, double2 *hi_face) {
+    hipLaunchKernelGGL(pack_faces_proj_kernel, dim3((g.Nx + 255) / 256), dim3(256), 0, s, g.Nx, g.Wt, g.V, field, U,
+                       kind, lo_face, hi_face);
 }
 
 }  // namespace sm
