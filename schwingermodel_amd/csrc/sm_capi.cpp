@@ -422,6 +422,24 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     c->nparts_red = reduce_blocks(2 * c->g.V);
     c->fcfg = cg_fused_config(c->g);
     c->racfg = cg_ra_config(c->g);
+    // every per-tile partial slot must fit c->partials (2 kMaxPartials complex;
+    // the one-pass CG grids write 3 per tile): tall shards march longer chunks
+    // instead of writing past it
+    auto fit = [Nx](CGFusedCfg &f) {
+        while (3L * cg_fused_blocks(f) > 2L * kMaxPartials && f.xchunk < Nx) {
+            f.xchunk = std::min(Nx, 2 * f.xchunk);
+            f.XB = (Nx + f.xchunk - 1) / f.xchunk;
+        }
+        return 3L * cg_fused_blocks(f) <= 2L * kMaxPartials;
+    };
+    while (c->nparts_dslash > kMaxPartials && c->cfg.xchunk < Nx) {
+        c->cfg.xchunk = std::min(Nx, 2 * c->cfg.xchunk);
+        c->nparts_dslash = dslash_blocks(c->g, c->cfg);
+    }
+    if (!fit(c->fcfg) || !fit(c->racfg) || c->nparts_dslash > kMaxPartials) {
+        delete c;
+        return fail(SM_ERR_ARG, "shard %dx%d too wide for the partial-sum buffer", Nx, Wt);
+    }
     // recompute-Ad pass from 1024^2 sites per shard up (tools/tune_cg.py, ms per
     // iteration against the stored-Ad pass: 1024^2 0.054 vs 0.060, 2048^2 0.174
     // vs 0.223, 4096^2 0.588 vs 0.778); below that the stored-Ad pass is faster
