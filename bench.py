@@ -82,7 +82,8 @@ def parse(argv=None):
     ap.add_argument("--device", type=int, default=None, help="override the rank -> GPU mapping")
     ap.add_argument("--cg-path", choices=list(CG_PATH_ID), default="recompute")
     ap.add_argument("--no-link-angles", action="store_true",
-                    help="recompute-Ad CG reads the complex links (160 B/site) instead of their angles (144)")
+                    help="recompute-Ad CG reads the complex links (160 B/site) instead of their angles "
+                         "(144; the default from 4M sites per shard)")
     return ap.parse_args(argv)
 
 
@@ -329,7 +330,7 @@ def time_cg_steps(rt, sh, m0, cg_path, warmup, steps, link_angles_off=False):
     import torch
     sm = sh.sm
     sm.check(sm.lib.sm_tune_cg(sh.L.ctx, CG_PATH_ID[cg_path], 0))
-    sm.check(sm.lib.sm_cg_link_angles(sh.L.ctx, 0 if link_angles_off else 1, None))
+    sm.check(sm.lib.sm_cg_link_angles(sh.L.ctx, 0 if link_angles_off else -1, None))  # -1: the size default
     sm.check(sm.lib.sm_cg_begin(sh.L.ctx, sh.p(sh.phi), sh.p(sh.x), m0, 0.0))
     sm.check(sm.lib.sm_cg_iterate(sh.L.ctx, warmup))
     barrier(rt)
@@ -453,7 +454,7 @@ def run_config5(args, rt):
     sh = Shard(rt, Nx, Nt, cfg["sigma"])
     sm = sh.sm
     sm.check(sm.lib.sm_tune_cg(sh.L.ctx, CG_PATH_ID[args.cg_path], 0))
-    sm.check(sm.lib.sm_cg_link_angles(sh.L.ctx, 0 if args.no_link_angles else 1, None))
+    sm.check(sm.lib.sm_cg_link_angles(sh.L.ctx, 0 if args.no_link_angles else -1, None))
     tol = 1e-10
     # warm the kernels once on a short solve, then the timed solve from x0 = phi
     res = sm.CGResult()

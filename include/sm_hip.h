@@ -132,6 +132,10 @@ int sm_tune(sm_ctx *ctx, int bt, int xchunk, int xcd_remap, int variant);
  * were dominated at every size and removed). xchunk = rows per block of the
  * active one-pass kernel. < 0 / <= 0 keep. */
 int sm_tune_cg(sm_ctx *ctx, int fused, int xchunk);
+/* Launch geometry of the recompute-Ad CG pass (fused = 5): waves per block
+ * (1, 2 or 4; each wave owns 56 t-columns) and rows marched per block.
+ * Values <= 0 keep the current setting. */
+int sm_tune_cg_geometry(sm_ctx *ctx, int waves_per_block, int xchunk);
 /* Link angles in the recompute-Ad CG pass (fused = 5, on by default): the
  * pass reads each link as its angle theta = atan2(Im U, Re U) (16 instead of
  * 32 B/site; 144 instead of 160 B/site per iteration) and rebuilds

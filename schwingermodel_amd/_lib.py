@@ -90,6 +90,7 @@ def _load():
         "sm_cg_finish": ([vp, ctypes.POINTER(CGResult)], ci),
         "sm_tune_cg": ([vp, ci, ci], ci),
         "sm_cg_link_angles": ([vp, ci, ctypes.POINTER(ci)], ci),
+        "sm_tune_cg_geometry": ([vp, ci, ci], ci),
         # gauge field / molecular dynamics / HMC
         "sm_download_gauge": ([vp, vp, vp], ci),
         "sm_fill_gauge_dev": ([vp, u64, cd], ci),

@@ -454,6 +454,11 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     if (const char *e = getenv("SM_EO_CG_FOLDED")) c->eo_cg_folded = atoi(e);
     if (const char *e = getenv("SM_EO_CG_TD")) c->eo_cg_td = atoi(e);
     if (const char *e = getenv("SM_DEBUG_CG")) c->debug_cg = atoi(e);
+    // link angles from 4M sites per shard: below, the fields of a pass sit
+    // largely in the 256 MB MALL and the pass is bound by its VALU work, where
+    // the sincos costs more than the 16 B it saves (tools/tune_shapes.py:
+    // 4096x512 0.080 vs 0.068 ms per iteration, 4096x1024 0.141 vs 0.147)
+    c->link_angles = c->g.V >= (1L << 22) ? 1 : 0;
     if (const char *e = getenv("SM_CG_LINK_ANGLES")) c->link_angles = atoi(e);
     const int np = kMaxPartials;
     const size_t fb = sizeof(double2) * 2 * (size_t)c->g.V;
@@ -551,6 +556,22 @@ int sm_tune_cg(sm_ctx *c, int fused, int xchunk) {
         if (3 * cg_fused_blocks(f) > 2 * kMaxPartials) return fail(SM_ERR_ARG, "too many blocks");
         cur = f;
     }
+    return SM_OK;
+}
+
+int sm_tune_cg_geometry(sm_ctx *c, int waves_per_block, int xchunk) {
+    if (!c) return fail(SM_ERR_ARG, "null context");
+    CGFusedCfg f = c->racfg;
+    if (waves_per_block > 0) {
+        if (waves_per_block != 1 && waves_per_block != 2 && waves_per_block != 4)
+            return fail(SM_ERR_ARG, "waves per block must be 1, 2 or 4");
+        f.wpb = waves_per_block;
+        f.TBk = (f.NWT + f.wpb - 1) / f.wpb;
+    }
+    if (xchunk > 0) f.xchunk = xchunk;
+    f.XB = (c->g.Nx + f.xchunk - 1) / f.xchunk;
+    if (3L * cg_fused_blocks(f) > 2L * kMaxPartials) return fail(SM_ERR_ARG, "too many blocks");
+    c->racfg = f;
     return SM_OK;
 }
 

@@ -160,7 +160,7 @@ __device__ __forceinline__ Sp ra_site(double mass, double sr0, double sl0, const
 template <int SH, int XP, int FOLD, int RED = 0, int UC = 0>
 __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
     __shared__ double2 sh[4];
-    __shared__ double2 rlds[3][2][256];
+    extern __shared__ double2 rlds[];  // r_j ring: 3 slots x 2 planes x blockDim (dynamic: sized by waves per block)
     CGScalars *sc = a.sc;
     // Passes 0 and 1 take zero multipliers instead of branches: pass 0 has
     // d_0 = r_0 (alpha = beta = 0), pass 1 has r_0 = d_0 (beta2 = 0). The
@@ -313,15 +313,15 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
                     acc_n.x = nacc<FOLD>(acc_n.x, R2.a);  // Re dot(r, r), include/variables.h:185-188
                     acc_n.x = nacc<FOLD>(acc_n.x, R2.b);
                 }
-                rlds[s_w][0][threadIdx.x] = R2.a;
-                rlds[s_w][1][threadIdx.x] = R2.b;
+                rlds[(2 * s_w) * blockDim.x + threadIdx.x] = R2.a;
+                rlds[(2 * s_w + 1) * blockDim.x + threadIdx.x] = R2.b;
             }
             ld2(y + 3, Mq, Mx);  // consumed above: issued now, used next iteration
             if constexpr ((M & 2) != 0) Q2 = ra_site<FOLD, 1>(mass, sr0, sl0, J1, J0, J2, Ut1, Ux1, Ux0);  // S4: T(y+1)
             if constexpr ((M & 4) != 0) {
                 const Sp o = ra_site<FOLD, 0>(mass, sr0, sl0, Q1, Q0, Q2, Ut0, Ux0, Uxm);  // S5: Ad_j(y)
                 if (own) {
-                    const Sp R0 = Sp{rlds[s_r][0][threadIdx.x], rlds[s_r][1][threadIdx.x]};
+                    const Sp R0 = Sp{rlds[(2 * s_r) * blockDim.x + threadIdx.x], rlds[(2 * s_r + 1) * blockDim.x + threadIdx.x]};
                     acc_dA = cfma<FOLD>(acc_dA, J0.a, cconj(o.a));  // dot(d, Ad)
                     acc_dA = cfma<FOLD>(acc_dA, J0.b, cconj(o.b));
                     acc_rA = cfma<FOLD>(acc_rA, R0.a, cconj(o.a));  // dot(r, Ad)
@@ -378,8 +378,6 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
     CGFusedCfg c;
     c.NWT = (g.Wt + RW - 1) / RW;
     c.wpb = 4;
-    if (const char *e = getenv("SM_CGRA_WPB")) c.wpb = atoi(e);
-    if (c.wpb != 1 && c.wpb != 2) c.wpb = 4;
     c.TBk = (c.NWT + c.wpb - 1) / c.wpb;
     // rows per block: a chunk re-reads 8 halo rows of d_{j-1} (4 per side) and
     // runs 6 prologue steps, so chunks stay long where the grid is big enough
@@ -395,6 +393,32 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
         c.xchunk = (g.Nx + nchunks - 1) / nchunks;
         if (c.xchunk < 2) c.xchunk = 2;
     }
+    // Shard shapes of the BASELINE configs (4096^2 and its t-shards over 2/4/8
+    // GPUs, 8192^2 and its 8-way shard, 2048^2): measured in the library's own
+    // CG loop (tools/tune_shapes.py, profiles/r02_tune_shapes.jsonl; ms per
+    // iteration against the rule above): 4096x4096 one-wave blocks of 64 rows
+    // 0.477 vs 0.484; 4096x2048 1/32 0.257 vs 0.263; 4096x1024 1/40 0.141 vs
+    // 0.169; 4096x512 1/48 0.068 vs 0.079; 8192x8192 4/48 1.798 vs 1.820;
+    // 8192x1024 1/40 0.253 vs 0.260; 2048x2048 1/40 0.140 vs 0.151. Other
+    // shapes of >= 2048 rows take one-wave blocks of 40 rows.
+    static const int kShapes[][4] = {  // Nx, Wt, waves per block, rows per block
+        {4096, 4096, 1, 64}, {4096, 2048, 1, 32}, {4096, 1024, 1, 40}, {4096, 512, 1, 48},
+        {8192, 8192, 4, 48}, {8192, 1024, 1, 40}, {2048, 2048, 1, 40},
+    };
+    bool known = false;
+    for (const auto &k : kShapes)
+        if (k[0] == g.Nx && k[1] == g.Wt) {
+            c.wpb = k[2];
+            c.xchunk = k[3];
+            known = true;
+        }
+    if (!known && g.Nx >= 2048 && g.Wt >= 256) {
+        c.wpb = 1;
+        c.xchunk = 40;
+    }
+    if (const char *e = getenv("SM_CGRA_WPB")) c.wpb = atoi(e);
+    if (c.wpb != 1 && c.wpb != 2) c.wpb = 4;
+    c.TBk = (c.NWT + c.wpb - 1) / c.wpb;
     if (const char *e = getenv("SM_CGRA_XCHUNK")) c.xchunk = atoi(e);
     if (c.xchunk < 1) c.xchunk = 1;
     c.XB = (g.Nx + c.xchunk - 1) / c.xchunk;
@@ -429,33 +453,34 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
     a.Ua = Uang;
     a.fUa = fUang;
     const dim3 grid(tbn * c.XB), block(64 * c.wpb);
+    const size_t lds = sizeof(double2) * 6 * 64 * c.wpb;  // the r_j ring
     const int xp = pass >= 2 && (pass & 1) == 0;  // x takes passes j-1 and j together
     // one kernel per (shards, x pass, fold) combination
     const int f = c.fold >= 2 ? 2 : (c.fold ? 1 : 0);
     const int uc = Uang && f == 2;  // link angles: with the fused multiply-add fold only
     if (prev_partials && nshard == 1 && f == 2 && tb0 == 0 && tbn == c.TBk) {
         if (uc) {
-            if (xp) hipLaunchKernelGGL((cg_ra_kernel<0, 1, 2, 1, 1>), grid, block, 0, s, a);
-            else hipLaunchKernelGGL((cg_ra_kernel<0, 0, 2, 1, 1>), grid, block, 0, s, a);
+            if (xp) hipLaunchKernelGGL((cg_ra_kernel<0, 1, 2, 1, 1>), grid, block, lds, s, a);
+            else hipLaunchKernelGGL((cg_ra_kernel<0, 0, 2, 1, 1>), grid, block, lds, s, a);
         } else {
-            if (xp) hipLaunchKernelGGL((cg_ra_kernel<0, 1, 2, 1>), grid, block, 0, s, a);
-            else hipLaunchKernelGGL((cg_ra_kernel<0, 0, 2, 1>), grid, block, 0, s, a);
+            if (xp) hipLaunchKernelGGL((cg_ra_kernel<0, 1, 2, 1>), grid, block, lds, s, a);
+            else hipLaunchKernelGGL((cg_ra_kernel<0, 0, 2, 1>), grid, block, lds, s, a);
         }
         return;
     }
     if (uc) {
         const int sel = (nshard > 1 ? 2 : 0) + (xp ? 1 : 0);
         switch (sel) {
-            case 0: hipLaunchKernelGGL((cg_ra_kernel<0, 0, 2, 0, 1>), grid, block, 0, s, a); break;
-            case 1: hipLaunchKernelGGL((cg_ra_kernel<0, 1, 2, 0, 1>), grid, block, 0, s, a); break;
-            case 2: hipLaunchKernelGGL((cg_ra_kernel<1, 0, 2, 0, 1>), grid, block, 0, s, a); break;
-            case 3: hipLaunchKernelGGL((cg_ra_kernel<1, 1, 2, 0, 1>), grid, block, 0, s, a); break;
+            case 0: hipLaunchKernelGGL((cg_ra_kernel<0, 0, 2, 0, 1>), grid, block, lds, s, a); break;
+            case 1: hipLaunchKernelGGL((cg_ra_kernel<0, 1, 2, 0, 1>), grid, block, lds, s, a); break;
+            case 2: hipLaunchKernelGGL((cg_ra_kernel<1, 0, 2, 0, 1>), grid, block, lds, s, a); break;
+            case 3: hipLaunchKernelGGL((cg_ra_kernel<1, 1, 2, 0, 1>), grid, block, lds, s, a); break;
         }
         return;
     }
     const int sel = (nshard > 1 ? 6 : 0) + (xp ? 3 : 0) + f;
 #define SM_RA_CASE(SH, XP, F) \
-    case (SH) * 6 + (XP) * 3 + (F): hipLaunchKernelGGL((cg_ra_kernel<SH, XP, F>), grid, block, 0, s, a); break;
+    case (SH) * 6 + (XP) * 3 + (F): hipLaunchKernelGGL((cg_ra_kernel<SH, XP, F>), grid, block, lds, s, a); break;
     switch (sel) {
         SM_RA_CASE(0, 0, 0) SM_RA_CASE(0, 0, 1) SM_RA_CASE(0, 0, 2)
         SM_RA_CASE(0, 1, 0) SM_RA_CASE(0, 1, 1) SM_RA_CASE(0, 1, 2)

@@ -270,12 +270,24 @@ LaunchCfg dslash_config(const Geometry &g) {
     c.bt = g.Wt >= 256 ? 256 : (g.Wt >= 128 ? 128 : 64);
     if (const char *e = getenv("SM_BT")) c.bt = atoi(e);
     const int tb = (g.Wt + c.bt - 1) / c.bt;
-    int target = 2048;  // blocks: >> 256 CUs; 4096^2: xchunk 32 (tools/tune_dslash.py)
+    // 32-row marches where they give 256..4096 blocks, 16 rows above that,
+    // else ~2048 blocks (tools/shape_tune.hip, profiles/r02_shape_tune.jsonl,
+    // GB/s against the old 2048-block rule: 4096x2048 5648 vs 5157, 4096x512
+    // 6581 vs 6128, 8192x1024 5432 vs 5048, 8192x8192 5486 vs 5363; 4096^2
+    // is 32 rows either way)
+    const long b32 = (long)tb * ((g.Nx + 31) / 32);
+    int target = 2048;
     if (const char *e = getenv("SM_BLOCKS")) target = atoi(e);
-    int nchunks = (target + tb - 1) / tb;
-    if (nchunks > g.Nx) nchunks = g.Nx;
-    if (nchunks < 1) nchunks = 1;
-    c.xchunk = (g.Nx + nchunks - 1) / nchunks;
+    if (b32 >= 256 && b32 <= 4096 && !getenv("SM_BLOCKS")) {
+        c.xchunk = 32;
+    } else if (b32 > 4096 && !getenv("SM_BLOCKS")) {
+        c.xchunk = 16;
+    } else {
+        int nchunks = (target + tb - 1) / tb;
+        if (nchunks > g.Nx) nchunks = g.Nx;
+        if (nchunks < 1) nchunks = 1;
+        c.xchunk = (g.Nx + nchunks - 1) / nchunks;
+    }
     if (const char *e = getenv("SM_XCHUNK")) c.xchunk = atoi(e);
     c.xcd_remap = 1;
     if (const char *e = getenv("SM_XCD_REMAP")) c.xcd_remap = atoi(e);
