@@ -798,7 +798,7 @@ static int cg_ra_pass(sm_ctx *c) {
     double2 *dn = cg_dbuf(c, j);
     const CGFusedCfg &fc = c->racfg;
     const int nparts = cg_fused_blocks(fc);
-    c->cg_pending_x = 1;  // sm_cg_finish checks the device's final pass parity
+    c->cg_pending_x = 2;  // sm_cg_finish adds the rows still pending (by the final pass parity)
     c->cg_flush_pass = -1;
     const bool one = !c->sharded();
     const bool angles = c->link_angles && c->uang_state == 1;
@@ -897,7 +897,11 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
 
 int sm_cg_finish(sm_ctx *c, sm_cg_result *res) {
     if (!c || !res) return fail(SM_ERR_ARG, "null argument");
-    if (c->cg_active && c->cg_pending_x) {
+    if (c->cg_active && c->cg_pending_x == 2) {  // recompute-Ad pass: x rows by parity
+        launch_cg_ra_finish_x(c->stream, c->g, c->cg_x, cg_dbuf(c, 0), cg_dbuf(c, 1), cg_dbuf(c, 2), c->sc);
+        HIP_TRY(hipGetLastError());
+        c->cg_pending_x = 0;
+    } else if (c->cg_active && c->cg_pending_x) {
         launch_cg_td_finish_x(c->stream, 2 * c->g.V, c->cg_x, cg_dbuf(c, 0), cg_dbuf(c, 1), cg_dbuf(c, 2), c->sc);
         HIP_TRY(hipGetLastError());
         c->cg_pending_x = 0;

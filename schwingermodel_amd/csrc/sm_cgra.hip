@@ -6,15 +6,20 @@
 //                                                  src/conjugate_gradient.cpp:55-58)
 //     r_j     = r_{j-1} - alpha_{j-1} Ad_{j-1}    (:38-39)
 //     d_j     = d_{j-1} beta_{j-1} + r_j          (:55-58)
-//     x      <- (x + alpha_{j-2} d_{j-2}) + alpha_{j-1} d_{j-1}   on even j (:36-37)
+//     x      <- (x + alpha_{j-2} d_{j-2}) + alpha_{j-1} d_{j-1}   on the x rows of parity j & 1 (:36-37)
 //     Ad_j    = D D^dag d_j ; partials <d_j,Ad_j>, <r_j,Ad_j>, |r_j|^2, |Ad_j|^2
 // Mode 4 stores Ad_j and reads it back in pass j+1. Here Ad_{j-1} = D D^dag
 // d_{j-1} is recomputed from the d_{j-1} rows the pass reads anyway, with the
 // same stencil code on the same operands, so it is bitwise the value pass j-1
 // used for its dots. A pass reads d_{j-1}, d_{j-2}, U (96 B/site) and writes
-// d_j (32), plus x on even passes (64): 160 B/site mean against 224 for mode 4
-// and 576 for the reference's sequence. The price is a second
-// D^dag + D per site: fp64 VALU work that runs under the HBM time.
+// d_j (32), plus x on half the rows (32 on average): 160 B/site against 224
+// for mode 4 and 576 for the reference's sequence; 144 with
+// the links read as angles (UC). Each x row takes its two updates together
+// every other pass, the even rows on even passes and the odd rows on odd
+// ones, so every pass moves the same bytes (with all of x on even passes the
+// odd pass was VALU-bound and the even one HBM-bound). The price of the
+// recomputation is a second D^dag + D per site: fp64 VALU work that runs
+// under the HBM time.
 //
 // Geometry: a wave owns RW = 56 consecutive t-columns; its 64 lanes cover
 // columns T0-4 .. T0+59. The four stencil stages (D^dag, D on d_{j-1}; D^dag,
@@ -66,13 +71,18 @@ struct RAArgs {
     const double2 *prev;  // RED: pass j-1's partials
     long pass;
     const double *Ua, *fUa;  // UC: link angles theta_t, theta_x (plane stride V) and their 4-deep faces
+    int xpar;                // XP: this pass updates x on the rows of parity xpar (= pass & 1)
 };
 
 // U(1) link from its angle (UC): one sincos in place of a 16-B load.
 __device__ __forceinline__ double2 u_of(double th) {
+#ifdef SM_PROBE_NO_SINCOS  // timing probe only (tools/): the link load without its sincos
+    return make_double2(th, th);
+#else
     double sn, cs;
     sincos(th, &sn, &cs);
     return make_double2(cs, sn);
+#endif
 }
 
 template <typename T>
@@ -251,7 +261,7 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
             const double2 *p = S2.p + (long)wrap(min(max(xr, x0 - 2), xe + 1)) * S2.xs;
             q.a = p[0];
             q.b = p[S2.ps];
-            if (XP) {
+            if (XP && (xr & 1) == a.xpar) {  // wave-uniform: only the rows this pass updates
                 const long n = (long)wrap(min(max(xr, x0), xe - 1)) * Wt + cx;
                 xv.a = a.x[n];
                 xv.b = a.x[n + a.V];
@@ -306,7 +316,7 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
                     const long n = (long)xr * Wt + c;
                     st_nt(a.dn + n, J2.a);
                     st_nt(a.dn + n + a.V, J2.b);
-                    if (XP) {  // x_j = (x_{j-2} + alpha_{j-2} d_{j-2}) + alpha_{j-1} d_{j-1}
+                    if (XP && (xr & 1) == a.xpar) {  // x_j = (x_{j-2} + alpha_{j-2} d_{j-2}) + alpha_{j-1} d_{j-1}
                         st_nt(a.x + n, cfma<FOLD>(cfma<FOLD>(X.a, alpha2, Q.a), alpha, D2.a));
                         st_nt(a.x + n + a.V, cfma<FOLD>(cfma<FOLD>(X.b, alpha2, Q.b), alpha, D2.b));
                     }
@@ -454,7 +464,10 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
     a.fUa = fUang;
     const dim3 grid(tbn * c.XB), block(64 * c.wpb);
     const size_t lds = sizeof(double2) * 6 * 64 * c.wpb;  // the r_j ring
-    const int xp = pass >= 2 && (pass & 1) == 0;  // x takes passes j-1 and j together
+    // x takes passes j-1 and j together, on the rows of parity j & 1: every
+    // pass from 1 on updates half the rows (pass 1: alpha_{-1} = 0)
+    const int xp = pass >= 1;
+    a.xpar = (int)(pass & 1);
     // one kernel per (shards, x pass, fold) combination
     const int f = c.fold >= 2 ? 2 : (c.fold ? 1 : 0);
     const int uc = Uang && f == 2;  // link angles: with the fused multiply-add fold only
@@ -520,6 +533,31 @@ __global__ void __launch_bounds__(256) angles_of_kernel(long n, const double2 *U
 
 void launch_angles_of(hipStream_t s, long n, const double2 *U, double *Ua) {
     hipLaunchKernelGGL(angles_of_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, U, Ua);
+}
+
+// After the last pass J = k of the recompute-Ad CG, the rows of parity
+// != (k & 1) still lack alpha_{k-1} d_{k-1} (their last update was pass k-1).
+// A stopping evaluation keeps alpha = alpha_{k-1}; a non-final one has moved it
+// to alpha2 (as cg_td_finish_x_kernel).
+__global__ void __launch_bounds__(256) cg_ra_finish_x_kernel(long V, int Wt, double2 *x, const double2 *d0,
+                                                             const double2 *d1, const double2 *d2,
+                                                             const CGScalars *sc) {
+    const int k = sc->k;
+    if (k < 1) return;
+    const double2 alpha = sc->done ? sc->alpha : sc->alpha2;
+    const int i3 = (k - 1) % 3;
+    const double2 *d = i3 == 0 ? d0 : (i3 == 1 ? d1 : d2);
+    const int par = k & 1;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < 2 * V; i += (long)gridDim.x * blockDim.x) {
+        const long site = i < V ? i : i - V;
+        if ((int)((site / Wt) & 1) != par) x[i] = cfma<2>(x[i], alpha, d[i]);
+    }
+}
+
+void launch_cg_ra_finish_x(hipStream_t s, const Geometry &g, double2 *x, const double2 *d0, const double2 *d1,
+                           const double2 *d2, const CGScalars *sc) {
+    hipLaunchKernelGGL(cg_ra_finish_x_kernel, dim3(reduce_blocks(2 * g.V)), dim3(256), 0, s, g.V, g.Wt, x, d0, d1, d2,
+                       sc);
 }
 
 // k-deep t-faces: columns 0..k-1 go down (arrive as Wt..Wt+k-1), columns

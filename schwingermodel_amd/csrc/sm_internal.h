@@ -143,6 +143,10 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
 // links off the unit circle (> 1e-14 in |U|^2) to partials; returns the block count.
 int launch_link_angles(hipStream_t s, long n, const double2 *U, double *Ua, double2 *partials);
 void launch_angles_of(hipStream_t s, long n, const double2 *U, double *Ua);  // faces: angles only
+// Recompute-Ad CG: after the last pass add alpha_{k-1} d_{k-1} to the rows
+// whose x update is still pending (parity != k & 1; x row = site / Wt).
+void launch_cg_ra_finish_x(hipStream_t s, const Geometry &g, double2 *x, const double2 *d0, const double2 *d1,
+                           const double2 *d2, const CGScalars *sc);
 // prev_partials != null (one shard, fold 2): redundant scalars as in
 // cg_onepass_kernel: every block evaluates pass j-1's scalars from its partials
 // (cg1_redundant); the caller keeps the partials by pass parity and flushes.

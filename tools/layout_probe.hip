@@ -60,8 +60,10 @@ static double time_us(hipStream_t s, int K, int R, F launch) {
 }
 
 int main(int argc, char **argv) {
-    const int N = argc > 1 ? atoi(argv[1]) : 4096;
-    const long V = (long)N * N;
+    // argv[1]: "N" (N x N) or "NxxNt"; the pool is sized for the largest lattice asked
+    int N = 4096, NT = 4096;
+    if (argc > 1 && sscanf(argv[1], "%dx%d", &N, &NT) != 2) NT = N = atoi(argv[1]);
+    const long V = (long)N * NT;
     const long maxPG = 1 << 16, maxAG = 1 << 20;
     const int NF = 6;  // in/d1, U, out/dn, d2, x, spare
     const size_t pool_elems = (size_t)NF * (2 * (V + maxPG) + maxAG) + 4096;
@@ -85,20 +87,20 @@ int main(int argc, char **argv) {
         for (int k = 0; k < NF; ++k) f[k] = pool + (size_t)k * (2 * PS + AG);
         Geometry g;
         g.Nx = N;
-        g.Wt = N;
+        g.Wt = NT;
         g.t0 = 0;
-        g.Ntg = N;
+        g.Ntg = NT;
         g.V = PS;
         LaunchCfg dc = dslash_config(g);
         TFaces tf;
-        tf.lo = f[0] + (N - 1);
-        tf.lo_xs = N;
+        tf.lo = f[0] + (NT - 1);
+        tf.lo_xs = NT;
         tf.lo_ps = PS;
         tf.hi = f[0];
-        tf.hi_xs = N;
+        tf.hi_xs = NT;
         tf.hi_ps = PS;
         const double us_d = time_us(s, 20, 7, [&] {
-            launch_dslash(s, g, dc, 0, f[0], f[2], f[1], f[1] + (N - 1), tf, -0.06, nullptr, nullptr, nullptr);
+            launch_dslash(s, g, dc, 0, f[0], f[2], f[1], f[1] + (NT - 1), tf, -0.06, nullptr, nullptr, nullptr);
         });
         CGFusedCfg rc = cg_ra_config(g);
         const double us_odd = time_us(s, 10, 5, [&] {
@@ -120,11 +122,14 @@ int main(int argc, char **argv) {
                          rc.TBk, nullptr, Ua);
         });
         CHECK(hipGetLastError());
-        printf("{\"N\": %d, \"variant\": \"link angles\", \"cg_odd_us\": %.2f, \"cg_even_us\": %.2f, \"cg_iter_ms\": %.4f}\n",
-               N, us_odd_a, us_even_a, (us_odd_a + us_even_a) / 2e3);
-        printf("{\"N\": %d, \"plane_gap\": %ld, \"array_gap\": %ld, \"dslash_us\": %.2f, \"dslash_GBps\": %.1f, "
-               "\"cg_odd_us\": %.2f, \"cg_even_us\": %.2f, \"cg_iter_ms\": %.4f}\n",
-               N, PG, AG, us_d, 96.0 * V / us_d / 1e3, us_odd, us_even, (us_odd + us_even) / 2e3);
+        const double ns_site = 1e3 / (double)V;  // us -> ns per site
+        printf("{\"Nx\": %d, \"Nt\": %d, \"plane_gap\": %ld, \"array_gap\": %ld, \"dslash_us\": %.2f, "
+               "\"dslash_GBps\": %.1f, \"cg_odd_us\": %.2f, \"cg_even_us\": %.2f, \"cg_iter_ms\": %.4f, "
+               "\"angles_odd_us\": %.2f, \"angles_even_us\": %.2f, \"angles_iter_ms\": %.4f, "
+               "\"ps_per_site\": {\"dslash\": %.3f, \"cg\": %.3f, \"cg_angles\": %.3f}}\n",
+               N, NT, PG, AG, us_d, 96.0 * V / us_d / 1e3, us_odd, us_even, (us_odd + us_even) / 2e3, us_odd_a,
+               us_even_a, (us_odd_a + us_even_a) / 2e3, 1e3 * us_d * ns_site,
+               1e3 * (us_odd + us_even) / 2 * ns_site, 1e3 * (us_odd_a + us_even_a) / 2 * ns_site);
         fflush(stdout);
     }
     return 0;
