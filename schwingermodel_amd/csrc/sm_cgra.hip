@@ -47,6 +47,7 @@
 
 #include "sm_device.h"
 #include "sm_internal.h"
+#include "sm_sincos.h"
 
 #pragma clang fp contract(off)
 
@@ -74,14 +75,16 @@ struct RAArgs {
     int xpar;                // XP: this pass updates x on the rows of parity xpar (= pass & 1)
 };
 
-// U(1) link from its angle (UC): one sincos in place of a 16-B load.
+// U(1) link from its angle (UC): cos and sin of theta in [-pi, pi]
+// (sm_sincos.h: reduced-range fdlibm kernels, within 1 ulp) in place of a
+// 16-B load.
 __device__ __forceinline__ double2 u_of(double th) {
 #ifdef SM_PROBE_NO_SINCOS  // timing probe only (tools/): the link load without its sincos
     return make_double2(th, th);
 #else
-    double sn, cs;
-    sincos(th, &sn, &cs);
-    return make_double2(cs, sn);
+    double c, s;
+    sm_cos_sin_pi(th, &c, &s);
+    return make_double2(c, s);
 #endif
 }
 
