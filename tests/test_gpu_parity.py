@@ -347,3 +347,31 @@ def test_link_angles_follow_gauge_updates(sm):
         assert bits_equal(xb.view(np.float64), xbc.view(np.float64))
     finally:
         sm.check(sm.lib.sm_cg_link_angles(L.ctx, 1, None))
+
+
+@pytest.mark.parametrize("wpb,xchunk", [(1, 0), (2, 0), (1, 5), (2, 64), (4, 40), (1, 300)])
+def test_recompute_launch_geometries_agree(sm, wpb, xchunk):
+    """The recompute-Ad pass under every launch geometry sm_tune_cg_geometry
+    offers (one-, two- and four-wave blocks; chunks shorter than the halo,
+    longer than the lattice) solves to the same iteration count and x as the
+    stored-Ad pass (the reduction-order band). 200 x 150 sites: 3 waves of 56
+    columns, the last one partial."""
+    Nx, Nt = 200, 150
+    S = Nx * Nt
+    L = sm.init(Nx, Nt)
+    U, psi = sm.spinor(S), sm.spinor(S)
+    P = lambda a: a.ctypes.data  # noqa: E731
+    sm.lib.sm_fill_gauge(4321, 0.4242, Nt, 0, Nx, 0, Nt, P(U.mu0), P(U.mu1))
+    sm.lib.sm_fill_spinor(5678, Nt, 0, Nx, 0, Nt, P(psi.mu0), P(psi.mu1))
+    out = {}
+    for fused in (4, 5):
+        sm.check(sm.lib.sm_tune_cg(L.ctx, fused, 0))
+        if fused == 5:
+            sm.check(sm.lib.sm_tune_cg_geometry(L.ctx, wpb, xchunk))
+        x = sm.spinor(S)
+        assert sm.conjugate_gradient(U, psi, x, -0.12) == 1
+        out[fused] = (flat(x), L.last_cg.iterations)
+    assert abs(out[5][1] - out[4][1]) <= 1, (out[5][1], out[4][1])
+    rel = np.linalg.norm(out[5][0] - out[4][0]) / np.linalg.norm(out[4][0])
+    assert rel <= 1e-11, rel
+    assert sm.lib.sm_tune_cg_geometry(L.ctx, 3, 0) != 0  # 1, 2 or 4 waves only
