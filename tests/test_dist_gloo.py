@@ -2,7 +2,8 @@
 
 Each rank owns t in [t0, t0+Wt) from sm_shard_plan (the product's host
 geometry), exchanges its t-faces with schwingermodel_amd.dist.exchange_faces
-(the same face protocol the GPU halo uses) and applies the oracle's local
+(the transport the GPU's host-staged halo uses; the GPU ships spin-projected
+faces over it, these full-spinor faces feed the oracle) and applies the oracle's local
 operator; the gathered result must equal the reference's single-domain golden
 vectors BIT FOR BIT (the reference itself is bitwise decomposition-invariant,
 tests/golden/manifest.json "decomposition_2x2").
