@@ -484,6 +484,10 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     chk(hipHostMalloc(&c->h_face, sizeof(double) * 4 * kMaxFaceDoubles * (size_t)Nx));
     chk(hipHostMalloc(&c->h_red, sizeof(double) * 8));
     if (e == hipSuccess) chk(hipMemset(c->sc, 0, sizeof(CGScalars)));
+    // face slots start as zeros, not whatever the allocator hands back
+    if (e == hipSuccess) chk(hipMemset(c->faces, 0, sizeof(double2) * 2 * (size_t)Nx * 8));
+    if (e == hipSuccess) chk(hipMemset(c->faces2, 0, sizeof(double2) * 56 * (size_t)Nx));
+    if (e == hipSuccess) chk(hipMemset(c->faces4, 0, sizeof(double2) * 64 * (size_t)Nx));
     if (e != hipSuccess) {
         sm_destroy(c);
         return fail(SM_ERR_HIP, "allocation failed: %s", hipGetErrorString(e));
@@ -819,7 +823,10 @@ static int cg_ra_pass(sm_ctx *c) {
         }
         return SM_OK;
     }
-    double2 *f1 = one ? nullptr : face4_recv_d(c, j), *f2 = one ? nullptr : face4_recv_d(c, j - 1);
+    // pass 0 has no d_{-2}: its (zero-weighted) faces are d_0's own, never the
+    // other slot, which holds nothing of this solve yet (the zero multiplier
+    // beta2 = 0 would turn a stale NaN there into a NaN iterate)
+    double2 *f1 = one ? nullptr : face4_recv_d(c, j), *f2 = one ? nullptr : (first ? f1 : face4_recv_d(c, j - 1));
     auto pass = [&](int tb0, int tbn, hipStream_t st) {
         launch_cg_ra(st, c->g, fc, c->kshards(), d1, d2, dn, c->cg_x, c->U, f1, f2, one ? nullptr : face4_recv_U(c),
                      c->cg_mass, j, c->sc, c->partials, tb0, tbn, nullptr, ua, one ? nullptr : c->Uang_face);

@@ -149,3 +149,29 @@ def test_loopback_hmc_trajectory_and_even_odd(sm):
         assert a[1:] == b[1:], (a, b)
         assert abs(a[0] - b[0]) <= 1e-9 * max(1.0, abs(a[0])), (a, b)
     assert np.linalg.norm(U2 - U1) / np.linalg.norm(U1) <= 1e-12
+
+
+def test_loopback_cg_after_nan_solve(sm):
+    """A solve that leaves NaN in every face slot (phi = NaN) must not poison
+    the next one: pass 0 of the recompute-Ad CG weights d_{-2} by zero, so its
+    faces must be d_0's, not the previous solve's (regression: a stale NaN
+    times beta2 = 0 made the next solve run to max_iter)."""
+    Nx, Nt = 64, 4096
+    S = Nx * Nt
+    U, psi, _, _ = fields(sm, Nx, Nt, 0.2374)
+    h = lambda a: (ptr(a[:2 * S]), ptr(a[2 * S:]))  # noqa: E731
+    its = {}
+    for name, kw in (("one", {}), ("loop", {"loopback": True})):
+        L = sm.Lattice(Nx, Nt, **kw)
+        sm.check(sm.lib.sm_upload_gauge(L.ctx, *h(U)))
+        sm.check(sm.lib.sm_tune_cg(L.ctx, 5, 0))
+        bad = np.full(4 * S, np.nan)
+        x = np.empty(4 * S)
+        res = sm.CGResult()
+        sm.lib.sm_cg(L.ctx, *h(bad), *h(x), -0.06, 1e-10, 6, ctypes.byref(res))  # does not converge
+        assert res.converged == 0
+        sm.check(sm.lib.sm_cg(L.ctx, *h(psi), *h(x), -0.06, 1e-10, 10000, ctypes.byref(res)))
+        its[name] = (res.converged, res.iterations, x.copy())
+        L.close()
+    assert its["loop"][0] == its["one"][0] == 1 and its["loop"][1] == its["one"][1], (its["loop"][:2], its["one"][:2])
+    assert np.linalg.norm(its["loop"][2] - its["one"][2]) / np.linalg.norm(its["one"][2]) <= 1e-13
