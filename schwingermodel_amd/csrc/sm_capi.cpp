@@ -448,6 +448,8 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     if (const char *e = getenv("SM_CG_FUSED")) c->cg_fused = atoi(e);
     if (const char *e = getenv("SM_EDGE_CONCURRENT")) c->edge_concurrent = atoi(e);
     if (const char *e = getenv("SM_SPLIT_TEST")) c->split_test = atoi(e);
+    if (const char *e = getenv("SM_CG_FACE_PIPE")) c->cg_face_pipe = atoi(e);
+    if (const char *e = getenv("SM_CG_EDGE_XCHUNK")) c->cg_edge_xchunk = atoi(e);
     if (const char *e = getenv("SM_CGRA_RED_MAX_BLOCKS")) c->cg_ra_red_max_blocks = atoi(e);
     if (const char *e = getenv("SM_CG_REDUNDANT")) c->cg_redundant = atoi(e);
     if (const char *e = getenv("SM_EO_FUSED")) c->eo_fused = atoi(e);
@@ -712,6 +714,7 @@ int sm_cg_begin(sm_ctx *c, const double *phi, double *x, double m0, double tol) 
     c->cg_issued = 0;
     c->cg_flush_pass = -1;
     c->cg_pending_x = 0;
+    c->cg_faces_for = -1;
     return SM_OK;
 }
 
@@ -794,6 +797,17 @@ static int cg_onepass(sm_ctx *c) {
 // two-direction pass without the Ad vector, d_i in cg_dbuf(i). t-shards: the
 // 4-deep faces of d_{j-1} arrive in slot j & 1 on the comm stream while the
 // interior t-blocks run; d_{j-2}'s faces are still in slot (j-1) & 1.
+// The blocks owning columns 0..3 and Wt-4..Wt-1 (the 4-deep faces) are all
+// edge blocks (outside [tb_lo, tb_hi]), so the edge launch can pack the faces.
+static bool ra_edge_owns_faces(const sm_ctx *c, const CGFusedCfg &fc, int tb_lo, int tb_hi) {
+    const int Wt = c->g.Wt;
+    if (Wt < 8) return false;  // lo and hi columns would overlap
+    auto blk = [&](int col) { return col / kRAWaveCols / fc.wpb; };
+    for (int col : {0, 3, Wt - 4, Wt - 1})
+        if (blk(col) >= tb_lo && blk(col) <= tb_hi) return false;
+    return true;
+}
+
 static int cg_ra_pass(sm_ctx *c) {
     const long j = c->cg_issued;
     const bool first = j == 0;
@@ -827,10 +841,6 @@ static int cg_ra_pass(sm_ctx *c) {
     // other slot, which holds nothing of this solve yet (the zero multiplier
     // beta2 = 0 would turn a stale NaN there into a NaN iterate)
     double2 *f1 = one ? nullptr : face4_recv_d(c, j), *f2 = one ? nullptr : (first ? f1 : face4_recv_d(c, j - 1));
-    auto pass = [&](int tb0, int tbn, hipStream_t st) {
-        launch_cg_ra(st, c->g, fc, c->kshards(), d1, d2, dn, c->cg_x, c->U, f1, f2, one ? nullptr : face4_recv_U(c),
-                     c->cg_mass, j, c->sc, c->partials, tb0, tbn, nullptr, ua, one ? nullptr : c->Uang_face);
-    };
     // interior t-blocks: every lane's column (56g-4 .. 56g+59) inside [0, Wt)
     auto interior = [&](int tb) {
         const int g_lo = fc.wpb * tb, g_hi = std::min(fc.wpb * tb + fc.wpb - 1, fc.NWT - 1);
@@ -843,26 +853,53 @@ static int cg_ra_pass(sm_ctx *c) {
             tb_hi = tb;
         }
     const bool split = tb_hi >= tb_lo && tb_hi >= 0;
+    const bool conc = split && (one ? c->split_test == 2 : c->edge_concurrent != 0);
+    const int nint = split ? tb_hi - tb_lo + 1 : 0, nedge = fc.TBk - nint;
+    // Pipelined faces (t-shards, edge launch concurrent): the edge blocks write
+    // d_j's 4-deep send faces themselves, and the exchange for pass j+1 follows
+    // them on the comm stream, under the interior launch and the scalar step;
+    // the edge launch marches short chunks so it ends long before the interior
+    // one (its blocks otherwise run as long as the whole pass, AFTER the faces).
+    CGFusedCfg ec = fc;
+    const bool pipe = conc && !one && c->cg_face_pipe && ra_edge_owns_faces(c, fc, tb_lo, tb_hi);
+    if (pipe && c->cg_edge_xchunk > 0 && c->cg_edge_xchunk < fc.xchunk) {
+        ec.xchunk = c->cg_edge_xchunk;
+        ec.XB = (c->g.Nx + ec.xchunk - 1) / ec.xchunk;
+        if (3L * (nint * fc.XB + nedge * ec.XB) > 2L * kMaxPartials) ec = fc;
+    }
+    const int nparts_pass = split ? nint * fc.XB + nedge * ec.XB : nparts;
+    auto pass = [&](const CGFusedCfg &cf, int tb0, int tbn, hipStream_t st, int pbase, double2 *fsend) {
+        launch_cg_ra(st, c->g, cf, c->kshards(), d1, d2, dn, c->cg_x, c->U, f1, f2, one ? nullptr : face4_recv_U(c),
+                     c->cg_mass, j, c->sc, c->partials, tb0, tbn, nullptr, ua, one ? nullptr : c->Uang_face, fsend,
+                     pbase);
+    };
     HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
-    if (!one) TRY(halo4(c, c->comm_stream, d1, f1));
+    // d_{j-1}'s faces: already in slot j & 1 if pass j-1 sent them (pipe)
+    if (!one && !(pipe && c->cg_faces_for == j)) TRY(halo4(c, c->comm_stream, d1, f1));
+    c->cg_faces_for = -1;
     // edge t-blocks (tb_hi, TBk) and [0, tb_lo), wrapping: one launch on the
     // comm stream behind the faces, concurrent with the interior launch
-    const bool conc = split && (one ? c->split_test == 2 : c->edge_concurrent != 0);
-    if (conc) pass(tb_hi + 1, fc.TBk - 1 - tb_hi + tb_lo, c->comm_stream);
+    if (conc) pass(ec, tb_hi + 1, nedge, c->comm_stream, nint * fc.XB, pipe ? face4_send(c, 0) : nullptr);
     HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
-    if (split) pass(tb_lo, tb_hi - tb_lo + 1, c->stream);
+    if (split) pass(fc, tb_lo, nint, c->stream, 0, nullptr);
+    if (pipe) {  // d_j's faces into slot (j+1) & 1 (d_{j-2}'s, read by this pass's edge launch above)
+        double2 *r = face4_recv_d(c, j + 1);
+        TRY(exchange_faces_on(c, c->comm_stream, face4_send(c, 0), face4_send(c, 1), r, r + (size_t)8 * c->g.Nx,
+                              (size_t)16 * c->g.Nx));
+        c->cg_faces_for = j + 1;
+    }
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
     if (!split) {
-        pass(0, fc.TBk, c->stream);
+        pass(fc, 0, fc.TBk, c->stream, 0, nullptr);
     } else if (!conc) {
-        pass(tb_hi + 1, fc.TBk - 1 - tb_hi + tb_lo, c->stream);
+        pass(fc, tb_hi + 1, nedge, c->stream, nint * fc.XB, nullptr);
     }
     if (one) {
-        launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
+        launch_cg1_scalars(c->stream, nparts_pass, c->partials, c->sc, first);
         return SM_OK;
     }
-    launch_cg1_local_sum(c->stream, nparts, c->partials, c->sc);
+    launch_cg1_local_sum(c->stream, nparts_pass, c->partials, c->sc);
     TRY(allreduce_dev(c, (double *)c->sc->sum3, 6));
     launch_cg1_from_sums(c->stream, c->sc, first);
     return SM_OK;

@@ -73,6 +73,8 @@ struct RAArgs {
     long pass;
     const double *Ua, *fUa;  // UC: link angles theta_t, theta_x (plane stride V) and their 4-deep faces
     int xpar;                // XP: this pass updates x on the rows of parity xpar (= pass & 1)
+    int pbase;               // partial slots: tile pbase + (t-block - tb0) * XB + x-chunk
+    double2 *fsend;          // SH: != null -> the edge blocks also write d_j's 4-deep send faces
 };
 
 // U(1) link from its angle (UC): cos and sin of theta in [-pi, pi]
@@ -210,14 +212,15 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
         alpha2 = sc->alpha2;
         beta2 = rebuild ? sc->beta2 : z2;
     }
-    int tb, xc;
+    int tb, tbr, xc;
     {
         int w = blockIdx.x;
         if (a.remap) {  // consecutive ids of one XCD take x-adjacent tiles (L2 reuse of halo rows)
             const int n = a.tbn * a.XB, q = n >> 3, rr = n & 7, xcd = w & 7;
             w = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (w >> 3);
         }
-        tb = a.tb0 + w % a.tbn;
+        tbr = w % a.tbn;
+        tb = a.tb0 + tbr;
         if (tb >= a.TBk) tb -= a.TBk;  // edge block-columns TBk-1 and 0 in one launch
         xc = w / a.tbn;
     }
@@ -319,6 +322,13 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
                     const long n = (long)xr * Wt + c;
                     st_nt(a.dn + n, J2.a);
                     st_nt(a.dn + n + a.V, J2.b);
+                    if (SH && a.fsend) {  // fused face pack ([col][plane][x], lo: columns 0..3, hi: Wt-4..Wt-1)
+                        const int fcol = c < RH ? c : (c >= Wt - RH ? c - (Wt - RH) + RH : -1);
+                        if (fcol >= 0) {
+                            a.fsend[(long)(2 * fcol) * Nx + xr] = J2.a;
+                            a.fsend[(long)(2 * fcol + 1) * Nx + xr] = J2.b;
+                        }
+                    }
                     if (XP && (xr & 1) == a.xpar) {  // x_j = (x_{j-2} + alpha_{j-2} d_{j-2}) + alpha_{j-1} d_{j-1}
                         st_nt(a.x + n, cfma<FOLD>(cfma<FOLD>(X.a, alpha2, Q.a), alpha, D2.a));
                         st_nt(a.x + n + a.V, cfma<FOLD>(cfma<FOLD>(X.b, alpha2, Q.b), alpha, D2.b));
@@ -380,7 +390,7 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
     __syncthreads();
     const double2 s2 = block_sum(acc_n, sh);
     if (threadIdx.x == 0) {
-        double2 *p = a.partials + 3 * ((long)tb * a.XB + xc);  // one slot per tile
+        double2 *p = a.partials + 3 * (a.pbase + (long)tbr * a.XB + xc);  // one slot per tile
         p[0] = s0;
         p[1] = s1;
         p[2] = s2;
@@ -448,7 +458,8 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
 void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard, const double2 *d1,
                   const double2 *d2, double2 *dn, double2 *x, const double2 *U, const double2 *f1,
                   const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
-                  int tb0, int tbn, const double2 *prev_partials, const double *Uang, const double *fUang) {
+                  int tb0, int tbn, const double2 *prev_partials, const double *Uang, const double *fUang,
+                  double2 *fsend, int pbase) {
     if (tbn <= 0) return;
     RAArgs a;
     a.d1 = d1; a.d2 = d2; a.dn = dn; a.x = x; a.U = U;
@@ -465,6 +476,8 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
     a.pass = pass;
     a.Ua = Uang;
     a.fUa = fUang;
+    a.fsend = fsend;
+    a.pbase = pbase;
     const dim3 grid(tbn * c.XB), block(64 * c.wpb);
     const size_t lds = sizeof(double2) * 6 * 64 * c.wpb;  // the r_j ring
     // x takes passes j-1 and j together, on the rows of parity j & 1: every

@@ -88,6 +88,12 @@ struct sm_ctx {
     // (1: edge after interior, 2: concurrent) to measure it on one GPU.
     int edge_concurrent = 1;
     int split_test = 0;
+    // recompute-Ad CG on t-shards: the edge launch packs d_j's faces and the
+    // exchange for pass j+1 is issued right behind it (cg_faces_for: the pass
+    // whose d_{j-1} faces are already in flight); edge launch rows per block
+    int cg_face_pipe = 1;
+    int cg_edge_xchunk = 16;
+    long cg_faces_for = -1;
     ncclComm_t comm = nullptr;
     bool hosted = false;            // host-callback transport instead of RCCL
     sm_host_transport tr{};

@@ -137,7 +137,10 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
                   const double2 *d2, double2 *dn, double2 *x, const double2 *U, const double2 *f1,
                   const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
                   int tb0, int tbn, const double2 *prev_partials = nullptr, const double *Uang = nullptr,
-                  const double *fUang = nullptr);
+                  const double *fUang = nullptr, double2 *fsend = nullptr, int pbase = 0);
+// (partial slot of a tile: pbase + (t-block - tb0) * XB + x-chunk; fsend (t-shards):
+// the blocks owning columns 0..3 / Wt-4..Wt-1 also write d_j's 4-deep send
+// faces, lo at fsend and hi at fsend + 8 Nx, as launch_pack_faces_k would)
 // Link angles of U for the passes above (Uang: 16 instead of 32 B/site of
 // links): writes theta = atan2(Im, Re) of n links and, per block, the count of
 // links off the unit circle (> 1e-14 in |U|^2) to partials; returns the block count.
