@@ -139,7 +139,7 @@ int apply(sm_ctx *c, const double2 *in, double2 *out, double mass, int dagger, c
     TFaces f;
     const int TB = (c->g.Wt + c->cfg.bt - 1) / c->cfg.bt;
     const bool one = !c->sharded();
-    if (TB < 3 || (one && !c->split_test)) {
+    if (TB < 3 || (one && !c->split_test) || (!one && !c->apply_split)) {
         TRY(halo(c, in, 0, dagger ? FACE_DDAG : FACE_D, &f));
         launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip);
     } else {
@@ -449,6 +449,8 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     if (const char *e = getenv("SM_EDGE_CONCURRENT")) c->edge_concurrent = atoi(e);
     if (const char *e = getenv("SM_SPLIT_TEST")) c->split_test = atoi(e);
     if (const char *e = getenv("SM_CG_FACE_PIPE")) c->cg_face_pipe = atoi(e);
+    if (const char *e = getenv("SM_CG_TAIL")) c->cg_tail = atoi(e);
+    if (const char *e = getenv("SM_APPLY_SPLIT")) c->apply_split = atoi(e);
     if (const char *e = getenv("SM_CG_EDGE_XCHUNK")) c->cg_edge_xchunk = atoi(e);
     if (const char *e = getenv("SM_CGRA_RED_MAX_BLOCKS")) c->cg_ra_red_max_blocks = atoi(e);
     if (const char *e = getenv("SM_CG_REDUNDANT")) c->cg_redundant = atoi(e);
@@ -481,11 +483,14 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     chk(hipMalloc(&c->sums, sizeof(double2) * 4));
     chk(hipMalloc(&c->Fbuf, sizeof(double) * 2 * (size_t)c->g.V));
     chk(hipMalloc(&c->sc, sizeof(CGScalars)));
+    chk(hipMalloc(&c->tick, sizeof(unsigned) * (1 + kMaxTickGroups)));
+    chk(hipMalloc(&c->gsum, sizeof(double2) * 3 * kMaxTickGroups));
     chk(hipHostMalloc(&c->h_sc, sizeof(CGScalars)));
     chk(hipHostMalloc(&c->h_sums, sizeof(double2) * 4));
     chk(hipHostMalloc(&c->h_face, sizeof(double) * 4 * kMaxFaceDoubles * (size_t)Nx));
     chk(hipHostMalloc(&c->h_red, sizeof(double) * 8));
     if (e == hipSuccess) chk(hipMemset(c->sc, 0, sizeof(CGScalars)));
+    if (e == hipSuccess) chk(hipMemset(c->tick, 0, sizeof(unsigned) * (1 + kMaxTickGroups)));
     // face slots start as zeros, not whatever the allocator hands back
     if (e == hipSuccess) chk(hipMemset(c->faces, 0, sizeof(double2) * 2 * (size_t)Nx * 8));
     if (e == hipSuccess) chk(hipMemset(c->faces2, 0, sizeof(double2) * 56 * (size_t)Nx));
@@ -531,9 +536,11 @@ int sm_destroy(sm_ctx *c) {
     if (!c) return SM_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);  // e.g. a CG's trailing face exchange
     if (c->comm) ncclCommDestroy(c->comm);
     void *dev[] = {c->U, c->ghostU, c->fields, c->faces, c->faces2, c->faces4, c->partials, c->sums, c->Fbuf, c->sc,
-                   c->U_alt, c->Pmd, c->Fmd, c->eo, c->Ucb, c->eo_faces, c->eo_faces4, c->Uang, c->Uang_face};
+                   c->U_alt, c->Pmd, c->Fmd, c->eo, c->Ucb, c->eo_faces, c->eo_faces4, c->Uang, c->Uang_face,
+                   c->tick, c->gsum};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_sc) (void)hipHostFree(c->h_sc);
@@ -827,12 +834,14 @@ static int cg_ra_pass(sm_ctx *c) {
         const bool red = c->cg_redundant && fc.fold >= 2 && nparts <= c->cg_ra_red_max_blocks;
         double2 *part = red ? c->partials + (j & 1) * 3 * (size_t)nparts : c->partials;
         const double2 *prev = red ? c->partials + ((j + 1) & 1) * 3 * (size_t)nparts : nullptr;
+        const bool tail = !red && c->cg_tail && fc.fold >= 2 && (nparts + 63) / 64 <= kMaxTickGroups;
         launch_cg_ra(c->stream, c->g, fc, 1, d1, d2, dn, c->cg_x, c->U, nullptr, nullptr, nullptr, c->cg_mass, j,
-                     c->sc, part, 0, fc.TBk, prev, ua);
+                     c->sc, part, 0, fc.TBk, prev, ua, nullptr, nullptr, 0, tail ? c->tick : nullptr, nparts, c->gsum,
+                     nullptr);
         if (red) {
             c->cg_flush_pass = j;
             c->cg_flush_nparts = nparts;
-        } else {
+        } else if (!tail) {
             launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
         }
         return SM_OK;
@@ -868,10 +877,14 @@ static int cg_ra_pass(sm_ctx *c) {
         if (3L * (nint * fc.XB + nedge * ec.XB) > 2L * kMaxPartials) ec = fc;
     }
     const int nparts_pass = split ? nint * fc.XB + nedge * ec.XB : nparts;
+    double2 *sums = c->sc->sum3;  // this shard's sums (all-reduced below)
+    // ticketed tail: the pass's last block forms the scalars (one shard) or
+    // this shard's sums, instead of a separate kernel
+    const bool tail = c->cg_tail && fc.fold >= 2 && (nparts_pass + 63) / 64 <= kMaxTickGroups;
     auto pass = [&](const CGFusedCfg &cf, int tb0, int tbn, hipStream_t st, int pbase, double2 *fsend) {
         launch_cg_ra(st, c->g, cf, c->kshards(), d1, d2, dn, c->cg_x, c->U, f1, f2, one ? nullptr : face4_recv_U(c),
                      c->cg_mass, j, c->sc, c->partials, tb0, tbn, nullptr, ua, one ? nullptr : c->Uang_face, fsend,
-                     pbase);
+                     pbase, tail ? c->tick : nullptr, nparts_pass, c->gsum, one ? nullptr : sums);
     };
     HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
@@ -896,11 +909,11 @@ static int cg_ra_pass(sm_ctx *c) {
         pass(fc, tb_hi + 1, nedge, c->stream, nint * fc.XB, nullptr);
     }
     if (one) {
-        launch_cg1_scalars(c->stream, nparts_pass, c->partials, c->sc, first);
+        if (!tail) launch_cg1_scalars(c->stream, nparts_pass, c->partials, c->sc, first);
         return SM_OK;
     }
-    launch_cg1_local_sum(c->stream, nparts_pass, c->partials, c->sc);
-    TRY(allreduce_dev(c, (double *)c->sc->sum3, 6));
+    if (!tail) launch_cg1_local_sum(c->stream, nparts_pass, c->partials, c->sc);
+    TRY(allreduce_dev(c, (double *)sums, 6));
     launch_cg1_from_sums(c->stream, c->sc, first);
     return SM_OK;
 }
@@ -941,6 +954,10 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
 
 int sm_cg_finish(sm_ctx *c, sm_cg_result *res) {
     if (!c || !res) return fail(SM_ERR_ARG, "null argument");
+    if (c->cg_active && c->sharded()) {  // the last pass's face exchange (pipelined faces) joins the main stream
+        HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+    }
     if (c->cg_active && c->cg_pending_x == 2) {  // recompute-Ad pass: x rows by parity
         launch_cg_ra_finish_x(c->stream, c->g, c->cg_x, cg_dbuf(c, 0), cg_dbuf(c, 1), cg_dbuf(c, 2), c->sc);
         HIP_TRY(hipGetLastError());

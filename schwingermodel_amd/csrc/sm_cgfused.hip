@@ -326,31 +326,8 @@ __device__ void sum3_partials(int nparts, const double2 *part, double2 out[3]) {
         }
 }
 
-__device__ __forceinline__ void store_state(CGScalars *sc, const CGRed &s) {
-    sc->rn = s.rn;
-    sc->alpha = s.alpha;
-    sc->beta = s.beta;
-    sc->alpha2 = s.alpha2;
-    sc->beta2 = s.beta2;
-    sc->err = s.err;
-    sc->k = s.k;
-    sc->done = s.done;
-    sc->converged = s.converged;
-}
-
 __device__ __attribute__((noinline)) void cg1_scalars(CGScalars *sc, int first, double2 dA, double2 rA, double2 nn) {
-    CGRed s;
-    s.rn = sc->rn;
-    s.alpha = sc->alpha;
-    s.beta = sc->beta;
-    s.alpha2 = sc->alpha2;
-    s.beta2 = sc->beta2;
-    s.err = sc->err;
-    s.k = sc->k;
-    s.done = sc->done;
-    s.converged = sc->converged;
-    s.pad = 0;
-    store_state(sc, cg1_eval(s, sc->tol, sc->phi_norm, sc->max_iter, first, dA, rA, nn));
+    cg1_update(sc, first, dA, rA, nn);
 }
 
 // Redundant-scalar path: S_J of the last issued pass J into red[J & 1] and the

@@ -43,6 +43,13 @@
 // the dots with fused multiply-adds: one rounding where GCC's expansion has
 // two or three, so the iterates differ from FOLD = 1 at rounding level (the
 // parity bar for CG is the converged solution, 1e-12).
+//
+// TK = 1 (the default with FOLD = 2 on grids that do not take the redundant
+// scalars) ends the pass with a ticketed tail instead of a separate scalar
+// kernel: the last block of each group of 64 tiles sums the group's partials,
+// the last group's block sums the group sums in order and forms the scalars
+// (one shard) or writes the shard's three sums for the all-reduce (t-shards).
+// The order is fixed, so results stay run-to-run reproducible.
 #include <type_traits>
 
 #include "sm_device.h"
@@ -75,6 +82,12 @@ struct RAArgs {
     int xpar;                // XP: this pass updates x on the rows of parity xpar (= pass & 1)
     int pbase;               // partial slots: tile pbase + (t-block - tb0) * XB + x-chunk
     double2 *fsend;          // SH: != null -> the edge blocks also write d_j's 4-deep send faces
+    // TK (ticketed tail): counters tick[0] (groups) and tick[1 + g] (64 tiles
+    // each), ntiles tiles over every launch of the pass, group sums gsum; the
+    // last block forms the scalars (out3 == null) or writes the 3 sums to out3
+    unsigned *tick;
+    int ntiles;
+    double2 *gsum, *out3;
 };
 
 // U(1) link from its angle (UC): cos and sin of theta in [-pi, pi]
@@ -172,7 +185,7 @@ __device__ __forceinline__ Sp ra_site(double mass, double sr0, double sl0, const
     return o;
 }
 
-template <int SH, int XP, int FOLD, int RED = 0, int UC = 0>
+template <int SH, int XP, int FOLD, int RED = 0, int UC = 0, int TK = 0>
 __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
     __shared__ double2 sh[4];
     extern __shared__ double2 rlds[];  // r_j ring: 3 slots x 2 planes x blockDim (dynamic: sized by waves per block)
@@ -389,11 +402,68 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
     const double2 s1 = block_sum(acc_rA, sh);
     __syncthreads();
     const double2 s2 = block_sum(acc_n, sh);
+    const long tile = a.pbase + (long)tbr * a.XB + xc;
+    double2 *p = a.partials + 3 * tile;  // one slot per tile
+    if (!TK) {
+        if (threadIdx.x == 0) {
+            p[0] = s0;
+            p[1] = s1;
+            p[2] = s2;
+        }
+        return;
+    }
+    // Ticketed tail: the last block of each group of 64 tiles sums the group
+    // (one wave, one tile per lane, fixed butterfly order), the last group's
+    // block sums the group sums in order and forms the scalars (or writes the
+    // shard's sums for the all-reduce), so no scalar / local-sum kernel follows.
     if (threadIdx.x == 0) {
-        double2 *p = a.partials + 3 * (a.pbase + (long)tbr * a.XB + xc);  // one slot per tile
-        p[0] = s0;
-        p[1] = s1;
-        p[2] = s2;
+        publish_partial(p, s0);
+        publish_partial(p + 1, s1);
+        publish_partial(p + 2, s2);
+    }
+    __shared__ int s_last;
+    const int grp = (int)(tile >> 6);
+    const int gsz = min(64, a.ntiles - (grp << 6));
+    if (!last_block_arrive(a.tick + 1 + grp, (unsigned)gsz, &s_last)) return;
+    const double2 zz = make_double2(0.0, 0.0);
+    if (threadIdx.x < 64) {
+        double2 v0 = zz, v1 = zz, v2 = zz;
+        if (lane < gsz) {
+            const double2 *q = a.partials + 3 * (((long)grp << 6) + lane);
+            v0 = load_published(q);
+            v1 = load_published(q + 1);
+            v2 = load_published(q + 2);
+        }
+        v0 = wave_sum(v0);
+        v1 = wave_sum(v1);
+        v2 = wave_sum(v2);
+        if (lane == 0) {
+            publish_partial(a.gsum + 3 * grp, v0);
+            publish_partial(a.gsum + 3 * grp + 1, v1);
+            publish_partial(a.gsum + 3 * grp + 2, v2);
+        }
+    }
+    const int ngrp = (a.ntiles + 63) >> 6;
+    if (!last_block_arrive(a.tick, (unsigned)ngrp, &s_last)) return;
+    if (threadIdx.x < 64) {
+        double2 v0 = zz, v1 = zz, v2 = zz;
+        for (int i = lane; i < ngrp; i += 64) {
+            v0 = cadd(v0, load_published(a.gsum + 3 * i));
+            v1 = cadd(v1, load_published(a.gsum + 3 * i + 1));
+            v2 = cadd(v2, load_published(a.gsum + 3 * i + 2));
+        }
+        v0 = wave_sum(v0);
+        v1 = wave_sum(v1);
+        v2 = wave_sum(v2);
+        if (lane == 0) {
+            if (a.out3) {
+                a.out3[0] = v0;
+                a.out3[1] = v1;
+                a.out3[2] = v2;
+            } else {
+                cg1_update(sc, a.first, v0, v1, v2);
+            }
+        }
     }
 }
 
@@ -455,11 +525,24 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
     return c;
 }
 
+template <int SH, int RED, int UC, int F>
+static void ra_go(int xp, int tk, dim3 grid, dim3 block, size_t lds, hipStream_t s, const RAArgs &a) {
+    if constexpr (F == 2) {
+        if (tk) {
+            if (xp) hipLaunchKernelGGL((cg_ra_kernel<SH, 1, F, RED, UC, 1>), grid, block, lds, s, a);
+            else hipLaunchKernelGGL((cg_ra_kernel<SH, 0, F, RED, UC, 1>), grid, block, lds, s, a);
+            return;
+        }
+    }
+    if (xp) hipLaunchKernelGGL((cg_ra_kernel<SH, 1, F, RED, UC, 0>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((cg_ra_kernel<SH, 0, F, RED, UC, 0>), grid, block, lds, s, a);
+}
+
 void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard, const double2 *d1,
                   const double2 *d2, double2 *dn, double2 *x, const double2 *U, const double2 *f1,
                   const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
                   int tb0, int tbn, const double2 *prev_partials, const double *Uang, const double *fUang,
-                  double2 *fsend, int pbase) {
+                  double2 *fsend, int pbase, unsigned *tick, int ntiles, double2 *gsum, double2 *out3) {
     if (tbn <= 0) return;
     RAArgs a;
     a.d1 = d1; a.d2 = d2; a.dn = dn; a.x = x; a.U = U;
@@ -478,45 +561,41 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
     a.fUa = fUang;
     a.fsend = fsend;
     a.pbase = pbase;
+    a.tick = tick;
+    a.ntiles = ntiles;
+    a.gsum = gsum;
+    a.out3 = out3;
     const dim3 grid(tbn * c.XB), block(64 * c.wpb);
     const size_t lds = sizeof(double2) * 6 * 64 * c.wpb;  // the r_j ring
     // x takes passes j-1 and j together, on the rows of parity j & 1: every
     // pass from 1 on updates half the rows (pass 1: alpha_{-1} = 0)
     const int xp = pass >= 1;
     a.xpar = (int)(pass & 1);
-    // one kernel per (shards, x pass, fold) combination
+    // one kernel per (shards, x pass, fold, scalar mode, link form, tail) combination
     const int f = c.fold >= 2 ? 2 : (c.fold ? 1 : 0);
     const int uc = Uang && f == 2;  // link angles: with the fused multiply-add fold only
+    const int tk = tick != nullptr && f == 2;
     if (prev_partials && nshard == 1 && f == 2 && tb0 == 0 && tbn == c.TBk) {
+        if (uc) ra_go<0, 1, 1, 2>(xp, 0, grid, block, lds, s, a);
+        else ra_go<0, 1, 0, 2>(xp, 0, grid, block, lds, s, a);
+        return;
+    }
+    const bool sh = nshard > 1;
+    if (f == 2) {
         if (uc) {
-            if (xp) hipLaunchKernelGGL((cg_ra_kernel<0, 1, 2, 1, 1>), grid, block, lds, s, a);
-            else hipLaunchKernelGGL((cg_ra_kernel<0, 0, 2, 1, 1>), grid, block, lds, s, a);
+            if (sh) ra_go<1, 0, 1, 2>(xp, tk, grid, block, lds, s, a);
+            else ra_go<0, 0, 1, 2>(xp, tk, grid, block, lds, s, a);
         } else {
-            if (xp) hipLaunchKernelGGL((cg_ra_kernel<0, 1, 2, 1>), grid, block, lds, s, a);
-            else hipLaunchKernelGGL((cg_ra_kernel<0, 0, 2, 1>), grid, block, lds, s, a);
+            if (sh) ra_go<1, 0, 0, 2>(xp, tk, grid, block, lds, s, a);
+            else ra_go<0, 0, 0, 2>(xp, tk, grid, block, lds, s, a);
         }
-        return;
+    } else if (f == 1) {
+        if (sh) ra_go<1, 0, 0, 1>(xp, 0, grid, block, lds, s, a);
+        else ra_go<0, 0, 0, 1>(xp, 0, grid, block, lds, s, a);
+    } else {
+        if (sh) ra_go<1, 0, 0, 0>(xp, 0, grid, block, lds, s, a);
+        else ra_go<0, 0, 0, 0>(xp, 0, grid, block, lds, s, a);
     }
-    if (uc) {
-        const int sel = (nshard > 1 ? 2 : 0) + (xp ? 1 : 0);
-        switch (sel) {
-            case 0: hipLaunchKernelGGL((cg_ra_kernel<0, 0, 2, 0, 1>), grid, block, lds, s, a); break;
-            case 1: hipLaunchKernelGGL((cg_ra_kernel<0, 1, 2, 0, 1>), grid, block, lds, s, a); break;
-            case 2: hipLaunchKernelGGL((cg_ra_kernel<1, 0, 2, 0, 1>), grid, block, lds, s, a); break;
-            case 3: hipLaunchKernelGGL((cg_ra_kernel<1, 1, 2, 0, 1>), grid, block, lds, s, a); break;
-        }
-        return;
-    }
-    const int sel = (nshard > 1 ? 6 : 0) + (xp ? 3 : 0) + f;
-#define SM_RA_CASE(SH, XP, F) \
-    case (SH) * 6 + (XP) * 3 + (F): hipLaunchKernelGGL((cg_ra_kernel<SH, XP, F>), grid, block, lds, s, a); break;
-    switch (sel) {
-        SM_RA_CASE(0, 0, 0) SM_RA_CASE(0, 0, 1) SM_RA_CASE(0, 0, 2)
-        SM_RA_CASE(0, 1, 0) SM_RA_CASE(0, 1, 1) SM_RA_CASE(0, 1, 2)
-        SM_RA_CASE(1, 0, 0) SM_RA_CASE(1, 0, 1) SM_RA_CASE(1, 0, 2)
-        SM_RA_CASE(1, 1, 0) SM_RA_CASE(1, 1, 1) SM_RA_CASE(1, 1, 2)
-    }
-#undef SM_RA_CASE
 }
 
 // Link angles for the UC passes: theta = atan2(Im U, Re U) for each of the n

@@ -92,8 +92,14 @@ struct sm_ctx {
     // exchange for pass j+1 is issued right behind it (cg_faces_for: the pass
     // whose d_{j-1} faces are already in flight); edge launch rows per block
     int cg_face_pipe = 1;
+    int apply_split = 1;            // t-shard Dirac apply: interior / edge launches around the faces (0: faces first)
     int cg_edge_xchunk = 16;
     long cg_faces_for = -1;
+    // recompute-Ad pass: ticketed tail (the pass's last block sums the partials
+    // by groups of 64 and forms the scalars / the shard's sums), no scalar kernel
+    int cg_tail = 1;
+    unsigned *tick = nullptr;       // 1 + kMaxTickGroups counters, zeroed at creation
+    double2 *gsum = nullptr;        // 3 per group
     ncclComm_t comm = nullptr;
     bool hosted = false;            // host-callback transport instead of RCCL
     sm_host_transport tr{};

@@ -218,6 +218,35 @@ __device__ __forceinline__ CGRed cg1_eval(CGRed s, double tol, double phi_norm, 
     return s;
 }
 
+__device__ __forceinline__ void store_state(CGScalars *sc, const CGRed &s) {
+    sc->rn = s.rn;
+    sc->alpha = s.alpha;
+    sc->beta = s.beta;
+    sc->alpha2 = s.alpha2;
+    sc->beta2 = s.beta2;
+    sc->err = s.err;
+    sc->k = s.k;
+    sc->done = s.done;
+    sc->converged = s.converged;
+}
+
+// One scalar step on the state in sc (the scalar kernel's, or the ticketed
+// tail's last block, sm_cgra.hip).
+__device__ __forceinline__ void cg1_update(CGScalars *sc, int first, double2 dA, double2 rA, double2 nn) {
+    CGRed s;
+    s.rn = sc->rn;
+    s.alpha = sc->alpha;
+    s.beta = sc->beta;
+    s.alpha2 = sc->alpha2;
+    s.beta2 = sc->beta2;
+    s.err = sc->err;
+    s.k = sc->k;
+    s.done = sc->done;
+    s.converged = sc->converged;
+    s.pad = 0;
+    store_state(sc, cg1_eval(s, sc->tol, sc->phi_norm, sc->max_iter, first, dA, rA, nn));
+}
+
 // Redundant scalars: S_{j-1} from S_{j-2} (red[j & 1]) and pass j-1's partials,
 // evaluated by every block (all threads: block sums in a fixed order); block 0
 // stores it to red[(j-1) & 1]. Returns S_{j-1} (valid in thread 0).
@@ -317,4 +346,42 @@ __device__ __forceinline__ void cg_beta_scalar(CGScalars *sc, double2 rr) {
     sc->rn = make_double2(err_sqr, 0.0);
 }
 
+// Ticketed tail (sm_cgra.hip, TK): blocks publish their partials with
+// write-through (agent-scope atomic) stores -- no release fence, which would
+// write back the XCD's whole dirty L2 in every block -- wait for them, then
+// take a relaxed agent-scope ticket; the block drawing the last ticket of a
+// group reads the group's partials with agent-scope atomic loads and re-arms
+// the counter (zeroed at context creation).
+__device__ __forceinline__ void publish_partial(double2 *slot, double2 v) {
+    __hip_atomic_store(&slot->x, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&slot->y, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double2 load_published(const double2 *slot) {
+    return make_double2(__hip_atomic_load(&slot->x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                        __hip_atomic_load(&slot->y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+// Every thread of the block calls it; true in the block that arrived last.
+__device__ __forceinline__ bool last_block_arrive(unsigned *counter, unsigned nblocks, int *sh_flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through stores are done
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = t == nblocks - 1;
+        if (last) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *sh_flag = last;
+    }
+    __syncthreads();
+    return *sh_flag != 0;
+}
+// Fixed-order wave sum (butterfly; every lane gets the same bits).
+__device__ __forceinline__ double2 wave_sum(double2 v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        v.x += __shfl_xor(v.x, off);
+        v.y += __shfl_xor(v.y, off);
+    }
+    return v;
+}
+
 }  // namespace sm
+

@@ -137,7 +137,12 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
                   const double2 *d2, double2 *dn, double2 *x, const double2 *U, const double2 *f1,
                   const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
                   int tb0, int tbn, const double2 *prev_partials = nullptr, const double *Uang = nullptr,
-                  const double *fUang = nullptr, double2 *fsend = nullptr, int pbase = 0);
+                  const double *fUang = nullptr, double2 *fsend = nullptr, int pbase = 0,
+                  unsigned *tick = nullptr, int ntiles = 0, double2 *gsum = nullptr, double2 *out3 = nullptr);
+// (tick != null: ticketed tail over the ntiles tiles of every launch of the
+// pass -- the last block forms the scalars in sc, or writes the shard's three
+// sums to out3; tick holds 1 + ceil(ntiles / 64) zeroed counters, gsum 3 per group)
+constexpr int kMaxTickGroups = 1024;
 // (partial slot of a tile: pbase + (t-block - tb0) * XB + x-chunk; fsend (t-shards):
 // the blocks owning columns 0..3 / Wt-4..Wt-1 also write d_j's 4-deep send
 // faces, lo at fsend and hi at fsend + 8 Nx, as launch_pack_faces_k would)

@@ -10,7 +10,8 @@ six scalars and the scalar kernel). The difference per iteration is what a
 t-shard pays on top of its own stencil work, minus the xGMI wire time.
 
     python tools/loopback_probe.py [--shapes 4096x512,4096x1024] [--iters 200] [--rounds 3]
-Prints one JSON line per (shape, context): ms per CG iteration (median over rounds).
+Prints one JSON line per (shape, context): ms per CG iteration and us per
+Dirac apply (medians over rounds).
 """
 import argparse
 import ctypes
@@ -29,6 +30,7 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--applies", type=int, default=50)
     ap.add_argument("--m0", type=float, default=-0.06)
     ap.add_argument("--sigma", type=float, default=0.2374)
     a = ap.parse_args()
@@ -68,9 +70,23 @@ def main():
                 sm.check(sm.lib.sm_cg_finish(L.ctx, ctypes.byref(res)))
                 if res.converged or res.iterations != a.warmup + a.iters - 1:
                     raise SystemExit(f"{k} {shape}: {res.iterations} iterations, converged={res.converged}")
+        # the Dirac apply (1-deep spin-projected faces, interior / edge split)
+        out = torch.empty_like(phi)
+        ap = {k: [] for k in ctxs}
+        for _ in range(a.rounds):
+            for k, L in ctxs.items():
+                for _ in range(3):
+                    sm.check(sm.lib.sm_dirac_dev(L.ctx, vp(phi), vp(out), a.m0, 0))
+                e0.record(s)
+                for _ in range(a.applies):
+                    sm.check(sm.lib.sm_dirac_dev(L.ctx, vp(phi), vp(out), a.m0, 0))
+                e1.record(s)
+                e1.synchronize()
+                ap[k].append(e0.elapsed_time(e1) * 1e3 / a.applies)
         for k, L in ctxs.items():
             print(json.dumps({"shape": shape, "context": k, "ms_per_iter": round(statistics.median(times[k]), 4),
-                              "min": round(min(times[k]), 4), "iters": a.iters}), flush=True)
+                              "min": round(min(times[k]), 4), "iters": a.iters,
+                              "apply_us": round(statistics.median(ap[k]), 2)}), flush=True)
             L.close()
         del dU, phi, x
 
