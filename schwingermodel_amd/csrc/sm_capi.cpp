@@ -450,6 +450,10 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     if (const char *e = getenv("SM_SPLIT_TEST")) c->split_test = atoi(e);
     if (const char *e = getenv("SM_CG_FACE_PIPE")) c->cg_face_pipe = atoi(e);
     if (const char *e = getenv("SM_CG_TAIL")) c->cg_tail = atoi(e);
+    // t-shard apply: faces first, then one launch, on shards narrower than 2048
+    // (RCCL loopback, us per apply: 4096x1024 79 vs 91 split; 4096x2048 166 vs
+    // 164, 4096^2 296 vs 292; profiles/r02_v8_apply_split.log)
+    c->apply_split = c->g.Wt >= 2048 ? 1 : 0;
     if (const char *e = getenv("SM_APPLY_SPLIT")) c->apply_split = atoi(e);
     if (const char *e = getenv("SM_CG_EDGE_XCHUNK")) c->cg_edge_xchunk = atoi(e);
     if (const char *e = getenv("SM_CGRA_RED_MAX_BLOCKS")) c->cg_ra_red_max_blocks = atoi(e);

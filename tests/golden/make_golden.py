@@ -166,6 +166,49 @@ def make_hmc_stat(log_dir=None):
     return dict(c, **res, program="reference src/main.cpp (CPU, 1 rank)")
 
 
+def make_hmc_stat_chains(k, prior):
+    """k more independent runs of the reference HMC program (it seeds rand()
+    from the clock in seconds, src/main.cpp:17, so the starts are 2 s apart),
+    run in parallel; returns each chain's statistics and the pooled mean of
+    these and the prior recorded chain (independent: error = sqrt(sum dEp^2) / n)."""
+    import time
+    c = HMC_STAT
+    params = f"1\n1\n{c['m0']}\n{c['md_steps']}\n{c['tau']}\n{c['beta']}\n{c['Ntherm']}\n{c['Nmeas']}\n{c['Nsteps']}\n0\n"
+    exe = os.path.join(REF_DIR, f"SM_{c['Nx']}x{c['Nt']}_ref")
+    chains = []
+    with tempfile.TemporaryDirectory() as root:
+        procs = []
+        for i in range(k):
+            d = os.path.join(root, f"chain{i}")
+            os.makedirs(d)
+            env = dict(os.environ, HOSTNAME=os.environ.get("HOSTNAME", "localhost"))
+            p = subprocess.Popen([exe], stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                 cwd=d, text=True, env=env)
+            p.stdin.write(params)
+            p.stdin.close()
+            procs.append((d, p))
+            time.sleep(2.2)
+        for d, p in procs:
+            out, err = p.stdout.read(), p.stderr.read()
+            p.wait(timeout=3600)
+            if p.returncode != 0 or "Ep = " not in out:
+                raise SystemExit(f"reference HMC chain failed ({p.returncode}):\n{out[-2000:]}\n{err[-2000:]}")
+            sim = [f for f in os.listdir(d) if f.endswith("_SimData.txt")][0]
+            with open(os.path.join(d, sim)) as f:
+                chains.append(parse_hmc_output(out, f.read()))
+    base = {key: HMC_STAT[key] for key in HMC_STAT}
+    allc = [{key: prior[key] for key in ("Ep", "dEp", "gS", "dgS", "acceptance", "seconds")}] + chains
+    n = len(allc)
+    pooled = {
+        "Ep": sum(ch["Ep"] for ch in allc) / n,
+        "dEp": (sum(ch["dEp"] ** 2 for ch in allc)) ** 0.5 / n,
+        "gS": sum(ch["gS"] for ch in allc) / n,
+        "dgS": (sum(ch["dgS"] ** 2 for ch in allc)) ** 0.5 / n,
+        "acceptance": sum(ch["acceptance"] for ch in allc) / n,
+    }
+    return dict(base, chains=allc, pooled=pooled, program="reference src/main.cpp (CPU, 1 rank), independent chains")
+
+
 def make_md(name, nx, nt, sigma, m0, beta, tau, steps, mpi=None):
     exe = os.path.join(REF_DIR, f"sm_ref_{nx}x{nt}")
     S = nx * nt
@@ -229,6 +272,8 @@ def main():
     ap.add_argument("--md-only", action="store_true", help="regenerate only the MD fixtures")
     ap.add_argument("--hmc-stat", action="store_true", help="(re)run the reference HMC program (~2 min)")
     ap.add_argument("--hmc-log-dir", default=None, help="reuse a finished reference HMC run directory")
+    ap.add_argument("--hmc-chains", type=int, default=0,
+                    help="run this many more independent reference HMC chains in parallel (~4 min) into hmc_stat_chains")
     ap.add_argument("--conf-only", action="store_true", help="regenerate only the SaveConf fixtures")
     args = ap.parse_args()
     if args.conf_only:
@@ -239,6 +284,15 @@ def main():
         with open(path) as f:
             manifest = json.load(f)
         manifest["conf"] = {n: make_conf(n, nx, nt, sg, rk, args.mpirun) for n, nx, nt, sg, rk in CONF_FIXTURES}
+        with open(path, "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+        return
+    if args.hmc_chains:
+        path = os.path.join(HERE, "manifest.json")
+        with open(path) as f:
+            manifest = json.load(f)
+        manifest["hmc_stat_chains"] = make_hmc_stat_chains(args.hmc_chains, manifest["hmc_stat"])
+        print(json.dumps(manifest["hmc_stat_chains"]["pooled"]), file=sys.stderr)
         with open(path, "w") as f:
             json.dump(manifest, f, indent=1, sort_keys=True)
         return

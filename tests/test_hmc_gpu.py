@@ -2,10 +2,12 @@
 `sm_hmc` program (the reference's src/main.cpp over libsm_hip.so).
 
 The reference seeds its RNG from the clock, so parity of a Markov chain is
-statistical: the same physics parameters as a recorded run of the unmodified
-reference program (tests/golden/manifest.json "hmc_stat", make_golden.py
---hmc-stat) must give the average plaquette and gauge action within their
-combined jackknife errors (4 sigma) and a similar acceptance rate. Everything
+statistical: the same physics parameters as seven recorded independent runs of
+the unmodified reference program (tests/golden/manifest.json "hmc_stat" and
+"hmc_stat_chains", make_golden.py --hmc-stat / --hmc-chains 6) must give the
+average plaquette and gauge action within 4 combined sigmas of the pooled
+reference mean (errors from the chains' scatter, no fixed slack) and a similar
+acceptance rate. Everything
 else is checked exactly: the summary statistics against a restatement over
 the returned series, the trajectory count, and the configuration files.
 """
@@ -32,8 +34,27 @@ def sm():
 
 @pytest.fixture(scope="module")
 def ref():
+    """The recorded reference chain's parameters, with the pooled statistics of
+    all recorded independent reference chains (make_golden.py --hmc-chains)."""
     with open(os.path.join(GOLDEN, "manifest.json")) as f:
-        return json.load(f)["hmc_stat"]
+        m = json.load(f)
+    r = dict(m["hmc_stat"])
+    if "hmc_stat_chains" in m:
+        ch = m["hmc_stat_chains"]["chains"]
+        n = len(ch)
+        r.update(m["hmc_stat_chains"]["pooled"])
+        r["n_chains"] = n
+        # successive trajectories are correlated, so a chain's binned jackknife
+        # error understates it: take the reference error from the scatter of
+        # the independent chains' means, and the factor by which that scatter
+        # exceeds the chains' own jackknife errors to inflate ours
+        for key, dkey in (("Ep", "dEp"), ("gS", "dgS")):
+            mean = sum(c[key] for c in ch) / n
+            sd = math.sqrt(sum((c[key] - mean) ** 2 for c in ch) / (n - 1))
+            rms_jk = math.sqrt(sum(c[dkey] ** 2 for c in ch) / n)
+            r[dkey] = sd / math.sqrt(n)
+            r["inflate_" + key] = max(1.0, sd / rms_jk)
+    return r
 
 
 def seq_mean(x):
@@ -49,7 +70,7 @@ def test_hmc_run_matches_reference_statistics(sm, ref):
     L = sm.Lattice(N, Nt)
     p = sm.HMCParams(ref["m0"], ref["beta"], ref["tau"], ref["md_steps"], 1e-10, 10000, 20261015)
     s = sm.HMCSummary()
-    n = ref["Nmeas"]
+    n = 4 * ref["Nmeas"]  # a 4x longer chain than each reference chain
     sp, gs = np.empty(n), np.empty(n)
     sm.check(sm.lib.sm_hmc_run(L.ctx, ctypes.byref(p), 1, 0, ref["Ntherm"], n, ref["Nsteps"], None, ctypes.byref(s),
                                ptr(sp), ptr(gs)))
@@ -62,12 +83,15 @@ def test_hmc_run_matches_reference_statistics(sm, ref):
     assert s.gS == seq_mean(gs) / V
     assert abs(s.gS - ref["beta"] * (1.0 - s.Ep)) <= 1e-12  # S_G = beta sum (1 - Re U_01)
     assert s.acceptance == s.accepted / (n + ref["Nsteps"] * (n - 1))
-    # statistical parity with the reference program
-    sig = math.hypot(s.dEp, ref["dEp"])
-    assert abs(s.Ep - ref["Ep"]) <= 4 * sig + 1e-3, (s.Ep, s.dEp, ref["Ep"], ref["dEp"])
-    sig = math.hypot(s.dgS, ref["dgS"])
-    assert abs(s.gS - ref["gS"]) <= 4 * sig + 2e-3, (s.gS, ref["gS"])
-    assert abs(s.acceptance - ref["acceptance"]) <= 0.15, (s.acceptance, ref["acceptance"])
+    # statistical parity with the reference program: within 4 combined sigmas
+    # of the pooled independent reference chains (their scatter), our jackknife
+    # error inflated by the factor the reference chains show (no fixed slack)
+    slack = 0.0 if "n_chains" in ref else 1.0  # a single recorded chain keeps round 1's +1e-3 / +2e-3
+    sig = math.hypot(s.dEp * ref.get("inflate_Ep", 1.0), ref["dEp"])
+    assert abs(s.Ep - ref["Ep"]) <= 4 * sig + 1e-3 * slack, (s.Ep, s.dEp, ref["Ep"], ref["dEp"], sig)
+    sig = math.hypot(s.dgS * ref.get("inflate_gS", 1.0), ref["dgS"])
+    assert abs(s.gS - ref["gS"]) <= 4 * sig + 2e-3 * slack, (s.gS, ref["gS"], sig)
+    assert abs(s.acceptance - ref["acceptance"]) <= 0.1, (s.acceptance, ref["acceptance"])
 
 
 def test_sm_hmc_program(tmp_path, sm):
