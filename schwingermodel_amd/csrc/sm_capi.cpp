@@ -450,6 +450,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     if (const char *e = getenv("SM_SPLIT_TEST")) c->split_test = atoi(e);
     if (const char *e = getenv("SM_CG_FACE_PIPE")) c->cg_face_pipe = atoi(e);
     if (const char *e = getenv("SM_CG_TAIL")) c->cg_tail = atoi(e);
+    if (const char *e = getenv("SM_CG_RED_SHARDS")) c->cg_red_shards = atoi(e);
     // t-shard apply: faces first, then one launch, on shards narrower than 2048
     // (RCCL loopback, us per apply: 4096x1024 79 vs 91 split; 4096x2048 166 vs
     // 164, 4096^2 296 vs 292; profiles/r02_v8_apply_split.log)
@@ -724,6 +725,7 @@ int sm_cg_begin(sm_ctx *c, const double *phi, double *x, double m0, double tol) 
     c->cg_active = 1;
     c->cg_issued = 0;
     c->cg_flush_pass = -1;
+    c->cg_flush_sums = 0;
     c->cg_pending_x = 0;
     c->cg_faces_for = -1;
     return SM_OK;
@@ -829,6 +831,7 @@ static int cg_ra_pass(sm_ctx *c) {
     const int nparts = cg_fused_blocks(fc);
     c->cg_pending_x = 2;  // sm_cg_finish adds the rows still pending (by the final pass parity)
     c->cg_flush_pass = -1;
+    c->cg_flush_sums = 0;
     const bool one = !c->sharded();
     const bool angles = c->link_angles && c->uang_state == 1;
     const double *ua = angles ? c->Uang : nullptr;
@@ -881,14 +884,18 @@ static int cg_ra_pass(sm_ctx *c) {
         if (3L * (nint * fc.XB + nedge * ec.XB) > 2L * kMaxPartials) ec = fc;
     }
     const int nparts_pass = split ? nint * fc.XB + nedge * ec.XB : nparts;
-    double2 *sums = c->sc->sum3;  // this shard's sums (all-reduced below)
     // ticketed tail: the pass's last block forms the scalars (one shard) or
     // this shard's sums, instead of a separate kernel
     const bool tail = c->cg_tail && fc.fold >= 2 && (nparts_pass + 63) / 64 <= kMaxTickGroups;
+    // t-shard redundant scalars (with the tail): every block of pass j
+    // evaluates pass j-1's scalars from its all-reduced sums (kept by pass
+    // parity), so no scalar kernel sits between the all-reduce and the next pass
+    const bool red = !one && tail && c->cg_red_shards;
+    double2 *sums = red ? &c->sc->sumr[j & 1][0] : c->sc->sum3;  // this shard's sums (all-reduced below)
     auto pass = [&](const CGFusedCfg &cf, int tb0, int tbn, hipStream_t st, int pbase, double2 *fsend) {
         launch_cg_ra(st, c->g, cf, c->kshards(), d1, d2, dn, c->cg_x, c->U, f1, f2, one ? nullptr : face4_recv_U(c),
                      c->cg_mass, j, c->sc, c->partials, tb0, tbn, nullptr, ua, one ? nullptr : c->Uang_face, fsend,
-                     pbase, tail ? c->tick : nullptr, nparts_pass, c->gsum, one ? nullptr : sums);
+                     pbase, tail ? c->tick : nullptr, nparts_pass, c->gsum, one ? nullptr : sums, red ? 1 : 0);
     };
     HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
@@ -918,6 +925,11 @@ static int cg_ra_pass(sm_ctx *c) {
     }
     if (!tail) launch_cg1_local_sum(c->stream, nparts_pass, c->partials, c->sc);
     TRY(allreduce_dev(c, (double *)sums, 6));
+    if (red) {
+        c->cg_flush_pass = j;
+        c->cg_flush_sums = 1;
+        return SM_OK;
+    }
     launch_cg1_from_sums(c->stream, c->sc, first);
     return SM_OK;
 }
@@ -949,8 +961,10 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
     if (c->cg_fused >= 4 && c->cg_flush_pass >= 0) {  // redundant scalars: evaluate the last pass for the host
         const long J = c->cg_flush_pass;
         const int nparts = c->cg_flush_nparts;
-        launch_cg1_flush(c->stream, nparts, c->partials + (J & 1) * 3 * (size_t)nparts, c->sc, J);
+        if (c->cg_flush_sums) launch_cg_ra_flush_sums(c->stream, c->sc, J);
+        else launch_cg1_flush(c->stream, nparts, c->partials + (J & 1) * 3 * (size_t)nparts, c->sc, J);
         c->cg_flush_pass = -1;
+        c->cg_flush_sums = 0;
     }
     HIP_TRY(hipGetLastError());
     return SM_OK;

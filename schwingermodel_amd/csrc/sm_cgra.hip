@@ -185,6 +185,34 @@ __device__ __forceinline__ Sp ra_site(double mass, double sr0, double sl0, const
     return o;
 }
 
+// t-shards (RED = 2): pass j-1's scalars from its all-reduced sums
+// (sumr[(j-1) & 1]) and the state two passes back (red[j & 1]); block 0 keeps
+// the new state. One thread per block calls it; noinline keeps the division
+// chain's registers out of the march's allocation (inlined, the x-updating
+// t-shard kernels reached 256 VGPRs and one wave per SIMD).
+__device__ __attribute__((noinline)) void ra_scalars_from_sums(CGScalars *sc, long j, double2 *ab, int *stop) {
+    CGRed s = sc->red[j & 1];
+    const double2 *sums = sc->sumr[(j - 1) & 1];
+    if (!s.done) s = cg1_eval(s, sc->tol, sc->phi_norm, sc->max_iter, j - 1 == 0, sums[0], sums[1], sums[2]);
+    if (blockIdx.x == 0) sc->red[(j - 1) & 1] = s;
+    ab[0] = s.alpha;
+    ab[1] = s.beta;
+    ab[2] = s.alpha2;
+    ab[3] = s.beta2;
+    *stop = s.done;
+}
+
+__global__ void cg_ra_flush_sums_kernel(CGScalars *sc, long J) {
+    double2 ab[4];
+    int stop;
+    ra_scalars_from_sums(sc, J + 1, ab, &stop);  // S_J into red[J & 1]
+    store_state(sc, sc->red[J & 1]);
+}
+
+void launch_cg_ra_flush_sums(hipStream_t s, CGScalars *sc, long pass) {
+    hipLaunchKernelGGL(cg_ra_flush_sums_kernel, dim3(1), dim3(1), 0, s, sc, pass);
+}
+
 template <int SH, int XP, int FOLD, int RED = 0, int UC = 0, int TK = 0>
 __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
     __shared__ double2 sh[4];
@@ -199,7 +227,9 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
     if (RED) {  // every block evaluates pass j-1's scalars itself (same sums, same order)
         __shared__ double2 s_ab[4];
         __shared__ int s_stop;
-        if (!first) {
+        if (!first && RED == 2) {
+            if (threadIdx.x == 0) ra_scalars_from_sums(sc, a.pass, s_ab, &s_stop);
+        } else if (!first) {
             const CGRed s = cg1_redundant(sc, a.prev, a.TBk * a.XB, a.pass, sh);
             if (threadIdx.x == 0) {
                 s_ab[0] = s.alpha;
@@ -214,10 +244,18 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
         }
         __syncthreads();
         if (s_stop) return;  // block-uniform
-        alpha = first ? z2 : s_ab[0];
-        beta = first ? z2 : s_ab[1];
-        alpha2 = s_ab[2];
-        beta2 = rebuild ? s_ab[3] : z2;
+        // block-uniform values: into scalar registers, as the sc loads of the
+        // non-redundant path are (not 16 VGPRs held across the march)
+        auto uni = [](double2 v) {
+            return make_double2(__hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v.x)),
+                                                 __builtin_amdgcn_readfirstlane(__double2loint(v.x))),
+                                __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v.y)),
+                                                 __builtin_amdgcn_readfirstlane(__double2loint(v.y))));
+        };
+        alpha = first ? z2 : uni(s_ab[0]);
+        beta = first ? z2 : uni(s_ab[1]);
+        alpha2 = uni(s_ab[2]);
+        beta2 = rebuild ? uni(s_ab[3]) : z2;
     } else {
         if (sc->done) return;  // grid-uniform: converged (or max_iter) in an earlier pass
         alpha = first ? z2 : sc->alpha;
@@ -542,7 +580,8 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
                   const double2 *d2, double2 *dn, double2 *x, const double2 *U, const double2 *f1,
                   const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
                   int tb0, int tbn, const double2 *prev_partials, const double *Uang, const double *fUang,
-                  double2 *fsend, int pbase, unsigned *tick, int ntiles, double2 *gsum, double2 *out3) {
+                  double2 *fsend, int pbase, unsigned *tick, int ntiles, double2 *gsum, double2 *out3,
+                  int red_sums) {
     if (tbn <= 0) return;
     RAArgs a;
     a.d1 = d1; a.d2 = d2; a.dn = dn; a.x = x; a.U = U;
@@ -581,6 +620,11 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
         return;
     }
     const bool sh = nshard > 1;
+    if (red_sums && sh && f == 2 && tk) {  // t-shards: scalars from pass j-1's all-reduced sums (sc->sumr)
+        if (uc) ra_go<1, 2, 1, 2>(xp, tk, grid, block, lds, s, a);
+        else ra_go<1, 2, 0, 2>(xp, tk, grid, block, lds, s, a);
+        return;
+    }
     if (f == 2) {
         if (uc) {
             if (sh) ra_go<1, 0, 1, 2>(xp, tk, grid, block, lds, s, a);

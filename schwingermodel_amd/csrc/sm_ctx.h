@@ -98,6 +98,8 @@ struct sm_ctx {
     // recompute-Ad pass: ticketed tail (the pass's last block sums the partials
     // by groups of 64 and forms the scalars / the shard's sums), no scalar kernel
     int cg_tail = 1;
+    int cg_red_shards = 1;          // t-shards: next pass's blocks evaluate the scalars from the all-reduced sums
+    int cg_flush_sums = 0;          // the pending flush evaluates sc->sumr (t-shards), not partials
     unsigned *tick = nullptr;       // 1 + kMaxTickGroups counters, zeroed at creation
     double2 *gsum = nullptr;        // 3 per group
     ncclComm_t comm = nullptr;

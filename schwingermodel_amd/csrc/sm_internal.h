@@ -60,6 +60,7 @@ struct CGScalars {
     int max_iter;        // one-pass path: the device stops itself at k == max_iter
     double2 sum3[3];     // one-pass path, multi-shard: all-reduced <d,Ad>, <r,Ad>, (|r|^2,|Ad|^2)
     CGRed red[2];        // one-pass path, redundant scalars: state S_i in red[i & 1]; red[1] = S_-1
+    double2 sumr[2][3];  // recompute-Ad pass on t-shards, redundant scalars: pass i's all-reduced sums in sumr[i & 1]
 };
 
 enum Epilogue { EPI_NONE = 0, EPI_DOT = 1 };
@@ -138,7 +139,8 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
                   const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
                   int tb0, int tbn, const double2 *prev_partials = nullptr, const double *Uang = nullptr,
                   const double *fUang = nullptr, double2 *fsend = nullptr, int pbase = 0,
-                  unsigned *tick = nullptr, int ntiles = 0, double2 *gsum = nullptr, double2 *out3 = nullptr);
+                  unsigned *tick = nullptr, int ntiles = 0, double2 *gsum = nullptr, double2 *out3 = nullptr,
+                  int red_sums = 0);
 // (tick != null: ticketed tail over the ntiles tiles of every launch of the
 // pass -- the last block forms the scalars in sc, or writes the shard's three
 // sums to out3; tick holds 1 + ceil(ntiles / 64) zeroed counters, gsum 3 per group)
@@ -175,6 +177,8 @@ void launch_cg1_flush(hipStream_t s, int nparts, const double2 *partials, CGScal
 constexpr int kRedundantMaxBlocks = 128;
 void launch_cg1_scalars(hipStream_t s, int nparts, const double2 *partials, CGScalars *sc, int first);
 void launch_cg1_local_sum(hipStream_t s, int nparts, const double2 *partials, CGScalars *sc);
+// t-shard redundant scalars (sm_cgra.hip): S_J of the last issued pass J from its all-reduced sums
+void launch_cg_ra_flush_sums(hipStream_t s, CGScalars *sc, long pass);
 void launch_cg1_from_sums(hipStream_t s, CGScalars *sc, int first);
 void launch_pack_faces2(hipStream_t s, const Geometry &g, const double2 *field, double2 *lo,
                         double2 *hi);
