@@ -450,59 +450,7 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
         }
         return;
     }
-    // Ticketed tail: the last block of each group of 64 tiles sums the group
-    // (one wave, one tile per lane, fixed butterfly order), the last group's
-    // block sums the group sums in order and forms the scalars (or writes the
-    // shard's sums for the all-reduce), so no scalar / local-sum kernel follows.
-    if (threadIdx.x == 0) {
-        publish_partial(p, s0);
-        publish_partial(p + 1, s1);
-        publish_partial(p + 2, s2);
-    }
-    __shared__ int s_last;
-    const int grp = (int)(tile >> 6);
-    const int gsz = min(64, a.ntiles - (grp << 6));
-    if (!last_block_arrive(a.tick + 1 + grp, (unsigned)gsz, &s_last)) return;
-    const double2 zz = make_double2(0.0, 0.0);
-    if (threadIdx.x < 64) {
-        double2 v0 = zz, v1 = zz, v2 = zz;
-        if (lane < gsz) {
-            const double2 *q = a.partials + 3 * (((long)grp << 6) + lane);
-            v0 = load_published(q);
-            v1 = load_published(q + 1);
-            v2 = load_published(q + 2);
-        }
-        v0 = wave_sum(v0);
-        v1 = wave_sum(v1);
-        v2 = wave_sum(v2);
-        if (lane == 0) {
-            publish_partial(a.gsum + 3 * grp, v0);
-            publish_partial(a.gsum + 3 * grp + 1, v1);
-            publish_partial(a.gsum + 3 * grp + 2, v2);
-        }
-    }
-    const int ngrp = (a.ntiles + 63) >> 6;
-    if (!last_block_arrive(a.tick, (unsigned)ngrp, &s_last)) return;
-    if (threadIdx.x < 64) {
-        double2 v0 = zz, v1 = zz, v2 = zz;
-        for (int i = lane; i < ngrp; i += 64) {
-            v0 = cadd(v0, load_published(a.gsum + 3 * i));
-            v1 = cadd(v1, load_published(a.gsum + 3 * i + 1));
-            v2 = cadd(v2, load_published(a.gsum + 3 * i + 2));
-        }
-        v0 = wave_sum(v0);
-        v1 = wave_sum(v1);
-        v2 = wave_sum(v2);
-        if (lane == 0) {
-            if (a.out3) {
-                a.out3[0] = v0;
-                a.out3[1] = v1;
-                a.out3[2] = v2;
-            } else {
-                cg1_update(sc, a.first, v0, v1, v2);
-            }
-        }
-    }
+    cg_ticketed_tail(a.partials, tile, a.ntiles, a.tick, a.gsum, a.out3, sc, a.first, s0, s1, s2);
 }
 
 CGFusedCfg cg_ra_config(const Geometry &g) {

@@ -383,5 +383,67 @@ __device__ __forceinline__ double2 wave_sum(double2 v) {
     return v;
 }
 
+// The ticketed tail of a CG pass (sm_cgra.hip, sm_eotd.hip): this block's
+// partials (s0, s1, s2 in thread 0) go to slot `tile` of ntiles; the last
+// block of each group of 64 tiles sums the group (one wave, one tile per
+// lane, fixed butterfly order), the last group's block sums the group sums in
+// order and forms the scalars in sc (out3 == null) or writes the three sums
+// to out3 (a t-shard's, for the all-reduce). Every thread of the block calls it.
+__device__ __forceinline__ void cg_ticketed_tail(double2 *partials, long tile, int ntiles, unsigned *tick,
+                                                 double2 *gsum, double2 *out3, CGScalars *sc, int first, double2 s0,
+                                                 double2 s1, double2 s2) {
+    double2 *p = partials + 3 * tile;
+    if (threadIdx.x == 0) {
+        publish_partial(p, s0);
+        publish_partial(p + 1, s1);
+        publish_partial(p + 2, s2);
+    }
+    __shared__ int s_last;
+    const int lane = threadIdx.x & 63;
+    const int grp = (int)(tile >> 6);
+    const int gsz = min(64, ntiles - (grp << 6));
+    if (!last_block_arrive(tick + 1 + grp, (unsigned)gsz, &s_last)) return;
+    const double2 zz = make_double2(0.0, 0.0);
+    if (threadIdx.x < 64) {
+        double2 v0 = zz, v1 = zz, v2 = zz;
+        if (lane < gsz) {
+            const double2 *q = partials + 3 * (((long)grp << 6) + lane);
+            v0 = load_published(q);
+            v1 = load_published(q + 1);
+            v2 = load_published(q + 2);
+        }
+        v0 = wave_sum(v0);
+        v1 = wave_sum(v1);
+        v2 = wave_sum(v2);
+        if (lane == 0) {
+            publish_partial(gsum + 3 * grp, v0);
+            publish_partial(gsum + 3 * grp + 1, v1);
+            publish_partial(gsum + 3 * grp + 2, v2);
+        }
+    }
+    const int ngrp = (ntiles + 63) >> 6;
+    if (!last_block_arrive(tick, (unsigned)ngrp, &s_last)) return;
+    if (threadIdx.x < 64) {
+        double2 v0 = zz, v1 = zz, v2 = zz;
+        for (int i = lane; i < ngrp; i += 64) {
+            v0 = cadd(v0, load_published(gsum + 3 * i));
+            v1 = cadd(v1, load_published(gsum + 3 * i + 1));
+            v2 = cadd(v2, load_published(gsum + 3 * i + 2));
+        }
+        v0 = wave_sum(v0);
+        v1 = wave_sum(v1);
+        v2 = wave_sum(v2);
+        if (lane == 0) {
+            if (out3) {
+                out3[0] = v0;
+                out3[1] = v1;
+                out3[2] = v2;
+            } else {
+                cg1_update(sc, first, v0, v1, v2);
+            }
+        }
+    }
+}
+
 }  // namespace sm
 

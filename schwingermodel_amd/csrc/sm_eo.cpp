@@ -252,6 +252,7 @@ static int eo_cg_twodir(sm_ctx *c, const double2 *b, double2 *x, double mass, do
     const EoTdCfg cfg = eo_td_config(c->g);
     const int nparts = eo_td_blocks(cfg);
     if (3 * nparts > 2 * kMaxPartials) return fail(SM_ERR_ARG, "even-odd CG grid too large");
+    const bool tail = c->cg_tail && (nparts + 63) / 64 <= kMaxTickGroups;
     long j = 0;
     auto pass = [&]() -> int {
         const bool first = j == 0;
@@ -271,12 +272,14 @@ static int eo_cg_twodir(sm_ctx *c, const double2 *b, double2 *x, double mass, do
             f.ue = eo_face4(c, EOF4_UE);
             f.uo = eo_face4(c, EOF4_UO);
         }
+        // ticketed tail: the pass's last block forms the scalars (or this
+        // shard's sums) instead of a separate kernel
         launch_eo_td(c->stream, c->g, cfg, d1, d2, aold, dbuf(j), abuf[j & 1], x, ucb(c, 0), ucb(c, 1), mass, j,
-                     c->sc, c->partials, f);
+                     c->sc, c->partials, f, tail ? c->tick : nullptr, c->gsum, c->sharded() ? c->sc->sum3 : nullptr);
         if (!c->sharded()) {
-            launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
+            if (!tail) launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
         } else {
-            launch_cg1_local_sum(c->stream, nparts, c->partials, c->sc);
+            if (!tail) launch_cg1_local_sum(c->stream, nparts, c->partials, c->sc);
             TRY(allreduce_dev(c, (double *)c->sc->sum3, 6));
             launch_cg1_from_sums(c->stream, c->sc, first);
         }

@@ -45,6 +45,8 @@ struct EoTDArgs {
     const double2 *f1, *f2, *fa, *fue, *fuo;  // SH: 4-deep faces of d1, d2, aold, Ue, Uo
     CGScalars *sc;
     double2 *partials;              // 3 per block: (|W|^2, 0), <r,Ad>, (|r|^2, |Ad|^2)
+    unsigned *tick;                 // != null: ticketed tail (sm_device.h cg_ticketed_tail)
+    double2 *gsum, *out3;           // its group sums; out3 != null: the shard's sums instead of the scalars
     long Vh;
     int Nx, Wh, t0, Ntg;
     int xchunk, NWT, TBk, XB, first, rebuild;
@@ -300,6 +302,10 @@ __global__ void __launch_bounds__(256) eo_td_kernel(EoTDArgs a) {
     const double2 s1 = block_sum(aRA, sh);
     __syncthreads();
     const double2 s2 = block_sum(make_double2(aR, aA), sh);
+    if (a.tick) {  // block-uniform
+        cg_ticketed_tail(a.partials, blockIdx.x, (int)gridDim.x, a.tick, a.gsum, a.out3, sc, a.first, s0, s1, s2);
+        return;
+    }
     if (threadIdx.x == 0) {
         double2 *p = a.partials + 3 * (long)blockIdx.x;
         p[0] = s0;
@@ -337,10 +343,12 @@ int eo_td_blocks(const EoTdCfg &c) { return c.TBk * c.XB; }
 
 void launch_eo_td(hipStream_t s, const Geometry &g, const EoTdCfg &c, const double2 *d1, const double2 *d2,
                   const double2 *aold, double2 *dn, double2 *anew, double2 *x, const double2 *Ue, const double2 *Uo,
-                  double mass, long pass, CGScalars *sc, double2 *partials, const EoTdFaces &f) {
+                  double mass, long pass, CGScalars *sc, double2 *partials, const EoTdFaces &f, unsigned *tick,
+                  double2 *gsum, double2 *out3) {
     EoTDArgs a;
     a.d1 = d1; a.d2 = d2; a.aold = aold; a.dn = dn; a.anew = anew; a.x = x;
     a.Ue = Ue; a.Uo = Uo; a.sc = sc; a.partials = partials;
+    a.tick = tick; a.gsum = gsum; a.out3 = out3;
     a.f1 = f.d1; a.f2 = f.d2; a.fa = f.ad; a.fue = f.ue; a.fuo = f.uo;
     a.Vh = g.V / 2; a.Nx = g.Nx; a.Wh = g.Wt / 2; a.t0 = g.t0; a.Ntg = g.Ntg;
     a.xchunk = c.xchunk; a.NWT = c.NWT; a.TBk = c.TBk; a.XB = c.XB;
