@@ -1,0 +1,97 @@
+"""The recompute-Ad CG's scheduling variants agree with each other.
+
+Round 2 moved work out of separate kernels: the ticketed tail (the pass's last
+block sums the partials and forms the scalars), the pipelined t-shard faces
+(the edge launch packs d_j's faces and the exchange for the next pass follows
+it) and the redundant t-shard scalars (every block evaluates the previous
+pass's scalars from the all-reduced sums). Each one changes only where a sum
+or a scalar step runs, or the order of a fixed-order sum, so a solve with it
+and one with the older form (the environment switches read at context
+creation) must reach the same iteration count and x to 1e-12 -- the
+reduction-order band of every other CG parity test
+(src/conjugate_gradient.cpp:28-66 is the recurrence all of them follow).
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ptr
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sm():
+    import schwingermodel_amd
+    return schwingermodel_amd
+
+
+def solve(sm, Nx, Nt, sigma, m0, env, loopback=False, eo=False):
+    S = Nx * Nt
+    U, psi = np.empty(4 * S), np.empty(4 * S)
+    sm.lib.sm_fill_gauge(4321, sigma, Nt, 0, Nx, 0, Nt, ptr(U[:2 * S]), ptr(U[2 * S:]))
+    sm.lib.sm_fill_spinor(5678, Nt, 0, Nx, 0, Nt, ptr(psi[:2 * S]), ptr(psi[2 * S:]))
+    old = {k: os.environ.get(k) for k in env}
+    try:
+        os.environ.update(env)
+        L = sm.Lattice(Nx, Nt, loopback=loopback)  # the switches are read here
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    try:
+        sm.check(sm.lib.sm_upload_gauge(L.ctx, ptr(U[:2 * S]), ptr(U[2 * S:])))
+        x = np.empty(4 * S)
+        res = sm.CGResult()
+        if eo:
+            sm.check(sm.lib.sm_eo_cg(L.ctx, ptr(psi[:2 * S]), ptr(psi[2 * S:]), ptr(x[:2 * S]), ptr(x[2 * S:]),
+                                     m0, 1e-10, 10000, ctypes.byref(res)))
+        else:
+            sm.check(sm.lib.sm_tune_cg(L.ctx, 5, 0))
+            sm.check(sm.lib.sm_cg(L.ctx, ptr(psi[:2 * S]), ptr(psi[2 * S:]), ptr(x[:2 * S]), ptr(x[2 * S:]), m0,
+                                  1e-10, 10000, ctypes.byref(res)))
+    finally:
+        L.close()
+    assert res.converged == 1
+    return res.iterations, x
+
+
+def agree(a, b):
+    (ia, xa), (ib, xb) = a, b
+    assert abs(ia - ib) <= max(1, ia // 100), (ia, ib)
+    rel = np.linalg.norm(xa - xb) / np.linalg.norm(xb)
+    assert rel <= 1e-12, rel
+
+
+# 1024^2 runs above the redundant-scalar threshold (the tail); 96 x 4096 has
+# 74 wave columns, so the tail's groups of 64 tiles straddle block columns
+@pytest.mark.parametrize("shape", [(1024, 1024), (96, 4096)], ids=["1024x1024", "96x4096"])
+def test_ticketed_tail_matches_scalar_kernel(sm, shape):
+    Nx, Nt = shape
+    env = {"SM_CGRA_RED_MAX_BLOCKS": "0"}
+    agree(solve(sm, Nx, Nt, 0.3246, -0.10, env), solve(sm, Nx, Nt, 0.3246, -0.10, dict(env, SM_CG_TAIL="0")))
+
+
+def test_even_odd_tail_matches_scalar_kernel(sm):
+    agree(solve(sm, 256, 256, 0.3246, -0.05, {}, eo=True),
+          solve(sm, 256, 256, 0.3246, -0.05, {"SM_CG_TAIL": "0"}, eo=True))
+
+
+# the t-shard path through the one-rank RCCL loopback: every variant against
+# the older schedule (faces packed and sent at the start of each pass, the
+# scalar kernel after the all-reduce, a separate local-sum kernel)
+@pytest.mark.parametrize("env", [
+    {},
+    {"SM_CG_RED_SHARDS": "0"},
+    {"SM_CG_FACE_PIPE": "0"},
+    {"SM_CG_EDGE_XCHUNK": "0"},
+    {"SM_CG_TAIL": "0"},
+], ids=["default", "no_red", "no_pipe", "long_edge", "no_tail"])
+def test_tshard_schedules_agree(sm, env):
+    old = {"SM_CG_FACE_PIPE": "0", "SM_CG_RED_SHARDS": "0", "SM_CG_TAIL": "0"}
+    agree(solve(sm, 64, 4096, 0.2374, -0.06, env, loopback=True),
+          solve(sm, 64, 4096, 0.2374, -0.06, old, loopback=True))
