@@ -480,9 +480,15 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
     // 0.169; 4096x512 1/48 0.068 vs 0.079; 8192x8192 4/48 1.798 vs 1.820;
     // 8192x1024 1/40 0.253 vs 0.260; 2048x2048 1/40 0.140 vs 0.151. Other
     // shapes of >= 2048 rows take one-wave blocks of 40 rows.
+    // Re-checked after the ticketed tail and the x row parity
+    // (profiles/r02_v9_reshape.log, same box per line): 8192^2 4/32 1.741 vs
+    // 4/48 1.78-1.92; 8192x1024 1/32 0.2635 vs 1/40 0.2650; 2048^2 1/64 0.142
+    // vs 1/40 0.146; the others unchanged. At 4096 columns chunk lengths that
+    // are not powers of two are ~10 % slower (48 / 80 / 96 rows 0.538-0.541
+    // against 0.488 for 32 and 64).
     static const int kShapes[][4] = {  // Nx, Wt, waves per block, rows per block
         {4096, 4096, 1, 64}, {4096, 2048, 1, 32}, {4096, 1024, 1, 40}, {4096, 512, 1, 48},
-        {8192, 8192, 4, 48}, {8192, 1024, 1, 40}, {2048, 2048, 1, 40},
+        {8192, 8192, 4, 32}, {8192, 1024, 1, 32}, {2048, 2048, 1, 64},
     };
     bool known = false;
     for (const auto &k : kShapes)
