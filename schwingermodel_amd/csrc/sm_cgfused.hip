@@ -475,7 +475,7 @@ __global__ void pack_faces2_kernel(int Nx, int Wt, long V, const double2 *f, dou
 
 void launch_pack_faces2(hipStream_t s, const Geometry &g, const double2 *field, double2 *lo,
                         double2 *hi) {
-    hipLaunchKernelGGL(pack_faces2_kernel, dim3((g.Nx + 255) / 256), dim3(256), 0, s, g.Nx, g.Wt, g.V,
+    hipLaunchKernelGGL(pack_faces2_kernel, dim3((g.Nx + 63) / 64), dim3(64), 0, s, g.Nx, g.Wt, g.V,
                        field, lo, hi);
 }
 

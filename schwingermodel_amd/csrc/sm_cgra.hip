@@ -667,7 +667,7 @@ __global__ void pack_faces_k_kernel(int Nx, int Wt, long V, int k, const double2
 }
 
 void launch_pack_faces_k(hipStream_t s, const Geometry &g, int k, const double2 *field, double2 *lo, double2 *hi) {
-    hipLaunchKernelGGL(pack_faces_k_kernel, dim3((g.Nx + 255) / 256), dim3(256), 0, s, g.Nx, g.Wt, g.V, k, field,
+    hipLaunchKernelGGL(pack_faces_k_kernel, dim3((g.Nx + 63) / 64), dim3(64), 0, s, g.Nx, g.Wt, g.V, k, field,
                        lo, hi);
 }
 

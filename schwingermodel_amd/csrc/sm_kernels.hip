@@ -655,7 +655,7 @@ __global__ void pack_faces_kernel(int Nx, int Wt, long V, const double2 *f, doub
 
 void launch_pack_faces(hipStream_t s, const Geometry &g, const double2 *field, double2 *lo_face,
                        double2 *hi_face) {
-    hipLaunchKernelGGL(pack_faces_kernel, dim3((g.Nx + 255) / 256), dim3(256), 0, s, g.Nx, g.Wt, g.V,
+    hipLaunchKernelGGL(pack_faces_kernel, dim3((g.Nx + 63) / 64), dim3(64), 0, s, g.Nx, g.Wt, g.V,
                        field, lo_face, hi_face);
 }
 
@@ -664,6 +664,8 @@ void launch_pack_faces(hipStream_t s, const Geometry &g, const double2 *field, d
 // times my t = Wt-1 column's backward-hop combination (the up-neighbour's
 // t = -1 hop, without its antiperiodic sign). The sums and the product are the
 // reference's own (src/dirac_operator.cpp:31-43, 255-267; force :493-506).
+// Face packs: one thread per row x, strided loads (a row apart), so they are
+// latency-bound; 64-thread blocks spread the Nx threads over 4x as many CUs.
 __global__ void pack_faces_proj_kernel(int Nx, int Wt, long V, const double2 *f, const double2 *U, int kind,
                                        double2 *lo, double2 *hi) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
@@ -692,7 +694,7 @@ __global__ void pack_faces_proj_kernel(int Nx, int Wt, long V, const double2 *f,
 
 void launch_pack_faces_proj(hipStream_t s, const Geometry &g, const double2 *field, const double2 *U, int kind,
                             double2 *lo_face, double2 *hi_face) {
-    hipLaunchKernelGGL(pack_faces_proj_kernel, dim3((g.Nx + 255) / 256), dim3(256), 0, s, g.Nx, g.Wt, g.V, field, U,
+    hipLaunchKernelGGL(pack_faces_proj_kernel, dim3((g.Nx + 63) / 64), dim3(64), 0, s, g.Nx, g.Wt, g.V, field, U,
                        kind, lo_face, hi_face);
 }
 
