@@ -95,3 +95,32 @@ def test_tshard_schedules_agree(sm, env):
     old = {"SM_CG_FACE_PIPE": "0", "SM_CG_RED_SHARDS": "0", "SM_CG_TAIL": "0"}
     agree(solve(sm, 64, 4096, 0.2374, -0.06, env, loopback=True),
           solve(sm, 64, 4096, 0.2374, -0.06, old, loopback=True))
+
+
+@pytest.mark.parametrize("max_iter", [16, 17], ids=["stop_even", "stop_odd"])
+def test_tshard_stop_at_max_iter_matches_one_shard(sm, max_iter):
+    """A solve cut off by max_iter after an even or an odd pass: the t-shard
+    path (redundant scalars flushed from the all-reduced sums, x rows still
+    pending added by the finish kernel) returns the one-shard x and count."""
+    Nx, Nt = 64, 4096
+    S = Nx * Nt
+    U, psi = np.empty(4 * S), np.empty(4 * S)
+    sm.lib.sm_fill_gauge(4321, 0.2374, Nt, 0, Nx, 0, Nt, ptr(U[:2 * S]), ptr(U[2 * S:]))
+    sm.lib.sm_fill_spinor(5678, Nt, 0, Nx, 0, Nt, ptr(psi[:2 * S]), ptr(psi[2 * S:]))
+    out = {}
+    for name, kw in (("one", {}), ("loop", {"loopback": True})):
+        L = sm.Lattice(Nx, Nt, **kw)
+        try:
+            sm.check(sm.lib.sm_upload_gauge(L.ctx, ptr(U[:2 * S]), ptr(U[2 * S:])))
+            sm.check(sm.lib.sm_tune_cg(L.ctx, 5, 0))
+            x = np.empty(4 * S)
+            res = sm.CGResult()
+            sm.lib.sm_cg(L.ctx, ptr(psi[:2 * S]), ptr(psi[2 * S:]), ptr(x[:2 * S]), ptr(x[2 * S:]), -0.06, 1e-10,
+                         max_iter, ctypes.byref(res))
+            out[name] = (res.converged, res.iterations, res.residual, x)
+        finally:
+            L.close()
+    (c1, i1, e1, x1), (c2, i2, e2, x2) = out["one"], out["loop"]
+    assert c1 == c2 == 0 and i1 == i2 == max_iter, (c1, c2, i1, i2)
+    assert abs(e1 - e2) <= 1e-12 * abs(e1), (e1, e2)
+    assert np.linalg.norm(x2 - x1) / np.linalg.norm(x1) <= 1e-13
