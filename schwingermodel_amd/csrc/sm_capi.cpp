@@ -97,6 +97,24 @@ int exchange_faces_on(sm_ctx *c, hipStream_t s, double2 *slo, double2 *shi, doub
     return SM_OK;
 }
 
+int exchange_faces_multi(sm_ctx *c, hipStream_t s, int n, double2 *const *slo, double2 *const *shi,
+                         double2 *const *rlo, double2 *const *rhi, size_t cnt) {
+    if (c->hosted) {
+        for (int i = 0; i < n; ++i) TRY(exchange_faces_on(c, s, slo[i], shi[i], rlo[i], rhi[i], cnt));
+        return SM_OK;
+    }
+    if (cnt > kMaxFaceDoubles * (size_t)c->g.Nx) return fail(SM_ERR_ARG, "face too large (%zu)", cnt);
+    NCCL_TRY(ncclGroupStart());
+    for (int i = 0; i < n; ++i) {
+        NCCL_TRY(ncclSend(shi[i], cnt, ncclDouble, up_rank(c), c->comm, s));
+        NCCL_TRY(ncclRecv(rlo[i], cnt, ncclDouble, down_rank(c), c->comm, s));
+        NCCL_TRY(ncclSend(slo[i], cnt, ncclDouble, down_rank(c), c->comm, s));
+        NCCL_TRY(ncclRecv(rhi[i], cnt, ncclDouble, up_rank(c), c->comm, s));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    return SM_OK;
+}
+
 int exchange_faces(sm_ctx *c, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi, size_t cnt) {
     return exchange_faces_on(c, c->stream, slo, shi, rlo, rhi, cnt);
 }

@@ -183,6 +183,10 @@ TFaces faces_for(sm_ctx *c, const double2 *in, const double2 *recv_lo, const dou
 double2 *face_buf(sm_ctx *c, int set, int which);
 int exchange_faces_on(sm_ctx *c, hipStream_t s, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi,
                       size_t cnt);
+// n independent face exchanges in ONE transport round (RCCL: one group of 4n
+// point-to-point operations; the host-staged transport runs them in turn)
+int exchange_faces_multi(sm_ctx *c, hipStream_t s, int n, double2 *const *slo, double2 *const *shi,
+                         double2 *const *rlo, double2 *const *rhi, size_t cnt);
 int exchange_faces(sm_ctx *c, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi, size_t cnt);
 int allreduce_dev(sm_ctx *c, double *dev, int n);
 int halo(sm_ctx *c, const double2 *field, int set, int kind, TFaces *f);  // kind: FaceKind

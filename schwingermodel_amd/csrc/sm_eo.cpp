@@ -48,7 +48,7 @@ static double2 *eo_face(sm_ctx *c, int slot) { return c->eo_faces + (size_t)slot
 // 4-deep face slots of the one-pass eo CG (16*Nx complex each): 0 send
 // staging, 1 / 2 even / odd links, 3 / 4 d_{j-1} by pass parity (pass j still
 // holds d_{j-2}'s), 5 Ad_{j-1}.
-enum { EOF4_SEND, EOF4_UE, EOF4_UO, EOF4_D0, EOF4_D1, EOF4_AD, EOF4_N };
+enum { EOF4_SEND, EOF4_UE, EOF4_UO, EOF4_D0, EOF4_D1, EOF4_AD, EOF4_SEND2, EOF4_N };
 static double2 *eo_face4(sm_ctx *c, int slot) { return c->eo_faces4 + (size_t)slot * 16 * c->g.Nx; }
 static bool eo_td_sharded_ok(const sm_ctx *c) { return c->sharded() && c->g.Wt >= 8; }
 
@@ -57,6 +57,18 @@ static int eo_halo4(sm_ctx *c, const double2 *f, int slot) {
     const size_t half = (size_t)8 * c->g.Nx;  // complex per side
     launch_pack_cb_faces4(c->stream, c->g, f, snd);
     return exchange_faces_on(c, c->stream, snd, snd + half, rcv, rcv + half, 2 * half);
+}
+
+// The 4-deep faces of two vectors (d_{j-1} and Ad_{j-1}) in one transport round.
+static int eo_halo4_pair(sm_ctx *c, const double2 *f1, int slot1, const double2 *f2, int slot2) {
+    double2 *s1 = eo_face4(c, EOF4_SEND), *s2 = eo_face4(c, EOF4_SEND2);
+    double2 *r1 = eo_face4(c, slot1), *r2 = eo_face4(c, slot2);
+    const size_t half = (size_t)8 * c->g.Nx;  // complex per side
+    launch_pack_cb_faces4(c->stream, c->g, f1, s1);
+    launch_pack_cb_faces4(c->stream, c->g, f2, s2);
+    double2 *slo[2] = {s1, s2}, *shi[2] = {s1 + half, s2 + half};
+    double2 *rlo[2] = {r1, r2}, *rhi[2] = {r1 + half, r2 + half};
+    return exchange_faces_multi(c, c->stream, 2, slo, shi, rlo, rhi, 2 * half);
 }
 
 // Exchange the checkerboard t-faces of f into face slot `slot`; returns the
@@ -264,10 +276,10 @@ static int eo_cg_twodir(sm_ctx *c, const double2 *b, double2 *x, double mass, do
         EoTdFaces f;
         if (c->sharded()) {  // faces of d_{j-1} (d_{j-2}'s are the previous pass's) and Ad_{j-1}
             const int sd = (j & 1) ? EOF4_D1 : EOF4_D0, sp = (j & 1) ? EOF4_D0 : EOF4_D1;
-            TRY(eo_halo4(c, d1, sd));
+            if (first) TRY(eo_halo4(c, d1, sd));
+            else TRY(eo_halo4_pair(c, d1, sd, aold, EOF4_AD));  // one transport round for both
             f.d1 = eo_face4(c, sd);
             f.d2 = j >= 2 ? eo_face4(c, sp) : f.d1;
-            if (!first) TRY(eo_halo4(c, aold, EOF4_AD));
             f.ad = first ? f.d1 : eo_face4(c, EOF4_AD);
             f.ue = eo_face4(c, EOF4_UE);
             f.uo = eo_face4(c, EOF4_UO);
