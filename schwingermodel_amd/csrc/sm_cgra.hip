@@ -185,23 +185,6 @@ __device__ __forceinline__ Sp ra_site(double mass, double sr0, double sl0, const
     return o;
 }
 
-// t-shards (RED = 2): pass j-1's scalars from its all-reduced sums
-// (sumr[(j-1) & 1]) and the state two passes back (red[j & 1]); block 0 keeps
-// the new state. One thread per block calls it; noinline keeps the division
-// chain's registers out of the march's allocation (inlined, the x-updating
-// t-shard kernels reached 256 VGPRs and one wave per SIMD).
-__device__ __attribute__((noinline)) void ra_scalars_from_sums(CGScalars *sc, long j, double2 *ab, int *stop) {
-    CGRed s = sc->red[j & 1];
-    const double2 *sums = sc->sumr[(j - 1) & 1];
-    if (!s.done) s = cg1_eval(s, sc->tol, sc->phi_norm, sc->max_iter, j - 1 == 0, sums[0], sums[1], sums[2]);
-    if (blockIdx.x == 0) sc->red[(j - 1) & 1] = s;
-    ab[0] = s.alpha;
-    ab[1] = s.beta;
-    ab[2] = s.alpha2;
-    ab[3] = s.beta2;
-    *stop = s.done;
-}
-
 __global__ void cg_ra_flush_sums_kernel(CGScalars *sc, long J) {
     double2 ab[4];
     int stop;
@@ -246,16 +229,10 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
         if (s_stop) return;  // block-uniform
         // block-uniform values: into scalar registers, as the sc loads of the
         // non-redundant path are (not 16 VGPRs held across the march)
-        auto uni = [](double2 v) {
-            return make_double2(__hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v.x)),
-                                                 __builtin_amdgcn_readfirstlane(__double2loint(v.x))),
-                                __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v.y)),
-                                                 __builtin_amdgcn_readfirstlane(__double2loint(v.y))));
-        };
-        alpha = first ? z2 : uni(s_ab[0]);
-        beta = first ? z2 : uni(s_ab[1]);
-        alpha2 = uni(s_ab[2]);
-        beta2 = rebuild ? uni(s_ab[3]) : z2;
+        alpha = first ? z2 : uniform_d2(s_ab[0]);
+        beta = first ? z2 : uniform_d2(s_ab[1]);
+        alpha2 = uniform_d2(s_ab[2]);
+        beta2 = rebuild ? uniform_d2(s_ab[3]) : z2;
     } else {
         if (sc->done) return;  // grid-uniform: converged (or max_iter) in an earlier pass
         alpha = first ? z2 : sc->alpha;

@@ -271,6 +271,31 @@ __device__ __forceinline__ CGRed cg1_redundant(CGScalars *sc, const double2 *pre
     return s;
 }
 
+// t-shards (sm_cgra.hip RED = 2, sm_eotd.hip red): pass j-1's scalars from its all-reduced sums
+// (sumr[(j-1) & 1]) and the state two passes back (red[j & 1]); block 0 keeps
+// the new state. One thread per block calls it; noinline keeps the division
+// chain's registers out of the march's allocation (inlined, the x-updating
+// t-shard kernels reached 256 VGPRs and one wave per SIMD).
+static __device__ __attribute__((noinline)) void ra_scalars_from_sums(CGScalars *sc, long j, double2 *ab, int *stop) {
+    CGRed s = sc->red[j & 1];
+    const double2 *sums = sc->sumr[(j - 1) & 1];
+    if (!s.done) s = cg1_eval(s, sc->tol, sc->phi_norm, sc->max_iter, j - 1 == 0, sums[0], sums[1], sums[2]);
+    if (blockIdx.x == 0) sc->red[(j - 1) & 1] = s;
+    ab[0] = s.alpha;
+    ab[1] = s.beta;
+    ab[2] = s.alpha2;
+    ab[3] = s.beta2;
+    *stop = s.done;
+}
+
+// A block-uniform double2 (e.g. read back from LDS) into scalar registers.
+__device__ __forceinline__ double2 uniform_d2(double2 v) {
+    return make_double2(__hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v.x)),
+                                         __builtin_amdgcn_readfirstlane(__double2loint(v.x))),
+                        __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v.y)),
+                                         __builtin_amdgcn_readfirstlane(__double2loint(v.y))));
+}
+
 // Wave-wide lane shifts by one (DPP wave_shr:1 / wave_shl:1, GFX9-family
 // incl. gfx950): no LDS, no barrier. Lane 0 (shr) / lane 63 (shl) receive 0.
 __device__ __forceinline__ double dpp_shr1(double v) {  // lane l <- lane l-1

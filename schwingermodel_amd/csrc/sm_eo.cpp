@@ -265,6 +265,9 @@ static int eo_cg_twodir(sm_ctx *c, const double2 *b, double2 *x, double mass, do
     const int nparts = eo_td_blocks(cfg);
     if (3 * nparts > 2 * kMaxPartials) return fail(SM_ERR_ARG, "even-odd CG grid too large");
     const bool tail = c->cg_tail && (nparts + 63) / 64 <= kMaxTickGroups;
+    // t-shards: every block evaluates the previous pass's scalars from the
+    // all-reduced sums (as the full CG's t-shard passes), flushed per chunk
+    const bool red = c->sharded() && tail && c->cg_red_shards;
     long j = 0;
     auto pass = [&]() -> int {
         const bool first = j == 0;
@@ -286,14 +289,15 @@ static int eo_cg_twodir(sm_ctx *c, const double2 *b, double2 *x, double mass, do
         }
         // ticketed tail: the pass's last block forms the scalars (or this
         // shard's sums) instead of a separate kernel
+        double2 *sums = red ? &c->sc->sumr[j & 1][0] : c->sc->sum3;
         launch_eo_td(c->stream, c->g, cfg, d1, d2, aold, dbuf(j), abuf[j & 1], x, ucb(c, 0), ucb(c, 1), mass, j,
-                     c->sc, c->partials, f, tail ? c->tick : nullptr, c->gsum, c->sharded() ? c->sc->sum3 : nullptr);
+                     c->sc, c->partials, f, tail ? c->tick : nullptr, c->gsum, c->sharded() ? sums : nullptr, red);
         if (!c->sharded()) {
             if (!tail) launch_cg1_scalars(c->stream, nparts, c->partials, c->sc, first);
         } else {
             if (!tail) launch_cg1_local_sum(c->stream, nparts, c->partials, c->sc);
-            TRY(allreduce_dev(c, (double *)c->sc->sum3, 6));
-            launch_cg1_from_sums(c->stream, c->sc, first);
+            TRY(allreduce_dev(c, (double *)sums, 6));
+            if (!red) launch_cg1_from_sums(c->stream, c->sc, first);
         }
         ++j;
         return SM_OK;
@@ -304,6 +308,7 @@ static int eo_cg_twodir(sm_ctx *c, const double2 *b, double2 *x, double mass, do
     while (j < passes) {
         const long nb = (passes - j) < chunk ? (passes - j) : chunk;
         for (long i = 0; i < nb; ++i) TRY(pass());
+        if (red) launch_cg_ra_flush_sums(c->stream, c->sc, j - 1);  // the last pass's scalars for the host
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(c->h_sc, c->sc, sizeof(CGScalars), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));

@@ -47,6 +47,8 @@ struct EoTDArgs {
     double2 *partials;              // 3 per block: (|W|^2, 0), <r,Ad>, (|r|^2, |Ad|^2)
     unsigned *tick;                 // != null: ticketed tail (sm_device.h cg_ticketed_tail)
     double2 *gsum, *out3;           // its group sums; out3 != null: the shard's sums instead of the scalars
+    int red;                        // t-shards: every block evaluates pass j-1's scalars from sc->sumr
+    long pass;
     long Vh;
     int Nx, Wh, t0, Ntg;
     int xchunk, NWT, TBk, XB, first, rebuild;
@@ -91,16 +93,38 @@ __device__ __forceinline__ void eo_bracket(double sr0, double sl0, const Sp &v, 
     }
 }
 
-template <int XP, int SH>
+template <int XP, int SH, int RED = 0>
 __global__ void __launch_bounds__(256) eo_td_kernel(EoTDArgs a) {
     __shared__ double2 sh[4];
     __shared__ double2 rlds[5][2][256];  // r_j of rows y .. y+4
     CGScalars *sc = a.sc;
-    if (sc->done) return;  // grid-uniform
     const double2 z2 = make_double2(0.0, 0.0);
     const bool first = a.first != 0, rebuild = a.rebuild != 0;
-    const double2 alpha = first ? z2 : sc->alpha, beta = first ? z2 : sc->beta;
-    const double2 alpha2 = sc->alpha2, beta2 = rebuild ? sc->beta2 : z2;
+    double2 alpha, beta, alpha2, beta2;
+    if (RED) {  // t-shards: pass j-1's scalars from its all-reduced sums (same step in every block)
+        __shared__ double2 s_ab[4];
+        __shared__ int s_stop;
+        if (threadIdx.x == 0) {
+            if (first) {
+                s_ab[0] = s_ab[1] = s_ab[2] = s_ab[3] = z2;
+                s_stop = 0;
+            } else {
+                ra_scalars_from_sums(sc, a.pass, s_ab, &s_stop);
+            }
+        }
+        __syncthreads();
+        if (s_stop) return;  // block-uniform
+        alpha = first ? z2 : uniform_d2(s_ab[0]);
+        beta = first ? z2 : uniform_d2(s_ab[1]);
+        alpha2 = uniform_d2(s_ab[2]);
+        beta2 = rebuild ? uniform_d2(s_ab[3]) : z2;
+    } else {
+        if (sc->done) return;  // grid-uniform
+        alpha = first ? z2 : sc->alpha;
+        beta = first ? z2 : sc->beta;
+        alpha2 = sc->alpha2;
+        beta2 = rebuild ? sc->beta2 : z2;
+    }
     const int tb = blockIdx.x % a.TBk, xc = blockIdx.x / a.TBk;
     const int lane = threadIdx.x & 63;
     const int gw = tb * 4 + (threadIdx.x >> 6);
@@ -344,8 +368,10 @@ int eo_td_blocks(const EoTdCfg &c) { return c.TBk * c.XB; }
 void launch_eo_td(hipStream_t s, const Geometry &g, const EoTdCfg &c, const double2 *d1, const double2 *d2,
                   const double2 *aold, double2 *dn, double2 *anew, double2 *x, const double2 *Ue, const double2 *Uo,
                   double mass, long pass, CGScalars *sc, double2 *partials, const EoTdFaces &f, unsigned *tick,
-                  double2 *gsum, double2 *out3) {
+                  double2 *gsum, double2 *out3, int red) {
     EoTDArgs a;
+    a.red = red;
+    a.pass = pass;
     a.d1 = d1; a.d2 = d2; a.aold = aold; a.dn = dn; a.anew = anew; a.x = x;
     a.Ue = Ue; a.Uo = Uo; a.sc = sc; a.partials = partials;
     a.tick = tick; a.gsum = gsum; a.out3 = out3;
@@ -357,7 +383,10 @@ void launch_eo_td(hipStream_t s, const Geometry &g, const EoTdCfg &c, const doub
     a.mass = mass;
     const dim3 grid(c.TBk * c.XB), block(256);
     const bool xp = pass >= 2 && (pass & 1) == 0;
-    if (f.d1) {
+    if (f.d1 && red) {
+        if (xp) hipLaunchKernelGGL((eo_td_kernel<1, 1, 1>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((eo_td_kernel<0, 1, 1>), grid, block, 0, s, a);
+    } else if (f.d1) {
         if (xp) hipLaunchKernelGGL((eo_td_kernel<1, 1>), grid, block, 0, s, a);
         else hipLaunchKernelGGL((eo_td_kernel<0, 1>), grid, block, 0, s, a);
     } else {

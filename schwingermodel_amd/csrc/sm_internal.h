@@ -256,7 +256,8 @@ struct EoTdFaces {
 void launch_eo_td(hipStream_t s, const Geometry &g, const EoTdCfg &c, const double2 *d1, const double2 *d2,
                   const double2 *aold, double2 *dn, double2 *anew, double2 *x, const double2 *Ue, const double2 *Uo,
                   double mass, long pass, CGScalars *sc, double2 *partials, const EoTdFaces &f,
-                  unsigned *tick = nullptr, double2 *gsum = nullptr, double2 *out3 = nullptr);  // tick: ticketed tail
+                  unsigned *tick = nullptr, double2 *gsum = nullptr, double2 *out3 = nullptr,  // tick: ticketed tail
+                  int red = 0);  // red: t-shard scalars from sc->sumr (out3 = this pass's sumr slot)
 void launch_pack_cb_faces4(hipStream_t s, const Geometry &g, const double2 *f, double2 *out);
 
 // Pack the t = 0 and t = Wt-1 columns (both planes) into contiguous faces.

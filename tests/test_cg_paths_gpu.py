@@ -124,3 +124,11 @@ def test_tshard_stop_at_max_iter_matches_one_shard(sm, max_iter):
     assert c1 == c2 == 0 and i1 == i2 == max_iter, (c1, c2, i1, i2)
     assert abs(e1 - e2) <= 1e-12 * abs(e1), (e1, e2)
     assert np.linalg.norm(x2 - x1) / np.linalg.norm(x1) <= 1e-13
+
+
+def test_even_odd_tshard_redundant_scalars_agree(sm):
+    """The even-odd CG on t-shards (RCCL loopback) with the redundant scalars
+    (every block evaluates the previous pass's scalars from the all-reduced
+    sums) against the scalar kernel after the all-reduce."""
+    agree(solve(sm, 64, 512, 0.3246, -0.05, {}, loopback=True, eo=True),
+          solve(sm, 64, 512, 0.3246, -0.05, {"SM_CG_RED_SHARDS": "0"}, loopback=True, eo=True))
