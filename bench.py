@@ -81,6 +81,9 @@ def parse(argv=None):
                     help="multi-GPU wire: RCCL (production) or the host-staged test transport")
     ap.add_argument("--device", type=int, default=None, help="override the rank -> GPU mapping")
     ap.add_argument("--cg-path", choices=list(CG_PATH_ID), default="recompute")
+    ap.add_argument("--rank-timeout", type=float, default=900.0,
+                    help="seconds before a rank that has not finished (e.g. stuck in ncclCommInitRank or a "
+                         "mismatched collective) dumps its stacks and exits 124; the spawner then ends the others")
     ap.add_argument("--no-link-angles", action="store_true",
                     help="recompute-Ad CG reads the complex links (160 B/site) instead of their angles "
                          "(144; the default from 4M sites per shard)")
@@ -97,21 +100,37 @@ def _free_port():
     return port
 
 
-def spawn_ranks(n):
+def spawn_ranks(n, argv=None, timeout=900.0, script=None, poll=0.2):
     """`bench.py --gpus N` without a launcher: start N fresh rank processes
-    (nothing in this parent touches the GPU) and exit with the worst code."""
+    (nothing in this parent touches the GPU) and wait for them with a
+    deadline. The first rank to fail, or the deadline, ends the others
+    (SIGTERM, then SIGKILL): a hung rank fails the job loudly instead of
+    holding the node. Returns the worst exit code (124 on the deadline)."""
     port = str(_free_port())
+    argv = sys.argv[1:] if argv is None else argv
+    script = script or os.path.abspath(__file__)
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
     rc = 0
+    deadline = time.monotonic() + timeout
     try:
-        for p in procs:
-            rc = max(rc, p.wait())
-            if rc:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = max(abs(c) for c in bad) or 1
+                print(f"[bench] a rank exited with {bad[0]}: ending the others", file=sys.stderr)
                 break
+            if all(c == 0 for c in codes):
+                break
+            if time.monotonic() > deadline:
+                rc = 124
+                print(f"[bench] ranks still running after {timeout:.0f} s: ending them", file=sys.stderr)
+                break
+            time.sleep(poll)
     finally:
         for p in procs:
             if p.poll() is None:
@@ -121,7 +140,29 @@ def spawn_ranks(n):
                 p.wait(timeout=30)
             except subprocess.TimeoutExpired:
                 p.kill()
+                p.wait()
     return rc
+
+
+def start_rank_watchdog(seconds):
+    """In-process deadline for a rank (also under torch.distributed.run): dump
+    every thread's stack to stderr and exit 124, so a rank stuck in a
+    collective fails the job instead of hanging it (the launcher then ends
+    the other ranks)."""
+    import faulthandler
+    import threading
+
+    def fire():
+        print(f"[bench] rank {os.environ.get('RANK', '0')}: no result after {seconds:.0f} s, exiting 124",
+              file=sys.stderr, flush=True)
+        faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+        sys.stderr.flush()
+        os._exit(124)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
 
 
 # --------------------------------------------------------------------------- CPU baseline
@@ -499,11 +540,12 @@ def main():
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
     if env_world is None and args.gpus > 1:
-        sys.exit(spawn_ranks(args.gpus))
+        sys.exit(spawn_ranks(args.gpus, timeout=args.rank_timeout + 60))
     world = int(env_world or "1")
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: refusing to measure the wrong job")
     rank = int(os.environ.get("RANK", "0"))
+    watchdog = start_rank_watchdog(args.rank_timeout)
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     cfg_id = args.config or (3 if world == 1 else 4)
     if cfg_id == 3 and world > 1:
@@ -536,6 +578,7 @@ def main():
     finally:
         if world > 1:
             dist.destroy_process_group()
+        watchdog.cancel()
 
 
 if __name__ == "__main__":

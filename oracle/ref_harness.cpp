@@ -71,6 +71,12 @@ static void setup(int rx, int rt) {
     initializeMPI();
     allocate_lattice_arrays();
     periodic_boundary();
+    // The reference's scratch globals are default-sized to the full lattice
+    // on every rank (src/variables.cpp:68-69, include/variables.h:59). The
+    // operators only touch maxSize elements of them, so shrink them to the
+    // rank's block: 8192^2 on 8 ranks otherwise holds 32 GiB of scratch.
+    DTEMP = spinor(mpi::maxSize);
+    TEMP = spinor(mpi::maxSize);
 }
 
 static int x_begin() { return mpi::coords[0] * mpi::width_x; }

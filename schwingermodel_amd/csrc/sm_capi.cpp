@@ -73,6 +73,8 @@ int down_rank(const sm_ctx *c) { return (c->shard - 1 + c->nshard) % c->nshard; 
 // column goes down (the down-neighbour's t = Wt). The face buffers are
 // [plane][x], 4*Nx doubles.
 
+ncclComm_t comm_for(const sm_ctx *c, hipStream_t s) { return s == c->comm_stream ? c->comm_side : c->comm; }
+
 int exchange_faces_on(sm_ctx *c, hipStream_t s, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi,
                       size_t cnt) {
     if (cnt > kMaxFaceDoubles * (size_t)c->g.Nx) return fail(SM_ERR_ARG, "face too large (%zu)", cnt);
@@ -88,11 +90,12 @@ int exchange_faces_on(sm_ctx *c, hipStream_t s, double2 *slo, double2 *shi, doub
         HIP_TRY(hipStreamSynchronize(s));  // staging buffers are reused
         return SM_OK;
     }
+    ncclComm_t cm = comm_for(c, s);
     NCCL_TRY(ncclGroupStart());
-    NCCL_TRY(ncclSend(shi, cnt, ncclDouble, up_rank(c), c->comm, s));
-    NCCL_TRY(ncclRecv(rlo, cnt, ncclDouble, down_rank(c), c->comm, s));
-    NCCL_TRY(ncclSend(slo, cnt, ncclDouble, down_rank(c), c->comm, s));
-    NCCL_TRY(ncclRecv(rhi, cnt, ncclDouble, up_rank(c), c->comm, s));
+    NCCL_TRY(ncclSend(shi, cnt, ncclDouble, up_rank(c), cm, s));
+    NCCL_TRY(ncclRecv(rlo, cnt, ncclDouble, down_rank(c), cm, s));
+    NCCL_TRY(ncclSend(slo, cnt, ncclDouble, down_rank(c), cm, s));
+    NCCL_TRY(ncclRecv(rhi, cnt, ncclDouble, up_rank(c), cm, s));
     NCCL_TRY(ncclGroupEnd());
     return SM_OK;
 }
@@ -104,12 +107,13 @@ int exchange_faces_multi(sm_ctx *c, hipStream_t s, int n, double2 *const *slo, d
         return SM_OK;
     }
     if (cnt > kMaxFaceDoubles * (size_t)c->g.Nx) return fail(SM_ERR_ARG, "face too large (%zu)", cnt);
+    ncclComm_t cm = comm_for(c, s);
     NCCL_TRY(ncclGroupStart());
     for (int i = 0; i < n; ++i) {
-        NCCL_TRY(ncclSend(shi[i], cnt, ncclDouble, up_rank(c), c->comm, s));
-        NCCL_TRY(ncclRecv(rlo[i], cnt, ncclDouble, down_rank(c), c->comm, s));
-        NCCL_TRY(ncclSend(slo[i], cnt, ncclDouble, down_rank(c), c->comm, s));
-        NCCL_TRY(ncclRecv(rhi[i], cnt, ncclDouble, up_rank(c), c->comm, s));
+        NCCL_TRY(ncclSend(shi[i], cnt, ncclDouble, up_rank(c), cm, s));
+        NCCL_TRY(ncclRecv(rlo[i], cnt, ncclDouble, down_rank(c), cm, s));
+        NCCL_TRY(ncclSend(slo[i], cnt, ncclDouble, down_rank(c), cm, s));
+        NCCL_TRY(ncclRecv(rhi[i], cnt, ncclDouble, up_rank(c), cm, s));
     }
     NCCL_TRY(ncclGroupEnd());
     return SM_OK;
@@ -131,7 +135,7 @@ int allreduce_dev(sm_ctx *c, double *dev, int n) {
         HIP_TRY(hipStreamSynchronize(c->stream));
         return SM_OK;
     }
-    NCCL_TRY(ncclAllReduce(dev, dev, n, ncclDouble, ncclSum, c->comm, c->stream));
+    NCCL_TRY(ncclAllReduce(dev, dev, n, ncclDouble, ncclSum, comm_for(c, c->stream), c->stream));
     return SM_OK;
 }
 
@@ -156,35 +160,28 @@ int apply(sm_ctx *c, const double2 *in, double2 *out, double mass, int dagger, c
           double2 *partials, const CGScalars *skip) {
     TFaces f;
     const int TB = (c->g.Wt + c->cfg.bt - 1) / c->cfg.bt;
-    const bool one = !c->sharded();
-    if (TB < 3 || (one && !c->split_test) || (!one && !c->apply_split)) {
+    if (!c->sharded() || TB < 3 || !c->apply_split) {
+        // one shard, or a narrow t-shard: faces first, then one launch
         TRY(halo(c, in, 0, dagger ? FACE_DDAG : FACE_D, &f));
         launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip);
     } else {
         // t-blocks 1..TB-2 never touch t = 0 / Wt-1: they run on the main
         // stream while the faces travel on the comm stream; the two edge
-        // block-columns follow the faces there, concurrently with the interior
-        const bool conc = one ? c->split_test == 2 : c->edge_concurrent != 0;
+        // block-columns (TB-1, then 0 by wrap-around, one launch) follow the
+        // faces there, concurrently with the interior launch
         double2 *slo = face_buf(c, 0, 0), *shi = face_buf(c, 0, 1);
         double2 *rlo = face_buf(c, 0, 2), *rhi = face_buf(c, 0, 3);
         HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
         HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
-        if (!one) {
-            launch_pack_faces_proj(c->comm_stream, c->g, in, c->U, dagger ? FACE_DDAG : FACE_D, slo, shi);
-            TRY(exchange_faces_on(c, c->comm_stream, slo, shi, rlo, rhi, (size_t)2 * c->g.Nx));
-        }
-        f = one ? faces_for(c, in, nullptr, nullptr) : faces_for(c, in, rlo, rhi);
-        // both edge block-columns (TB-1, then 0 by wrap-around) in one launch
-        if (conc)
-            launch_dslash(c->comm_stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip,
-                          TB - 1, 2);
+        launch_pack_faces_proj(c->comm_stream, c->g, in, c->U, dagger ? FACE_DDAG : FACE_D, slo, shi);
+        TRY(exchange_faces_on(c, c->comm_stream, slo, shi, rlo, rhi, (size_t)2 * c->g.Nx));
+        f = faces_for(c, in, rlo, rhi);
+        launch_dslash(c->comm_stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip,
+                      TB - 1, 2);
         HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
         launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip,
                       1, TB - 2);
         HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
-        if (!conc)
-            launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip,
-                          TB - 1, 2);
     }
     HIP_TRY(hipGetLastError());
     return SM_OK;
@@ -240,12 +237,13 @@ int halo2_multi(sm_ctx *c, hipStream_t s, const double2 *const *fields, double2 
                                   faces[f] + (size_t)4 * c->g.Nx, cnt));
         return SM_OK;
     }
+    ncclComm_t cm = comm_for(c, s);
     NCCL_TRY(ncclGroupStart());
     for (int f = 0; f < nf; ++f) {
-        NCCL_TRY(ncclSend(face2_send(c, f, 1), cnt, ncclDouble, up_rank(c), c->comm, s));
-        NCCL_TRY(ncclRecv(faces[f], cnt, ncclDouble, down_rank(c), c->comm, s));
-        NCCL_TRY(ncclSend(face2_send(c, f, 0), cnt, ncclDouble, down_rank(c), c->comm, s));
-        NCCL_TRY(ncclRecv(faces[f] + (size_t)4 * c->g.Nx, cnt, ncclDouble, up_rank(c), c->comm, s));
+        NCCL_TRY(ncclSend(face2_send(c, f, 1), cnt, ncclDouble, up_rank(c), cm, s));
+        NCCL_TRY(ncclRecv(faces[f], cnt, ncclDouble, down_rank(c), cm, s));
+        NCCL_TRY(ncclSend(face2_send(c, f, 0), cnt, ncclDouble, down_rank(c), cm, s));
+        NCCL_TRY(ncclRecv(faces[f] + (size_t)4 * c->g.Nx, cnt, ncclDouble, up_rank(c), cm, s));
     }
     NCCL_TRY(ncclGroupEnd());
     return SM_OK;
@@ -290,19 +288,29 @@ int exchange_ghost_U(sm_ctx *c) {
 
 
 // Link angles for the recompute-Ad pass (cg_ra_kernel UC), rebuilt at the
-// first solve after U changed. Collective on t-shards (a global count of links
-// off the unit circle decides for every shard alike).
+// first solve after U changed. On t-shards the decision is collective: the
+// path conditions below are rank-uniform (shape rules, the same test options
+// everywhere), but the link_angles wish is per context (sm_cg_link_angles),
+// so every shard whose angles are stale takes part in ONE all-reduce of
+// (links off the unit circle, shards not asking for angles) and the angles
+// are used only when both sums are 0.
 int ensure_link_angles(sm_ctx *c) {
-    if (!c->link_angles || c->cg_fused != 5 || c->racfg.fold < 2 || !cg_ra_ok(c) || c->uang_state != 0)
-        return SM_OK;
-    if (!c->Uang) HIP_TRY(hipMalloc(&c->Uang, sizeof(double) * 2 * (size_t)c->g.V));
-    if (c->sharded() && !c->Uang_face) HIP_TRY(hipMalloc(&c->Uang_face, sizeof(double) * 16 * (size_t)c->g.Nx));
-    const long n = 2 * c->g.V;
-    const int nb = launch_link_angles(c->stream, n, c->U, c->Uang, c->partials);
-    TRY(global_sum(c, nb, c->partials, 0));
+    if (c->cg_fused != 5 || c->racfg.fold < 2 || !cg_ra_ok(c) || c->uang_state != 0) return SM_OK;
+    if (!c->link_angles && !c->sharded()) return SM_OK;
+    if (c->link_angles) {
+        if (!c->Uang) HIP_TRY(hipMalloc(&c->Uang, sizeof(double) * 2 * (size_t)c->g.V));
+        if (c->sharded() && !c->Uang_face)
+            HIP_TRY(hipMalloc(&c->Uang_face, sizeof(double) * 16 * (size_t)c->g.Nx));
+        const int nb = launch_link_angles(c->stream, 2 * c->g.V, c->U, c->Uang, c->partials);
+        launch_sum_partials(c->stream, nb, c->partials, c->sums);  // (links off the circle, 0)
+    } else {
+        c->h_sums[1] = make_double2(0.0, 1.0);                      // (0, this shard declines)
+        HIP_TRY(hipMemcpyAsync(c->sums, c->h_sums + 1, sizeof(double2), hipMemcpyHostToDevice, c->stream));
+    }
+    TRY(allreduce_dev(c, (double *)c->sums, 2));
     HIP_TRY(hipMemcpyAsync(c->h_sums, c->sums, sizeof(double2), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    c->uang_state = c->h_sums[0].x == 0.0 ? 1 : 2;
+    c->uang_state = c->h_sums[0].x == 0.0 && c->h_sums[0].y == 0.0 ? 1 : 2;
     if (c->uang_state == 1 && c->sharded()) launch_angles_of(c->stream, 16 * (long)c->g.Nx, face4_recv_U(c), c->Uang_face);
     HIP_TRY(hipGetLastError());
     return SM_OK;
@@ -412,6 +420,76 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
     return SM_OK;
 }
 
+// Test-only switches. Every production choice above is a per-shape rule or
+// table; the tests force the alternatives through ONE environment variable,
+// read when a context is created: SM_TEST_OPTS="key=value,key=value". The
+// keys and the choice each forces:
+//   cg=0|4|5            CG path (six launches / stored Ad / recompute Ad)
+//   tail=0              scalar kernel instead of the ticketed tail
+//   red_shards=0        t-shards: scalar kernel after the all-reduce
+//   face_pipe=0         t-shards: no pipelined d_j faces
+//   edge_xchunk=N       t-shards: rows per edge block (0: the interior's)
+//   ra_red_max_blocks=N one shard: redundant scalars up to N blocks
+//   fold=0|1|2          recompute-Ad pass arithmetic (2: fused multiply-adds)
+//   link_angles=0|1     recompute-Ad pass reads the links as angles
+//   bt=64|128|256       Dirac apply t-columns per block
+//   eo_fused=0, eo_cg_td=0, eo_cg_folded=1   even-odd operator / CG forms
+//   debug_cg=1          CG host loops print their status (stderr)
+// An unknown key or a malformed value fails the creation.
+static int apply_test_opts(sm_ctx *c) {
+    const char *env = getenv("SM_TEST_OPTS");
+    if (!env || !*env) return SM_OK;
+    std::string all(env);
+    size_t pos = 0;
+    while (pos < all.size()) {
+        size_t end = all.find(',', pos);
+        if (end == std::string::npos) end = all.size();
+        const std::string kv = all.substr(pos, end - pos);
+        pos = end + 1;
+        if (kv.empty()) continue;
+        const size_t eq = kv.find('=');
+        char *tail = nullptr;
+        const long v = eq == std::string::npos ? 0 : strtol(kv.c_str() + eq + 1, &tail, 10);
+        if (eq == std::string::npos || !tail || *tail || tail == kv.c_str() + eq + 1)
+            return fail(SM_ERR_ARG, "SM_TEST_OPTS: malformed '%s'", kv.c_str());
+        const std::string k = kv.substr(0, eq);
+        const int iv = (int)v;
+        if (k == "cg") {
+            if (iv != 0 && iv != 4 && iv != 5) return fail(SM_ERR_ARG, "SM_TEST_OPTS: cg must be 0, 4 or 5");
+            c->cg_fused = iv;
+        } else if (k == "tail") {
+            c->cg_tail = iv;
+        } else if (k == "red_shards") {
+            c->cg_red_shards = iv;
+        } else if (k == "face_pipe") {
+            c->cg_face_pipe = iv;
+        } else if (k == "edge_xchunk") {
+            c->cg_edge_xchunk = iv;
+        } else if (k == "ra_red_max_blocks") {
+            c->cg_ra_red_max_blocks = iv;
+        } else if (k == "fold") {
+            c->racfg.fold = iv;
+        } else if (k == "link_angles") {
+            c->link_angles = iv ? 1 : 0;
+        } else if (k == "bt") {
+            if (iv != 64 && iv != 128 && iv != 256) return fail(SM_ERR_ARG, "SM_TEST_OPTS: bt must be 64, 128 or 256");
+            c->cfg.bt = iv;
+            c->nparts_dslash = dslash_blocks(c->g, c->cfg);
+        } else if (k == "eo_fused") {
+            c->eo_fused = iv;
+        } else if (k == "eo_cg_td") {
+            c->eo_cg_td = iv;
+        } else if (k == "eo_cg_folded") {
+            c->eo_cg_folded = iv;
+        } else if (k == "debug_cg") {
+            c->debug_cg = iv;
+        } else {
+            return fail(SM_ERR_ARG, "SM_TEST_OPTS: unknown key '%s'", k.c_str());
+        }
+    }
+    return SM_OK;
+}
+
 static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device,
                          const void *unique_id, const sm_host_transport *tr, bool loop = false) {
     if (!out) return fail(SM_ERR_ARG, "null out");
@@ -450,6 +528,23 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
         }
         return 3L * cg_fused_blocks(f) <= 2L * kMaxPartials;
     };
+    // Per-shape choices (measured):
+    // * CG path: the recompute-Ad pass from 256^2 sites per shard, the
+    //   stored-Ad pass below (latency-bound grids; tools/small_cg.py).
+    c->cg_fused = c->g.V >= (1L << 16) ? 5 : 4;
+    // * t-shard apply: faces first, then one launch, on shards narrower than
+    //   2048 (RCCL loopback, us per apply: 4096x1024 79 vs 91 split; 4096x2048
+    //   166 vs 164, 4096^2 296 vs 292; profiles/r02_v8_apply_split.log).
+    c->apply_split = c->g.Wt >= 2048 ? 1 : 0;
+    // * link angles from 4M sites per shard: below, the fields of a pass sit
+    //   largely in the 256 MB MALL and the pass is bound by its VALU work,
+    //   where the sincos costs more than the 16 B it saves (tools/tune_shapes.py:
+    //   4096x512 0.080 vs 0.068 ms per iteration, 4096x1024 0.141 vs 0.147).
+    c->link_angles = c->g.V >= (1L << 22) ? 1 : 0;
+    if (int rc = apply_test_opts(c); rc != SM_OK) {
+        delete c;
+        return rc;
+    }
     while (c->nparts_dslash > kMaxPartials && c->cfg.xchunk < Nx) {
         c->cfg.xchunk = std::min(Nx, 2 * c->cfg.xchunk);
         c->nparts_dslash = dslash_blocks(c->g, c->cfg);
@@ -458,48 +553,30 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
         delete c;
         return fail(SM_ERR_ARG, "shard %dx%d too wide for the partial-sum buffer", Nx, Wt);
     }
-    // recompute-Ad pass from 1024^2 sites per shard up (tools/tune_cg.py, ms per
-    // iteration against the stored-Ad pass: 1024^2 0.054 vs 0.060, 2048^2 0.174
-    // vs 0.223, 4096^2 0.588 vs 0.778); below that the stored-Ad pass is faster
-    // (512^2 0.028 vs 0.030, 256^2 0.016 vs 0.019)
-    c->cg_fused = c->g.V >= (1L << 16) ? 5 : 4;  // recompute-Ad from 256^2 sites per shard (tools/small_cg.py)
-    if (const char *e = getenv("SM_CG_FUSED")) c->cg_fused = atoi(e);
-    if (const char *e = getenv("SM_EDGE_CONCURRENT")) c->edge_concurrent = atoi(e);
-    if (const char *e = getenv("SM_SPLIT_TEST")) c->split_test = atoi(e);
-    if (const char *e = getenv("SM_CG_FACE_PIPE")) c->cg_face_pipe = atoi(e);
-    if (const char *e = getenv("SM_CG_TAIL")) c->cg_tail = atoi(e);
-    if (const char *e = getenv("SM_CG_RED_SHARDS")) c->cg_red_shards = atoi(e);
-    // t-shard apply: faces first, then one launch, on shards narrower than 2048
-    // (RCCL loopback, us per apply: 4096x1024 79 vs 91 split; 4096x2048 166 vs
-    // 164, 4096^2 296 vs 292; profiles/r02_v8_apply_split.log)
-    c->apply_split = c->g.Wt >= 2048 ? 1 : 0;
-    if (const char *e = getenv("SM_APPLY_SPLIT")) c->apply_split = atoi(e);
-    if (const char *e = getenv("SM_CG_EDGE_XCHUNK")) c->cg_edge_xchunk = atoi(e);
-    if (const char *e = getenv("SM_CGRA_RED_MAX_BLOCKS")) c->cg_ra_red_max_blocks = atoi(e);
-    if (const char *e = getenv("SM_CG_REDUNDANT")) c->cg_redundant = atoi(e);
-    if (const char *e = getenv("SM_EO_FUSED")) c->eo_fused = atoi(e);
-    if (const char *e = getenv("SM_EO_CG_FOLDED")) c->eo_cg_folded = atoi(e);
-    if (const char *e = getenv("SM_EO_CG_TD")) c->eo_cg_td = atoi(e);
-    if (const char *e = getenv("SM_DEBUG_CG")) c->debug_cg = atoi(e);
-    // link angles from 4M sites per shard: below, the fields of a pass sit
-    // largely in the 256 MB MALL and the pass is bound by its VALU work, where
-    // the sincos costs more than the 16 B it saves (tools/tune_shapes.py:
-    // 4096x512 0.080 vs 0.068 ms per iteration, 4096x1024 0.141 vs 0.147)
-    c->link_angles = c->g.V >= (1L << 22) ? 1 : 0;
-    if (const char *e = getenv("SM_CG_LINK_ANGLES")) c->link_angles = atoi(e);
     const int np = kMaxPartials;
     const size_t fb = sizeof(double2) * 2 * (size_t)c->g.V;
     hipError_t e = hipSuccess;
     auto chk = [&](hipError_t x) { if (e == hipSuccess) e = x; };
     chk(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
     c->stream = c->own_stream;
+    c->hosted = nshard > 1 && tr;
+    // The host-staged transport synchronises the stream inside every exchange
+    // and all-reduce, so a second stream buys it no overlap: its contexts run
+    // on ONE stream (one hardware queue per process, the fewest when several
+    // shards share a GPU). RCCL contexts overlap faces and edge blocks with
+    // the interior on a separate comm stream.
+    if (c->hosted) {
+        c->comm_stream = c->own_stream;
+    } else {
+        chk(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+        c->own_comm_stream = true;
+    }
     chk(hipMalloc(&c->U, fb));
     chk(hipMalloc(&c->ghostU, sizeof(double2) * (size_t)Nx));
     chk(hipMalloc(&c->fields, fb * NFIELDS));
     chk(hipMalloc(&c->faces, sizeof(double2) * 2 * (size_t)Nx * 8));
     chk(hipMalloc(&c->faces2, sizeof(double2) * 56 * (size_t)Nx));
     chk(hipMalloc(&c->faces4, sizeof(double2) * 64 * (size_t)Nx));
-    chk(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
     chk(hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming));
     chk(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
     chk(hipMalloc(&c->partials, sizeof(double2) * 2 * (size_t)np));
@@ -512,18 +589,20 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     chk(hipHostMalloc(&c->h_sums, sizeof(double2) * 4));
     chk(hipHostMalloc(&c->h_face, sizeof(double) * 4 * kMaxFaceDoubles * (size_t)Nx));
     chk(hipHostMalloc(&c->h_red, sizeof(double) * 8));
-    if (e == hipSuccess) chk(hipMemset(c->sc, 0, sizeof(CGScalars)));
-    if (e == hipSuccess) chk(hipMemset(c->tick, 0, sizeof(unsigned) * (1 + kMaxTickGroups)));
-    // face slots start as zeros, not whatever the allocator hands back
-    if (e == hipSuccess) chk(hipMemset(c->faces, 0, sizeof(double2) * 2 * (size_t)Nx * 8));
-    if (e == hipSuccess) chk(hipMemset(c->faces2, 0, sizeof(double2) * 56 * (size_t)Nx));
-    if (e == hipSuccess) chk(hipMemset(c->faces4, 0, sizeof(double2) * 64 * (size_t)Nx));
+    // on the context's stream, not the null stream (which would be one more
+    // hardware queue per process); face slots start as zeros, not whatever
+    // the allocator hands back
+    if (e == hipSuccess) chk(hipMemsetAsync(c->sc, 0, sizeof(CGScalars), c->own_stream));
+    if (e == hipSuccess) chk(hipMemsetAsync(c->tick, 0, sizeof(unsigned) * (1 + kMaxTickGroups), c->own_stream));
+    if (e == hipSuccess) chk(hipMemsetAsync(c->faces, 0, sizeof(double2) * 2 * (size_t)Nx * 8, c->own_stream));
+    if (e == hipSuccess) chk(hipMemsetAsync(c->faces2, 0, sizeof(double2) * 56 * (size_t)Nx, c->own_stream));
+    if (e == hipSuccess) chk(hipMemsetAsync(c->faces4, 0, sizeof(double2) * 64 * (size_t)Nx, c->own_stream));
+    if (e == hipSuccess) chk(hipStreamSynchronize(c->own_stream));
     if (e != hipSuccess) {
         sm_destroy(c);
         return fail(SM_ERR_HIP, "allocation failed: %s", hipGetErrorString(e));
     }
-    if (nshard > 1 && tr) {
-        c->hosted = true;
+    if (c->hosted) {
         c->tr = *tr;
     } else if (c->sharded()) {
         ncclUniqueId id;
@@ -533,6 +612,16 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
             c->comm = nullptr;
             sm_destroy(c);
             return fail(SM_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+        }
+        // the second communicator of the comm stream (comm_for): each
+        // communicator is driven from ONE stream, so its operations run in
+        // issue order without a cross-stream hand-off, and the main stream's
+        // all-reduce never queues behind the comm stream's face exchange
+        r = ncclCommSplit(c->comm, 0, shard, &c->comm_side, nullptr);
+        if (r != ncclSuccess) {
+            c->comm_side = nullptr;
+            sm_destroy(c);
+            return fail(SM_ERR_RCCL, "ncclCommSplit: %s", ncclGetErrorString(r));
         }
     }
     *out = c;
@@ -560,6 +649,7 @@ int sm_destroy(sm_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);  // e.g. a CG's trailing face exchange
+    if (c->comm_side) ncclCommDestroy(c->comm_side);
     if (c->comm) ncclCommDestroy(c->comm);
     void *dev[] = {c->U, c->ghostU, c->fields, c->faces, c->faces2, c->faces4, c->partials, c->sums, c->Fbuf, c->sc,
                    c->U_alt, c->Pmd, c->Fmd, c->eo, c->Ucb, c->eo_faces, c->eo_faces4, c->Uang, c->Uang_face,
@@ -573,7 +663,7 @@ int sm_destroy(sm_ctx *c) {
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
     if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
     if (c->ev_halo) (void)hipEventDestroy(c->ev_halo);
-    if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
+    if (c->comm_stream && c->own_comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
     return SM_OK;
@@ -613,7 +703,10 @@ int sm_tune_cg_geometry(sm_ctx *c, int waves_per_block, int xchunk) {
 
 int sm_cg_link_angles(sm_ctx *c, int on, int *in_use) {
     if (!c) return fail(SM_ERR_ARG, "null context");
-    if (on >= 0) c->link_angles = on ? 1 : 0;
+    if (on >= 0 && (on ? 1 : 0) != c->link_angles) {
+        c->link_angles = on ? 1 : 0;
+        c->uang_state = 0;  // decided again (collectively on t-shards) at the next solve
+    }
     if (in_use) *in_use = c->link_angles && c->cg_fused == 5 && c->uang_state == 1 ? 1 : 0;
     return SM_OK;
 }
@@ -643,7 +736,12 @@ int sm_bench_stream(sm_ctx *c, int two_reads, long n, const double *a, const dou
 
 int sm_set_stream(sm_ctx *c, void *s) {
     if (!c) return fail(SM_ERR_ARG, "null context");
+    // the old stream's work (and its communicator's operations) completes
+    // before any is issued on the new one: comm_for keys the main
+    // communicator to whichever stream is current
+    HIP_TRY(hipStreamSynchronize(c->stream));
     c->stream = s ? (hipStream_t)s : c->own_stream;
+    if (c->hosted) c->comm_stream = c->stream;  // hosted contexts run on one stream
     return SM_OK;
 }
 
@@ -773,7 +871,7 @@ static int cg_onepass(sm_ctx *c) {
     const int nparts = cg_fused_blocks(fc);
     // redundant scalars on small one-shard grids: partials by pass parity,
     // evaluated by every block of the next pass; sm_cg_iterate flushes the last
-    const bool redundant = !c->sharded() && c->cg_redundant && nparts <= c->cg_red_max_blocks;
+    const bool redundant = !c->sharded() && nparts <= c->cg_red_max_blocks;
     double2 *part = redundant ? c->partials + (j & 1) * 3 * (size_t)nparts : c->partials;
     const double2 *prev = redundant ? c->partials + ((j + 1) & 1) * 3 * (size_t)nparts : nullptr;
     auto pass = [&](int tb0, int tbn, hipStream_t st) {
@@ -808,16 +906,11 @@ static int cg_onepass(sm_ctx *c) {
     TRY(halo2_multi(c, c->comm_stream, flds, fcs, 3));
     // edge t-blocks (tb_hi, TBk) and [0, tb_lo), wrapping: one launch, on the
     // comm stream behind the faces, concurrent with the interior launch
-    const bool conc = split && c->edge_concurrent;
-    if (conc) pass(tb_hi + 1, fc.TBk - 1 - tb_hi + tb_lo, c->comm_stream);
+    if (split) pass(tb_hi + 1, fc.TBk - 1 - tb_hi + tb_lo, c->comm_stream);
     HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
     if (split) pass(tb_lo, tb_hi - tb_lo + 1, c->stream);
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
-    if (!split) {
-        pass(0, fc.TBk, c->stream);
-    } else if (!conc) {
-        pass(tb_hi + 1, fc.TBk - 1 - tb_hi + tb_lo, c->stream);
-    }
+    if (!split) pass(0, fc.TBk, c->stream);
     launch_cg1_local_sum(c->stream, nparts, c->partials, c->sc);
     TRY(allreduce_dev(c, (double *)c->sc->sum3, 6));
     launch_cg1_from_sums(c->stream, c->sc, first);
@@ -853,10 +946,10 @@ static int cg_ra_pass(sm_ctx *c) {
     const bool one = !c->sharded();
     const bool angles = c->link_angles && c->uang_state == 1;
     const double *ua = angles ? c->Uang : nullptr;
-    if (one && !c->split_test) {
+    if (one) {
         // redundant scalars on small grids (partials by pass parity; every block
         // of the next pass evaluates them; sm_cg_iterate flushes the last pass)
-        const bool red = c->cg_redundant && fc.fold >= 2 && nparts <= c->cg_ra_red_max_blocks;
+        const bool red = fc.fold >= 2 && nparts <= c->cg_ra_red_max_blocks;
         double2 *part = red ? c->partials + (j & 1) * 3 * (size_t)nparts : c->partials;
         const double2 *prev = red ? c->partials + ((j + 1) & 1) * 3 * (size_t)nparts : nullptr;
         const bool tail = !red && c->cg_tail && fc.fold >= 2 && (nparts + 63) / 64 <= kMaxTickGroups;
@@ -874,7 +967,7 @@ static int cg_ra_pass(sm_ctx *c) {
     // pass 0 has no d_{-2}: its (zero-weighted) faces are d_0's own, never the
     // other slot, which holds nothing of this solve yet (the zero multiplier
     // beta2 = 0 would turn a stale NaN there into a NaN iterate)
-    double2 *f1 = one ? nullptr : face4_recv_d(c, j), *f2 = one ? nullptr : (first ? f1 : face4_recv_d(c, j - 1));
+    double2 *f1 = face4_recv_d(c, j), *f2 = first ? f1 : face4_recv_d(c, j - 1);
     // interior t-blocks: every lane's column (56g-4 .. 56g+59) inside [0, Wt)
     auto interior = [&](int tb) {
         const int g_lo = fc.wpb * tb, g_hi = std::min(fc.wpb * tb + fc.wpb - 1, fc.NWT - 1);
@@ -887,7 +980,6 @@ static int cg_ra_pass(sm_ctx *c) {
             tb_hi = tb;
         }
     const bool split = tb_hi >= tb_lo && tb_hi >= 0;
-    const bool conc = split && (one ? c->split_test == 2 : c->edge_concurrent != 0);
     const int nint = split ? tb_hi - tb_lo + 1 : 0, nedge = fc.TBk - nint;
     // Pipelined faces (t-shards, edge launch concurrent): the edge blocks write
     // d_j's 4-deep send faces themselves, and the exchange for pass j+1 follows
@@ -895,7 +987,7 @@ static int cg_ra_pass(sm_ctx *c) {
     // the edge launch marches short chunks so it ends long before the interior
     // one (its blocks otherwise run as long as the whole pass, AFTER the faces).
     CGFusedCfg ec = fc;
-    const bool pipe = conc && !one && c->cg_face_pipe && ra_edge_owns_faces(c, fc, tb_lo, tb_hi);
+    const bool pipe = split && c->cg_face_pipe && ra_edge_owns_faces(c, fc, tb_lo, tb_hi);
     if (pipe && c->cg_edge_xchunk > 0 && c->cg_edge_xchunk < fc.xchunk) {
         ec.xchunk = c->cg_edge_xchunk;
         ec.XB = (c->g.Nx + ec.xchunk - 1) / ec.xchunk;
@@ -908,21 +1000,21 @@ static int cg_ra_pass(sm_ctx *c) {
     // t-shard redundant scalars (with the tail): every block of pass j
     // evaluates pass j-1's scalars from its all-reduced sums (kept by pass
     // parity), so no scalar kernel sits between the all-reduce and the next pass
-    const bool red = !one && tail && c->cg_red_shards;
+    const bool red = tail && c->cg_red_shards;
     double2 *sums = red ? &c->sc->sumr[j & 1][0] : c->sc->sum3;  // this shard's sums (all-reduced below)
     auto pass = [&](const CGFusedCfg &cf, int tb0, int tbn, hipStream_t st, int pbase, double2 *fsend) {
-        launch_cg_ra(st, c->g, cf, c->kshards(), d1, d2, dn, c->cg_x, c->U, f1, f2, one ? nullptr : face4_recv_U(c),
-                     c->cg_mass, j, c->sc, c->partials, tb0, tbn, nullptr, ua, one ? nullptr : c->Uang_face, fsend,
-                     pbase, tail ? c->tick : nullptr, nparts_pass, c->gsum, one ? nullptr : sums, red ? 1 : 0);
+        launch_cg_ra(st, c->g, cf, c->kshards(), d1, d2, dn, c->cg_x, c->U, f1, f2, face4_recv_U(c), c->cg_mass, j,
+                     c->sc, c->partials, tb0, tbn, nullptr, ua, c->Uang_face, fsend, pbase, tail ? c->tick : nullptr,
+                     nparts_pass, c->gsum, sums, red ? 1 : 0);
     };
     HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
     // d_{j-1}'s faces: already in slot j & 1 if pass j-1 sent them (pipe)
-    if (!one && !(pipe && c->cg_faces_for == j)) TRY(halo4(c, c->comm_stream, d1, f1));
+    if (!(pipe && c->cg_faces_for == j)) TRY(halo4(c, c->comm_stream, d1, f1));
     c->cg_faces_for = -1;
     // edge t-blocks (tb_hi, TBk) and [0, tb_lo), wrapping: one launch on the
     // comm stream behind the faces, concurrent with the interior launch
-    if (conc) pass(ec, tb_hi + 1, nedge, c->comm_stream, nint * fc.XB, pipe ? face4_send(c, 0) : nullptr);
+    if (split) pass(ec, tb_hi + 1, nedge, c->comm_stream, nint * fc.XB, pipe ? face4_send(c, 0) : nullptr);
     HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
     if (split) pass(fc, tb_lo, nint, c->stream, 0, nullptr);
     if (pipe) {  // d_j's faces into slot (j+1) & 1 (d_{j-2}'s, read by this pass's edge launch above)
@@ -932,15 +1024,7 @@ static int cg_ra_pass(sm_ctx *c) {
         c->cg_faces_for = j + 1;
     }
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
-    if (!split) {
-        pass(fc, 0, fc.TBk, c->stream, 0, nullptr);
-    } else if (!conc) {
-        pass(fc, tb_hi + 1, nedge, c->stream, nint * fc.XB, nullptr);
-    }
-    if (one) {
-        if (!tail) launch_cg1_scalars(c->stream, nparts_pass, c->partials, c->sc, first);
-        return SM_OK;
-    }
+    if (!split) pass(fc, 0, fc.TBk, c->stream, 0, nullptr);
     if (!tail) launch_cg1_local_sum(c->stream, nparts_pass, c->partials, c->sc);
     TRY(allreduce_dev(c, (double *)sums, 6));
     if (red) {

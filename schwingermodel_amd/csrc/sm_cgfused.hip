@@ -413,8 +413,7 @@ CGFusedCfg cg_fused_config(const Geometry &g) {
     CGFusedCfg c;
     c.NWT = (g.Wt + FW - 1) / FW;
     c.TBk = (c.NWT + 3) / 4;
-    int target = 4096;  // 4096^2: xchunk 18 (tools/tune_cg.py: 16-32 best, 128 -12 %)
-    if (const char *e = getenv("SM_CGF_BLOCKS")) target = atoi(e);
+    const int target = 4096;  // 4096^2: xchunk 18 (tools/tune_cg.py: 16-32 best, 128 -12 %)
     int nchunks = (target + c.TBk - 1) / c.TBk;
     if (nchunks > g.Nx) nchunks = g.Nx;
     if (nchunks < 1) nchunks = 1;
@@ -428,7 +427,6 @@ CGFusedCfg cg_fused_config(const Geometry &g) {
         const int xmin = g.Nx / 64 < 12 ? g.Nx / 64 : 12;
         if (c.xchunk < xmin) c.xchunk = xmin;
     }
-    if (const char *e = getenv("SM_CGF_XCHUNK")) c.xchunk = atoi(e);
     c.XB = (g.Nx + c.xchunk - 1) / c.xchunk;
     c.remap = 1;
     return c;

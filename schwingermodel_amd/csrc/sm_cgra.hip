@@ -478,11 +478,7 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
         c.wpb = 1;
         c.xchunk = 40;
     }
-    if (const char *e = getenv("SM_CGRA_WPB")) c.wpb = atoi(e);
-    if (c.wpb != 1 && c.wpb != 2) c.wpb = 4;
     c.TBk = (c.NWT + c.wpb - 1) / c.wpb;
-    if (const char *e = getenv("SM_CGRA_XCHUNK")) c.xchunk = atoi(e);
-    if (c.xchunk < 1) c.xchunk = 1;
     c.XB = (g.Nx + c.xchunk - 1) / c.xchunk;
     c.remap = 1;
     // 1: folded bracket, 0.604 vs 0.625 ms per iteration at 4096^2 against the
@@ -490,7 +486,6 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
     // (tools/ab_fold.sh, ABBA: 0.513-0.517 vs 0.519-0.520 ms burst, 0.548-0.554
     // vs 0.552-0.557 sustained)
     c.fold = 2;
-    if (const char *e = getenv("SM_CGRA_FOLD")) c.fold = atoi(e);
     return c;
 }
 

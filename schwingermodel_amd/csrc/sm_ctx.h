@@ -53,7 +53,7 @@ struct sm_ctx {
     // code path, faces and scalar sums over a one-rank communicator (self
     // send/recv). Tests the RCCL data path on a single GPU.
     bool loop = false;
-    int debug_cg = 0;  // SM_DEBUG_CG=1: the CG host loops print their status at each check (stderr)
+    int debug_cg = 0;  // test option debug_cg=1: the CG host loops print their status at each check (stderr)
     bool sharded() const { return nshard > 1 || loop; }  // faces + collectives (else periodic wrap)
     int kshards() const { return sharded() ? 2 : 1; }    // the kernels' view: > 1 reads faces
     sm::Geometry g{};
@@ -67,7 +67,6 @@ struct sm_ctx {
     // creation: 5 from 256^2 sites per shard, 4 below (latency-bound grids).
     int cg_fused = 4;
     int cg_red_max_blocks = sm::kRedundantMaxBlocks;  // stored-Ad pass: redundant scalars up to this grid
-    int cg_redundant = 1;           // those grids: every block evaluates the previous pass's scalars
     long cg_flush_pass = -1;        // last one-pass pass whose scalars still await evaluation
     int cg_flush_nparts = 0;        // its partial count (the one-pass or the recompute-Ad grid)
     int cg_ra_red_max_blocks = 512; // recompute-Ad pass: redundant scalars up to this many blocks (one shard)
@@ -80,14 +79,11 @@ struct sm_ctx {
     double *Uang = nullptr;         // 2V angles (plane mu0 then mu1)
     double *Uang_face = nullptr;    // t-shards: angles of the 4-deep ghost links (16 Nx)
     hipStream_t own_stream = nullptr, stream = nullptr;
-    hipStream_t comm_stream = nullptr;  // halo exchange overlapped with interior compute
+    hipStream_t comm_stream = nullptr;  // halo exchange overlapped with interior compute (hosted: == stream)
+    bool own_comm_stream = false;       // comm_stream created by (and destroyed with) this context
     hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
     // t-shards: the edge block-columns run on the comm stream right after the
-    // halo, concurrently with the interior launch (0: after it, on the main
-    // stream). split_test > 0 runs the same interior/edge split on ONE shard
-    // (1: edge after interior, 2: concurrent) to measure it on one GPU.
-    int edge_concurrent = 1;
-    int split_test = 0;
+    // halo, concurrently with the interior launch on the main stream.
     // recompute-Ad CG on t-shards: the edge launch packs d_j's faces and the
     // exchange for pass j+1 is issued right behind it (cg_faces_for: the pass
     // whose d_{j-1} faces are already in flight); edge launch rows per block
@@ -102,7 +98,8 @@ struct sm_ctx {
     int cg_flush_sums = 0;          // the pending flush evaluates sc->sumr (t-shards), not partials
     unsigned *tick = nullptr;       // 1 + kMaxTickGroups counters, zeroed at creation
     double2 *gsum = nullptr;        // 3 per group
-    ncclComm_t comm = nullptr;
+    ncclComm_t comm = nullptr;       // main-stream communicator (faces-first halos, ghost links, all-reduces)
+    ncclComm_t comm_side = nullptr;  // comm-stream communicator (overlapped faces), split from comm
     bool hosted = false;            // host-callback transport instead of RCCL
     sm_host_transport tr{};
     double *h_face = nullptr;       // pinned: send_lo, send_hi, recv_lo, recv_hi (4 x up to 8Nx doubles)
@@ -187,6 +184,13 @@ int exchange_faces_on(sm_ctx *c, hipStream_t s, double2 *slo, double2 *shi, doub
 // point-to-point operations; the host-staged transport runs them in turn)
 int exchange_faces_multi(sm_ctx *c, hipStream_t s, int n, double2 *const *slo, double2 *const *shi,
                          double2 *const *rlo, double2 *const *rhi, size_t cnt);
+// RCCL contexts hold two communicators over the same ranks, one per stream:
+// operations issued on the comm stream use comm_side, those on the main
+// stream use comm. Each communicator thus sees ONE stream and runs its
+// operations in issue order (the same sequence on every rank) without
+// relying on RCCL to order a communicator's work across streams, and with
+// no cross-stream hand-off (measured ~10 us each through the loopback).
+ncclComm_t comm_for(const sm_ctx *c, hipStream_t s);
 int exchange_faces(sm_ctx *c, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi, size_t cnt);
 int allreduce_dev(sm_ctx *c, double *dev, int n);
 int halo(sm_ctx *c, const double2 *field, int set, int kind, TFaces *f);  // kind: FaceKind

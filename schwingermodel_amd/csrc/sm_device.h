@@ -276,6 +276,17 @@ __device__ __forceinline__ CGRed cg1_redundant(CGScalars *sc, const double2 *pre
 // the new state. One thread per block calls it; noinline keeps the division
 // chain's registers out of the march's allocation (inlined, the x-updating
 // t-shard kernels reached 256 VGPRs and one wave per SIMD).
+//
+// Invariant after the stop: the host keeps issuing passes (chunks overshoot)
+// and each one all-reduces sumr[j & 1] in place, although no block wrote that
+// slot, so the slot becomes nshard times a stale sum. That is harmless ONLY
+// because it is never read: pass J+1 (the first after the stopping
+// evaluation of pass J) finds red[(J+1) & 1] without done, evaluates the
+// stop from sumr[J & 1] (still valid: written by pass J, reduced once) and
+// block 0 stores the stopped state into red[J & 1]; pass J+2 then finds
+// red[J & 1] done and returns, and from there both red slots carry done, so
+// `if (!s.done)` skips every sumr read. Any change that lets a pass read sumr
+// before both red slots are done must stop the overshoot all-reduces first.
 static __device__ __attribute__((noinline)) void ra_scalars_from_sums(CGScalars *sc, long j, double2 *ab, int *stop) {
     CGRed s = sc->red[j & 1];
     const double2 *sums = sc->sumr[(j - 1) & 1];
@@ -375,8 +386,20 @@ __device__ __forceinline__ void cg_beta_scalar(CGScalars *sc, double2 rr) {
 // write-through (agent-scope atomic) stores -- no release fence, which would
 // write back the XCD's whole dirty L2 in every block -- wait for them, then
 // take a relaxed agent-scope ticket; the block drawing the last ticket of a
-// group reads the group's partials with agent-scope atomic loads and re-arms
-// the counter (zeroed at context creation).
+// group issues an agent-scope acquire, reads the group's partials with
+// agent-scope atomic loads and re-arms the counter (zeroed at context
+// creation).
+//
+// Memory-model note (gfx9 / gfx950 assumption): the publishing side has no
+// release operation. Its ordering comes from the hardware: agent-scope atomic
+// stores are written through to the (coherent, memory-side) fabric, the
+// vector memory counter counts stores, so `s_waitcnt vmcnt(0)` before the
+// barrier means every publishing wave's stores have completed before its
+// block's ticket is taken. The winning block's acquire fence (an L1
+// invalidate, no L2 writeback) and its atomic loads then see them from any
+// XCD. Under the portable HIP/C++ model this is a relaxed publication; a
+// target without write-through atomic stores or with a different vmcnt
+// meaning needs a release fetch_add instead.
 __device__ __forceinline__ void publish_partial(double2 *slot, double2 v) {
     __hip_atomic_store(&slot->x, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&slot->y, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -396,7 +419,9 @@ __device__ __forceinline__ bool last_block_arrive(unsigned *counter, unsigned nb
         *sh_flag = last;
     }
     __syncthreads();
-    return *sh_flag != 0;
+    const bool last = *sh_flag != 0;
+    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // block-uniform: the winner only
+    return last;
 }
 // Fixed-order wave sum (butterfly; every lane gets the same bits).
 __device__ __forceinline__ double2 wave_sum(double2 v) {

@@ -398,8 +398,7 @@ EoFusedCfg eo_fused_config(const Geometry &g) {
     const int Wh = g.Wt / 2;
     c.NWT = (Wh + EW - 1) / EW;
     c.TBk = (c.NWT + 3) / 4;
-    int target = 4096;                                    // blocks (as the fused CG pass)
-    if (const char *e = getenv("SM_EO_BLOCKS")) target = atoi(e);
+    const int target = 4096;                              // blocks (as the fused CG pass)
     int nchunks = (target + c.TBk - 1) / c.TBk;
     if (nchunks > g.Nx / 2) nchunks = g.Nx / 2;
     if (nchunks < 1) nchunks = 1;
@@ -412,7 +411,6 @@ EoFusedCfg eo_fused_config(const Geometry &g) {
     xmin = xmin < 2 ? 2 : (xmin > 8 ? 8 : xmin);
     if (xchunk < xmin) xchunk = xmin;
     xchunk += xchunk & 1;                                 // even: every chunk starts on an even row
-    if (const char *e = getenv("SM_EO_XCHUNK")) xchunk = atoi(e);
     c.xchunk = xchunk;
     c.XB = (g.Nx + c.xchunk - 1) / c.xchunk;
     return c;

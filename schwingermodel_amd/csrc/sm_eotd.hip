@@ -356,7 +356,6 @@ EoTdCfg eo_td_config(const Geometry &g) {
         c.xchunk = (g.Nx + nchunks - 1) / nchunks;
         if (c.xchunk < 2) c.xchunk = 2;
     }
-    if (const char *e = getenv("SM_EOTD_XCHUNK")) c.xchunk = atoi(e);
     if (c.xchunk < 2) c.xchunk = 2;
     c.xchunk += c.xchunk & 1;  // even: the kernel's row parities are static
     c.XB = (g.Nx + c.xchunk - 1) / c.xchunk;

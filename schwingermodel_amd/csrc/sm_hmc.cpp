@@ -61,11 +61,12 @@ int sm_gather_gauge(sm_ctx *c, double *U0, double *U1) {
         HIP_TRY(hipMalloc(&buf, sizeof(double) * cnt * P));
         HIP_TRY(hipMemcpyAsync(buf, c->U, sizeof(double) * cnt, hipMemcpyDeviceToDevice, c->stream));
     }
+    ncclComm_t cm = comm_for(c, c->stream);
     NCCL_TRY(ncclGroupStart());
     if (c->shard == 0) {
-        for (int r = 1; r < P; r++) NCCL_TRY(ncclRecv(buf + (size_t)r * 2 * V, cnt, ncclDouble, r, c->comm, c->stream));
+        for (int r = 1; r < P; r++) NCCL_TRY(ncclRecv(buf + (size_t)r * 2 * V, cnt, ncclDouble, r, cm, c->stream));
     } else {
-        NCCL_TRY(ncclSend(c->U, cnt, ncclDouble, 0, c->comm, c->stream));
+        NCCL_TRY(ncclSend(c->U, cnt, ncclDouble, 0, cm, c->stream));
     }
     NCCL_TRY(ncclGroupEnd());
     HIP_TRY(hipStreamSynchronize(c->stream));

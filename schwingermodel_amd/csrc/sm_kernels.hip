@@ -268,7 +268,6 @@ __global__ void __launch_bounds__(256) dslash_kernel_proj(DArgs a) { dslash_body
 LaunchCfg dslash_config(const Geometry &g) {
     LaunchCfg c;
     c.bt = g.Wt >= 256 ? 256 : (g.Wt >= 128 ? 128 : 64);
-    if (const char *e = getenv("SM_BT")) c.bt = atoi(e);
     const int tb = (g.Wt + c.bt - 1) / c.bt;
     // 32-row marches where they give 256..4096 blocks, 16 rows above that,
     // else ~2048 blocks (tools/shape_tune.hip, profiles/r02_shape_tune.jsonl,
@@ -276,11 +275,10 @@ LaunchCfg dslash_config(const Geometry &g) {
     // 6581 vs 6128, 8192x1024 5432 vs 5048, 8192x8192 5486 vs 5363; 4096^2
     // is 32 rows either way)
     const long b32 = (long)tb * ((g.Nx + 31) / 32);
-    int target = 2048;
-    if (const char *e = getenv("SM_BLOCKS")) target = atoi(e);
-    if (b32 >= 256 && b32 <= 4096 && !getenv("SM_BLOCKS")) {
+    const int target = 2048;
+    if (b32 >= 256 && b32 <= 4096) {
         c.xchunk = 32;
-    } else if (b32 > 4096 && !getenv("SM_BLOCKS")) {
+    } else if (b32 > 4096) {
         c.xchunk = 16;
     } else {
         int nchunks = (target + tb - 1) / tb;
@@ -288,11 +286,8 @@ LaunchCfg dslash_config(const Geometry &g) {
         if (nchunks < 1) nchunks = 1;
         c.xchunk = (g.Nx + nchunks - 1) / nchunks;
     }
-    if (const char *e = getenv("SM_XCHUNK")) c.xchunk = atoi(e);
     c.xcd_remap = 1;
-    if (const char *e = getenv("SM_XCD_REMAP")) c.xcd_remap = atoi(e);
     c.variant = 1;  // two-row lookahead: 296 vs 315 us at 4096^2 (profiles/r01)
-    if (const char *e = getenv("SM_DSLASH_VARIANT")) c.variant = atoi(e);
     return c;
 }
 

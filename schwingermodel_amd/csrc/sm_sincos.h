@@ -8,6 +8,16 @@
 // (tests/test_sincos_host.py compiles this same header for the host), ~25 fp64
 // operations against ~60 for a general-argument sincos. Plain C as well, so
 // the host test runs the exact device arithmetic (explicit fmas, no contraction).
+//
+// The polynomial coefficients and the cos-kernel's compensated sum below are
+// those of fdlibm's k_sin.c / k_cos.c, which carry this notice:
+//
+//   Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+//
+//   Developed at SunSoft, a Sun Microsystems, Inc. business.
+//   Permission to use, copy, modify, and distribute this
+//   software is freely granted, provided that this notice
+//   is preserved.
 #pragma once
 
 #ifdef __HIPCC__

@@ -15,18 +15,6 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "multiproc: runs several worker processes on the one GPU")
 
 
-def pytest_collection_modifyitems(config, items):
-    """Multi-process GPU tests (several shards as processes sharing ONE GPU)
-    run before any test that initialises HIP inside the pytest process itself.
-    Measured on the MI355X pool: with the pytest process holding a HIP context,
-    6- and 8-process even-odd runs stalled inside GPU waits after a few CG
-    passes (every rank in a GPU sync, nothing progressing for minutes), while
-    the same tests pass with an idle parent. The extra context is a test-rig
-    artefact (a real t-sharded run has one process per GPU), so the suite keeps
-    the parent off the GPU until the multi-process tests are done."""
-    items.sort(key=lambda it: 0 if it.get_closest_marker("multiproc") else 1)  # stable sort
-
-
 @pytest.fixture(scope="session")
 def oracle():
     """ctypes handle on oracle/liboracle.so (built on demand; test checker only)."""
@@ -85,6 +73,32 @@ def load_md_fixture(name):
 
 def md_fixture_names():
     return sorted(load_manifest().get("md", {}).keys())
+
+
+def sm_opts(**kw):
+    """Environment of the library's test-only switches: ONE variable,
+    SM_TEST_OPTS="key=value,...", read when a context is created
+    (schwingermodel_amd/csrc/sm_capi.cpp apply_test_opts lists the keys)."""
+    return {"SM_TEST_OPTS": ",".join(f"{k}={v}" for k, v in kw.items())} if kw else {}
+
+
+class opts_env:
+    """Context manager: SM_TEST_OPTS set to **kw while a context is created."""
+
+    def __init__(self, **kw):
+        self.env = sm_opts(**kw)
+
+    def __enter__(self):
+        self.old = os.environ.get("SM_TEST_OPTS")
+        os.environ.pop("SM_TEST_OPTS", None)
+        os.environ.update(self.env)
+        return self
+
+    def __exit__(self, *exc):
+        os.environ.pop("SM_TEST_OPTS", None)
+        if self.old is not None:
+            os.environ["SM_TEST_OPTS"] = self.old
+        return False
 
 
 def ptr(a):

@@ -75,41 +75,69 @@ def run(cmd, **kw):
     return r.stdout
 
 
-# Large-lattice summary fixtures (BASELINE config 2): full outputs are too big
-# to commit, so keep the reference's outputs at SAMPLE_SITES seeded random
-# sites plus global norms; the GPU test regenerates the inputs with the same
-# counter-based generator (bit-exact, tests/test_capi_host.py) and compares.
-LARGE = [("l1024x1024_b3_m-0p10", 1024, 1024, 0.3246, -0.10)]
+# Large-lattice summary fixtures (BASELINE configs 2, 3 and 5): full outputs
+# are too big to commit, so keep the reference's outputs at SAMPLE_SITES seeded
+# random sites plus global norms; the GPU test regenerates the inputs with the
+# same counter-based generator (bit-exact, tests/test_capi_host.py) and
+# compares. name, Nx, Nt, sigma, m0, (ranks_x, ranks_t) of the reference run.
+# 1 rank is the reference's own sequential dot order; 8192^2 runs on 2x2 MPI
+# ranks (a 1-rank solve there takes ~8 h on one core), which changes only the
+# dots' summation order (the operators are decomposition-invariant bitwise,
+# manifest "decomposition_2x2").
+LARGE = [("l1024x1024_b3_m-0p10", 1024, 1024, 0.3246, -0.10, (1, 1)),
+         ("l4096x4096_b5_m-0p06", 4096, 4096, 0.2374, -0.06, (1, 1)),
+         ("l8192x8192_b2_m-0p19", 8192, 8192, 0.4242, -0.19, (2, 2))]
 SAMPLE_SITES = 4096
 
 
-def make_large(name, nx, nt, sigma, m0, workdir=None):
+def _fsum_sq(a, chunk=1 << 22):
+    """Exactly rounded sum of squares of a (math.fsum), streamed in chunks so
+    that an 8192^2 field never becomes one Python list."""
+    import itertools
+    return math.fsum(itertools.chain.from_iterable((a[i:i + chunk] * a[i:i + chunk]).tolist()
+                                                   for i in range(0, a.size, chunk)))
+
+
+def run_large_reference(name, nx, nt, sigma, m0, ranks, workdir, mpirun):
+    """Generate the inputs and run the reference's fixture mode in workdir
+    (resumable: a finished run leaves meta.json there)."""
     exe = os.path.join(REF_DIR, f"sm_ref_{nx}x{nt}")
-    with tempfile.TemporaryDirectory() as tmp:
-        d = workdir or tmp
-        if not os.path.exists(os.path.join(d, "meta.json")) or os.path.getsize(os.path.join(d, "meta.json")) == 0:
-            run([exe, "gen", d, str(SEED_U), repr(sigma), str(SEED_PSI), str(SEED_CHI)])
-            meta = json.loads(run([exe, "fixture", d, "1", "1", repr(m0), "1e-10", "10000"]))
+    mpath = os.path.join(workdir, "meta.json")
+    if os.path.exists(mpath) and os.path.getsize(mpath) > 0:
+        with open(mpath) as f:
+            return json.load(f)
+    os.makedirs(workdir, exist_ok=True)
+    run([exe, "gen", workdir, str(SEED_U), repr(sigma), str(SEED_PSI), str(SEED_CHI)])
+    rx, rt = ranks
+    cmd = [exe, "fixture", workdir, str(rx), str(rt), repr(m0), "1e-10", "10000"]
+    if rx * rt > 1:
+        cmd = [mpirun, "-n", str(rx * rt)] + cmd
+    meta = json.loads(run(cmd))
+    with open(mpath, "w") as f:
+        json.dump(meta, f)
+    return meta
+
+
+def make_large(name, nx, nt, sigma, m0, ranks, workdir, mpirun):
+    meta = run_large_reference(name, nx, nt, sigma, m0, ranks, workdir, mpirun)
+    S = nx * nt
+    meta_sha, meta_sumsq = {}, {}
+    rng = np.random.default_rng(20261015)
+    sites = np.sort(rng.choice(S, SAMPLE_SITES, replace=False))
+    out = {"sites": sites}
+    for k in OUTS:
+        a = np.fromfile(os.path.join(workdir, k + ".bin"), dtype=np.float64)
+        if k == "ref_force":
+            out[k] = np.concatenate([a[:S][sites], a[S:][sites]])
         else:
-            with open(os.path.join(d, "meta.json")) as f:
-                meta = json.load(f)
-        S = nx * nt
-        meta_sha, meta_sumsq = {}, {}
-        rng = np.random.default_rng(20261015)
-        sites = np.sort(rng.choice(S, SAMPLE_SITES, replace=False))
-        out = {"sites": sites}
-        for k in OUTS:
-            a = np.fromfile(os.path.join(d, k + ".bin"), dtype=np.float64)
-            if k == "ref_force":
-                out[k] = np.concatenate([a[:S][sites], a[S:][sites]])
-            else:
-                c0 = a[:2 * S].view(np.complex128)
-                c1 = a[2 * S:].view(np.complex128)
-                out[k] = np.concatenate([c0[sites], c1[sites]]).view(np.float64)
-            # machine-independent whole-field checks: SHA-256 of the bytes (the
-            # bitwise outputs) and the exactly rounded sum of squares (CG x)
-            meta_sha[k] = hashlib.sha256(a.tobytes()).hexdigest()
-            meta_sumsq[k] = math.fsum((a * a).tolist())
+            c0 = a[:2 * S].view(np.complex128)
+            c1 = a[2 * S:].view(np.complex128)
+            out[k] = np.concatenate([c0[sites], c1[sites]]).view(np.float64)
+        # machine-independent whole-field checks: SHA-256 of the bytes (the
+        # bitwise outputs) and the exactly rounded sum of squares (CG x)
+        meta_sha[k] = hashlib.sha256(a.tobytes()).hexdigest()
+        meta_sumsq[k] = _fsum_sq(a)
+        del a
     meta.update({"sigma": sigma, "file": name + ".npz", "summary": True, "sample_sites": SAMPLE_SITES,
                  "sha256": meta_sha, "fsum_sq": meta_sumsq})
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
@@ -266,8 +294,11 @@ def make_conf(name, nx, nt, sigma, ranks, mpirun):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mpi", action="store_true", help="also run 2x2 ranks (mpirun)")
-    ap.add_argument("--large", action="store_true", help="also the 1024^2 summary fixture (~4 min CPU)")
-    ap.add_argument("--large-workdir", default=None, help="reuse an existing reference run directory")
+    ap.add_argument("--large", nargs="+", default=None, metavar="NAME",
+                    help="(re)make only these summary fixtures (LARGE names): 1024^2 ~4 min on one core, "
+                         "4096^2 ~70 min on one core, 8192^2 ~2-3 h on 2x2 ranks")
+    ap.add_argument("--large-workdir", default="/tmp/sm_large",
+                    help="parent of the per-fixture reference run directories (resumable)")
     ap.add_argument("--mpirun", default="/opt/conda/bin/mpirun")
     ap.add_argument("--md-only", action="store_true", help="regenerate only the MD fixtures")
     ap.add_argument("--hmc-stat", action="store_true", help="(re)run the reference HMC program (~2 min)")
@@ -276,6 +307,24 @@ def main():
                     help="run this many more independent reference HMC chains in parallel (~4 min) into hmc_stat_chains")
     ap.add_argument("--conf-only", action="store_true", help="regenerate only the SaveConf fixtures")
     args = ap.parse_args()
+    if args.large:
+        todo = [e for e in LARGE if e[0] in args.large]
+        if len(todo) != len(args.large):
+            raise SystemExit(f"unknown large fixture in {args.large}; known: {[e[0] for e in LARGE]}")
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref",
+                        "REF_SIZES=" + " ".join(f"{e[1]}x{e[2]}" for e in todo)], check=True)
+        path = os.path.join(HERE, "manifest.json")
+        for name, nx, nt, sigma, m0, ranks in todo:
+            meta = make_large(name, nx, nt, sigma, m0, ranks, os.path.join(args.large_workdir, name),
+                              args.mpirun)
+            with open(path) as f:  # re-read: several --large runs may be in flight
+                manifest = json.load(f)
+            manifest.setdefault("large", {})[name] = meta
+            with open(path, "w") as f:
+                json.dump(manifest, f, indent=1, sort_keys=True)
+            print(name, json.dumps({k: meta[k] for k in ("cg_iters", "cg_true_relres", "cg_seconds")}),
+                  file=sys.stderr)
+        return
     if args.conf_only:
         sizes = sorted({f"{nx}x{nt}" for _, nx, nt, *_ in CONF_FIXTURES})
         subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref", "REF_SIZES=" + " ".join(sizes)],
@@ -365,16 +414,10 @@ def main():
                              "cg": {"tol": 1e-10, "max_iter": 10000}}
     manifest["jackknife"] = make_jackknife()
     manifest["conf"] = {n: make_conf(n, nx, nt, sg, rk, args.mpirun) for n, nx, nt, sg, rk in CONF_FIXTURES}
-    if args.large:
-        subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref", "REF_SIZES=1024x1024"], check=True)
-        manifest["large"] = {}
-        for name, nx, nt, sigma, m0 in LARGE:
-            manifest["large"][name] = make_large(name, nx, nt, sigma, m0, args.large_workdir)
-    else:
-        old = os.path.join(HERE, "manifest.json")
-        if os.path.exists(old):
-            with open(old) as f:
-                manifest["large"] = json.load(f).get("large", {})
+    old = os.path.join(HERE, "manifest.json")
+    if os.path.exists(old):
+        with open(old) as f:
+            manifest["large"] = json.load(f).get("large", {})
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
 

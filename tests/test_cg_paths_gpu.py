@@ -7,17 +7,16 @@ it) and the redundant t-shard scalars (every block evaluates the previous
 pass's scalars from the all-reduced sums). Each one changes only where a sum
 or a scalar step runs, or the order of a fixed-order sum, so a solve with it
 and one with the older form (the environment switches read at context
-creation) must reach the same iteration count and x to 1e-12 -- the
+creation, SM_TEST_OPTS) must reach the same iteration count and x to 1e-12 -- the
 reduction-order band of every other CG parity test
 (src/conjugate_gradient.cpp:28-66 is the recurrence all of them follow).
 """
 import ctypes
-import os
 
 import numpy as np
 import pytest
 
-from conftest import ptr
+from conftest import opts_env, ptr
 
 pytestmark = pytest.mark.gpu
 
@@ -28,21 +27,13 @@ def sm():
     return schwingermodel_amd
 
 
-def solve(sm, Nx, Nt, sigma, m0, env, loopback=False, eo=False):
+def solve(sm, Nx, Nt, sigma, m0, opts, loopback=False, eo=False):
     S = Nx * Nt
     U, psi = np.empty(4 * S), np.empty(4 * S)
     sm.lib.sm_fill_gauge(4321, sigma, Nt, 0, Nx, 0, Nt, ptr(U[:2 * S]), ptr(U[2 * S:]))
     sm.lib.sm_fill_spinor(5678, Nt, 0, Nx, 0, Nt, ptr(psi[:2 * S]), ptr(psi[2 * S:]))
-    old = {k: os.environ.get(k) for k in env}
-    try:
-        os.environ.update(env)
+    with opts_env(**opts):
         L = sm.Lattice(Nx, Nt, loopback=loopback)  # the switches are read here
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
     try:
         sm.check(sm.lib.sm_upload_gauge(L.ctx, ptr(U[:2 * S]), ptr(U[2 * S:])))
         x = np.empty(4 * S)
@@ -72,28 +63,28 @@ def agree(a, b):
 @pytest.mark.parametrize("shape", [(1024, 1024), (96, 4096)], ids=["1024x1024", "96x4096"])
 def test_ticketed_tail_matches_scalar_kernel(sm, shape):
     Nx, Nt = shape
-    env = {"SM_CGRA_RED_MAX_BLOCKS": "0"}
-    agree(solve(sm, Nx, Nt, 0.3246, -0.10, env), solve(sm, Nx, Nt, 0.3246, -0.10, dict(env, SM_CG_TAIL="0")))
+    opts = {"ra_red_max_blocks": 0}
+    agree(solve(sm, Nx, Nt, 0.3246, -0.10, opts), solve(sm, Nx, Nt, 0.3246, -0.10, dict(opts, tail=0)))
 
 
 def test_even_odd_tail_matches_scalar_kernel(sm):
     agree(solve(sm, 256, 256, 0.3246, -0.05, {}, eo=True),
-          solve(sm, 256, 256, 0.3246, -0.05, {"SM_CG_TAIL": "0"}, eo=True))
+          solve(sm, 256, 256, 0.3246, -0.05, {"tail": 0}, eo=True))
 
 
 # the t-shard path through the one-rank RCCL loopback: every variant against
 # the older schedule (faces packed and sent at the start of each pass, the
 # scalar kernel after the all-reduce, a separate local-sum kernel)
-@pytest.mark.parametrize("env", [
+@pytest.mark.parametrize("opts", [
     {},
-    {"SM_CG_RED_SHARDS": "0"},
-    {"SM_CG_FACE_PIPE": "0"},
-    {"SM_CG_EDGE_XCHUNK": "0"},
-    {"SM_CG_TAIL": "0"},
+    {"red_shards": 0},
+    {"face_pipe": 0},
+    {"edge_xchunk": 0},
+    {"tail": 0},
 ], ids=["default", "no_red", "no_pipe", "long_edge", "no_tail"])
-def test_tshard_schedules_agree(sm, env):
-    old = {"SM_CG_FACE_PIPE": "0", "SM_CG_RED_SHARDS": "0", "SM_CG_TAIL": "0"}
-    agree(solve(sm, 64, 4096, 0.2374, -0.06, env, loopback=True),
+def test_tshard_schedules_agree(sm, opts):
+    old = {"face_pipe": 0, "red_shards": 0, "tail": 0}
+    agree(solve(sm, 64, 4096, 0.2374, -0.06, opts, loopback=True),
           solve(sm, 64, 4096, 0.2374, -0.06, old, loopback=True))
 
 
@@ -131,4 +122,4 @@ def test_even_odd_tshard_redundant_scalars_agree(sm):
     (every block evaluates the previous pass's scalars from the all-reduced
     sums) against the scalar kernel after the all-reduce."""
     agree(solve(sm, 64, 512, 0.3246, -0.05, {}, loopback=True, eo=True),
-          solve(sm, 64, 512, 0.3246, -0.05, {"SM_CG_RED_SHARDS": "0"}, loopback=True, eo=True))
+          solve(sm, 64, 512, 0.3246, -0.05, {"red_shards": 0}, loopback=True, eo=True))

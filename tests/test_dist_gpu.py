@@ -8,6 +8,7 @@ reference's iteration count (+-1 %) to 1e-12 relative.
 """
 import pytest
 
+from conftest import sm_opts
 from distutil import run_world
 
 pytestmark = [pytest.mark.gpu, pytest.mark.multiproc]
@@ -22,7 +23,7 @@ pytestmark = [pytest.mark.gpu, pytest.mark.multiproc]
 def test_sharded_gpu_path_matches_reference(tmp_path, fixture, world):
     # bt = 64 so the Dirac apply of the larger shards also splits into interior
     # and edge t-blocks (the overlapped halo path)
-    env = {"SM_BT": "64"} if fixture.startswith("gen:") else None
+    env = sm_opts(bt=64) if fixture.startswith("gen:") else None
     rep = run_world("gpu", fixture, world, tmp_path, timeout=140, extra_env=env)
     c = rep["checks"]
     for k in ("ref_Dpsi", "ref_Ddagchi", "ref_DDdagpsi", "ref_force"):
@@ -36,9 +37,9 @@ def test_sharded_gpu_path_matches_reference(tmp_path, fixture, world):
 
 @pytest.mark.parametrize("fixture,world", [("l32x48_b3_m-0p10", 4), ("gen:48x1024:0.3:-0.05", 2)])
 def test_sharded_twodir_cg_matches_reference(tmp_path, fixture, world):
-    """The two-direction CG (SM_CG_FUSED=4: d_{j-2} faces instead of r faces)
+    """The two-direction CG (test option cg=4: d_{j-2} faces instead of r faces)
     on t-shards: the reference's iteration count and solution."""
-    rep = run_world("gpu", fixture, world, tmp_path, timeout=140, extra_env={"SM_CG_FUSED": "4"})
+    rep = run_world("gpu", fixture, world, tmp_path, timeout=140, extra_env=sm_opts(cg=4))
     assert rep["checks"]["ref_cgx"] <= 1e-12
     ref = rep["ref_cg_iters"]
     assert len(set(rep["cg_iters"])) == 1 and abs(rep["cg_iters"][0] - ref) <= max(1, ref // 100)
@@ -49,12 +50,12 @@ def test_sharded_twodir_cg_matches_reference(tmp_path, fixture, world):
                                            ("gen:48x1024:0.3:-0.05", 2), ("gen:32x960:0.4242:0.0", 4),
                                            ("l16x16_b2_m-0p19", 4), ("l16x16_b2_m-0p19", 8)])
 def test_sharded_recompute_cg_matches_reference(tmp_path, fixture, world):
-    """The recompute-Ad CG (SM_CG_FUSED=5: 4-deep faces of d_{j-1}, d_{j-2}'s
+    """The recompute-Ad CG (test option cg=5: 4-deep faces of d_{j-1}, d_{j-2}'s
     kept from the previous pass, 4-deep ghost links) on t-shards, including the
     interior/edge split of Wt = 512 / 240, the narrowest shard it takes (Wt = 4)
     and the fall-back to the stored-Ad pass below it (Wt = 2): the reference's
     iteration count and solution."""
-    rep = run_world("gpu", fixture, world, tmp_path, timeout=140, extra_env={"SM_CG_FUSED": "5"})
+    rep = run_world("gpu", fixture, world, tmp_path, timeout=140, extra_env=sm_opts(cg=5))
     assert rep["checks"]["ref_cgx"] <= 1e-12
     ref = rep["ref_cg_iters"]
     assert len(set(rep["cg_iters"])) == 1 and abs(rep["cg_iters"][0] - ref) <= max(1, ref // 100)
@@ -102,7 +103,7 @@ def test_sharded_even_odd_matches_one_shard(tmp_path, fixture, world, fused, fol
     half-lattice CG to 1e-10 in the same iteration count (+-1 %), the MD force
     to 1e-10, and an HMC trajectory with the same accept decision."""
     rep = run_world("eo", fixture, world, tmp_path, timeout=140,
-                    extra_env={"SM_EO_FUSED": fused, "SM_EO_CG_FOLDED": folded, "SM_EO_CG_TD": td})
+                    extra_env=sm_opts(eo_fused=fused, eo_cg_folded=folded, eo_cg_td=td))
     c = rep["checks"]
     assert c["dhat"] is True and c["dhatdag"] is True, c
     # the sharded dots sum per-shard partials: a different rounding order

@@ -22,7 +22,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, load_fixture, ptr
+from conftest import GOLDEN, load_fixture, opts_env, ptr
 
 pytestmark = pytest.mark.gpu
 MAXIT = 10000
@@ -85,11 +85,8 @@ def test_fused_dhat_bitwise_equals_two_hops(sm, name, dag):
     v = even_only(a["psi"], Nx, Nt)
     outs = []
     for fused in ("1", "0"):
-        os.environ["SM_EO_FUSED"] = fused  # read when the context is created
-        try:
+        with opts_env(eo_fused=fused):  # read when the context is created
             L = sm.Lattice(Nx, Nt)
-        finally:
-            os.environ.pop("SM_EO_FUSED", None)
         sm.check(sm.lib.sm_upload_gauge(L.ctx, ptr(a["U"][:2 * S]), ptr(a["U"][2 * S:])))
         o = np.empty(4 * S)
         sm.check(sm.lib.sm_eo_dhat(L.ctx, dag, ptr(v[:2 * S]), ptr(v[2 * S:]), ptr(o[:2 * S]), ptr(o[2 * S:]), m0))
@@ -128,7 +125,7 @@ def _gen_eo_case(sm, Nx, Nt):
     return {"Nx": Nx, "Nt": Nt, "m0": -0.1}, a
 
 
-@pytest.mark.parametrize("variant", ["SM_EO_CG_FOLDED", "SM_EO_CG_TD"], ids=["folded", "twodir"])
+@pytest.mark.parametrize("variant", ["eo_cg_folded", "eo_cg_td"], ids=["folded", "twodir"])
 @pytest.mark.parametrize("name", ["l64x64_b5_m-0p06", "l32x48_b3_m-0p10", "l16x16_b2_m-0p19", "gen:256x120",
                                   "gen:8x12"])
 def test_folded_eo_cg_matches_six_kernel_eo_cg(sm, name, variant):
@@ -148,11 +145,8 @@ def test_folded_eo_cg_matches_six_kernel_eo_cg(sm, name, variant):
     phi = even_only(a["psi"], Nx, Nt)
     out = {}
     for folded in ("1", "0"):
-        os.environ[variant] = folded  # read when the context is created
-        try:
+        with opts_env(**{variant: folded}):  # read when the context is created
             L = sm.Lattice(Nx, Nt)
-        finally:
-            os.environ.pop(variant, None)
         sm.check(sm.lib.sm_upload_gauge(L.ctx, ptr(a["U"][:2 * S]), ptr(a["U"][2 * S:])))
         x = np.empty(4 * S)
         res = sm.CGResult()

@@ -10,7 +10,7 @@ import ctypes
 import numpy as np
 import pytest
 
-from conftest import bits_equal, fixture_names, load_fixture, planes, ptr
+from conftest import bits_equal, fixture_names, load_fixture, opts_env, planes, ptr
 
 pytestmark = pytest.mark.gpu
 
@@ -190,19 +190,9 @@ def test_recompute_matches_twodir(sm, Nx, Nt, xchunk, fold, red):
     x within the reduction-order band, including chunks shorter than the
     4-row halo, Nt not a multiple of the 56-column wave and a lattice smaller
     than one wave's halo."""
-    import os
     S = Nx * Nt
-    env = {"SM_CGRA_FOLD": fold, "SM_CGRA_RED_MAX_BLOCKS": red}  # read when the context is created
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
+    with opts_env(fold=fold, ra_red_max_blocks=red):  # read when the context is created
         L = sm.init(Nx, Nt)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
     U, psi = sm.spinor(S), sm.spinor(S)
     P = lambda a: a.ctypes.data  # noqa: E731
     sm.lib.sm_fill_gauge(4321, 0.4242, Nt, 0, Nx, 0, Nt, P(U.mu0), P(U.mu1))
