@@ -277,6 +277,56 @@ def run_eo(name, result_path, dist, rank, world):
     dist.destroy_process_group()
 
 
+def run_eocg(name, result_path, dist, rank, world):
+    """mode "eocg": only the even-odd half-lattice CG on t-shards (hosted
+    transport) vs one shard, with max_iter from SM_WORKER_EO_MAXIT (a cut-off
+    solve stops mid-chunk and further passes are issued past the stop: the
+    redundant t-shard scalars must keep the stopped state). Reports each
+    shard's (converged, iterations) and the relative difference of x."""
+    import schwingermodel_amd as sm
+    from schwingermodel_amd import dist as smd
+    _, dims, sigma, m0s = name.split(":")
+    Nx, Nt = (int(v) for v in dims.split("x"))
+    sigma, m0 = float(sigma), float(m0s)
+    maxit = int(os.environ.get("SM_WORKER_EO_MAXIT", "10000"))
+    S = Nx * Nt
+    g = {k: np.empty(4 * S) for k in ("U", "psi")}
+    sm.lib.sm_fill_gauge(4321, sigma, Nt, 0, Nx, 0, Nt, g["U"].ctypes.data, g["U"][2 * S:].ctypes.data)
+    sm.lib.sm_fill_spinor(5678, Nt, 0, Nx, 0, Nt, g["psi"].ctypes.data, g["psi"][2 * S:].ctypes.data)
+    t0, Wt = ctypes.c_int(), ctypes.c_int()
+    sm.check(sm.lib.sm_shard_plan(Nt, world, rank, ctypes.byref(t0), ctypes.byref(Wt)))
+    t0, Wt = t0.value, Wt.value
+    P_ = lambda x: ctypes.c_void_p(x.ctypes.data)  # noqa: E731
+
+    def solve(ctx, V, U, p):
+        sm.check(sm.lib.sm_upload_gauge(ctx, P_(U[0]), P_(U[1])))
+        x0, x1 = np.empty(V, complex), np.empty(V, complex)
+        res = sm.CGResult()
+        sm.check(sm.lib.sm_eo_cg(ctx, P_(p[0]), P_(p[1]), P_(x0), P_(x1), m0, 1e-10, maxit, ctypes.byref(res)))
+        return (x0, x1), (int(res.converged), int(res.iterations))
+
+    mine = [shard_field(g[k], Nx, Nt, t0, Wt) for k in ("U", "psi")]
+    dev = int(os.environ.get("SM_DEVICE", "0"))
+    ctx, tr = smd.create_hosted_context(Nx, Nt, device=dev)
+    x, cg = solve(ctx, Nx * Wt, mine[0], mine[1])
+    sm.lib.sm_destroy(ctx)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, (x, cg))
+    if rank == 0:
+        L = sm.Lattice(Nx, Nt, device=dev)
+        full = [shard_field(g[k], Nx, Nt, 0, Nt) for k in ("U", "psi")]
+        x1, cg1 = solve(L.ctx, S, full[0], full[1])
+        L.close()
+        gsh = unshard([d[0] for d in gathered], Nx, Nt, Wt, complex)
+        ref = unshard([x1], Nx, Nt, Nt, complex)
+        rep = {"world": world, "Wt": Wt, "max_iter": maxit, "cg": [list(d[1]) for d in gathered],
+               "cg_one": list(cg1), "x_rel": float(np.linalg.norm(gsh - ref) / np.linalg.norm(ref))}
+        with open(result_path, "w") as f:
+            json.dump(rep, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def fill_block(sm, Nx, Nt, t0, Wt, sigma, seeds=(4321, 5678, 91011), nthreads=8):
     """U, psi, chi of the t-block [t0, t0+Wt) of the global synthetic fields
     (counter-based, row-separable: row blocks are filled in threads)."""
@@ -420,6 +470,8 @@ def main():
         return run_md(name, result_path, dist, rank, world)
     if mode == "eo":
         return run_eo(name, result_path, dist, rank, world)
+    if mode == "eocg":
+        return run_eocg(name, result_path, dist, rank, world)
     if mode == "big":
         return run_big(name, result_path, dist, rank, world)
     from conftest import bits_equal, load_fixture

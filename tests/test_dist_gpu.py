@@ -120,3 +120,27 @@ def test_sharded_even_odd_matches_one_shard(tmp_path, fixture, world, fused, fol
     assert abs(dH - rep["traj_one"][0]) <= 1e-6 * max(1.0, abs(rep["traj_one"][0]))
     assert acc == rep["traj_one"][1] and r == rep["traj_one"][2]
     assert c["traj_U"] <= 1e-8, c
+
+
+@pytest.mark.parametrize("red", [1, 0], ids=["red", "nored"])
+@pytest.mark.parametrize("max_iter", [10000, 16, 17], ids=["converge", "stop_even", "stop_odd"])
+def test_sharded_even_odd_cg_schedules(tmp_path, red, max_iter):
+    """The one-pass even-odd CG on 4 real t-shard processes (host transport),
+    with the redundant scalars (every block of pass j+1 evaluates pass j's
+    scalars from the all-reduced sums, test option red_shards=1) and with the
+    scalar kernel after the all-reduce (red_shards=0), converged and cut off
+    by max_iter after an even or an odd pass (the host keeps issuing passes
+    past the stop, so the stopped state must survive the overshoot, ADVICE
+    r02): every shard reports the one-shard iteration count and convergence
+    flag, and x agrees with the one-shard solve to 1e-10 (the sharded
+    reduction order)."""
+    rep = run_world("eocg", "gen:32x48:0.3:-0.1", 4, tmp_path, timeout=140,
+                    extra_env=dict(sm_opts(red_shards=red), SM_WORKER_EO_MAXIT=str(max_iter)))
+    assert rep["Wt"] >= 8  # the one-pass kernel on t-shards, not the six-launch fall-back
+    conv1, it1 = rep["cg_one"]
+    for conv, it in rep["cg"]:
+        assert conv == conv1, rep
+        assert it == it1 if max_iter < 10000 else abs(it - it1) <= max(1, it1 // 100), rep
+    if max_iter < 10000:
+        assert conv1 == 0 and it1 == max_iter, rep
+    assert rep["x_rel"] <= 1e-10, rep
