@@ -250,9 +250,10 @@ def cpu_baseline(cfg, threads, ncg):
 
 
 def load_traffic(nx, nt):
-    """HBM bytes per dslash launch from the committed rocprofv3 PMC summary
-    (profiles/*_dslash_pmc.json, FETCH_SIZE + WRITE_SIZE with the gfx950 rule);
-    the newest file for this local shape wins."""
+    """HBM bytes per launch of the Dirac apply and of the CG pass from the
+    committed rocprofv3 PMC summary (profiles/*_dslash_pmc.json, FETCH_SIZE +
+    WRITE_SIZE with the gfx950 rule); the newest file for this local shape
+    wins. Returns (file, apply bytes, CG pass bytes or None)."""
     best = None
     pdir = os.path.join(REPO, "profiles")
     if os.path.isdir(pdir):
@@ -264,7 +265,7 @@ def load_traffic(nx, nt):
                     with open(os.path.join(pdir, f)) as fh:
                         d = json.load(fh)
                     if d.get("Nx") == nx and d.get("Nt") == nt:
-                        best = (f, d.get("hbm_bytes_per_launch"))
+                        best = (f, d.get("hbm_bytes_per_launch"), d.get("cg_pass_hbm_bytes_per_launch"))
                 except Exception:  # noqa: BLE001
                     pass
     return best
@@ -481,6 +482,10 @@ def run_config34(args, rt, cfg_id):
         "cg_iteration": {"path": args.cg_path, "link_angles": cg_bps == BYTES_PER_SITE_CG_ANGLES,
                          "bytes_per_site": cg_bps,
                          "achieved_GBps_per_gpu": round(cg_bps * V * it_per_s / 1e9, 1),
+                         "frac_of_peak": round(cg_bps * V * it_per_s / 1e9 / HBM_PEAK_GBPS, 4),
+                         # counter bytes of the pass kernel (one launch = one iteration), same PMC file
+                         "traffic": tr[2] if tr and len(tr) > 2 else None,
+                         "traffic_bytes_per_site": round(tr[2] / V, 2) if tr and len(tr) > 2 and tr[2] else None,
                          "reference_sequence_bytes_per_site": 576},
         "weak": weak,
     })

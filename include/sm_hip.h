@@ -111,7 +111,11 @@ int sm_create_hosted(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard,
 int sm_create_loopback(sm_ctx **out, int Nx, int Nt_global, int device, const void *unique_id);
 int sm_destroy(sm_ctx *ctx);
 /* Launch on a caller stream (a hipStream_t, e.g. torch's current stream);
- * NULL restores the context's own stream. */
+ * NULL restores the context's own stream. Synchronises the previous stream
+ * first: each of a sharded context's two RCCL communicators is driven from
+ * one stream at a time (the main one from this stream, the second from the
+ * context's private comm stream), so no communicator's operations are ever
+ * in flight on two streams. */
 int sm_set_stream(sm_ctx *ctx, void *hip_stream);
 int sm_synchronize(sm_ctx *ctx);
 /* Launch-geometry knobs of the stencil kernels (tuning / A-B benchmarks):
@@ -145,7 +149,9 @@ int sm_tune_cg_geometry(sm_ctx *ctx, int waves_per_block, int xchunk);
  * links are exp(i theta), src/gauge_conf.cpp); otherwise the pass reads the
  * complex links. D, D^dag and the force always use the stored links bitwise.
  * on: 1 / 0 enable / disable, < 0 keep; *in_use (may be NULL): 1 if the last
- * sm_cg_begin / sm_cg set the angles up for the active path. */
+ * sm_cg_begin / sm_cg set the angles up for the active path. On t-shards the
+ * choice is collective at the next solve: the angles are used only if every
+ * shard asks for them (one all-reduce, which every shard joins). */
 int sm_cg_link_angles(sm_ctx *ctx, int on, int *in_use);
 /* Streaming-bandwidth ceiling on the ctx stream (measured roofline reference):
  * out = a + b (two_reads = 1: the stencil's 2-read/1-write byte mix) or

@@ -69,11 +69,17 @@ def main():
             e["hbm_GBps"] = (rd + wr) / avg_ns[k]
         kernels[k] = e
     dslash = [k for k in kernels if "dslash_kernel" in k and "<0, 0>" in k]
+    # the CG pass behind bench.py's value: one shard, x rows, fused multiply-
+    # adds, in-kernel scalars off, link angles, ticketed tail (sm_cgra.hip)
+    cgk = [k for k in kernels if "cg_ra_kernel<0, 1, 2, 0, 1, 1>" in k]
     out = {"Nx": a.nx, "Nt": a.nt, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes",
            "correction": "reads = 2 x FETCH_SIZE KiB (gfx950), writes = WRITE_SIZE KiB",
            "algorithmic_bytes_per_launch": 96 * sites,
            "dslash_kernel": dslash[0] if dslash else None,
            "hbm_bytes_per_launch": kernels[dslash[0]]["hbm_bytes"] if dslash else None,
+           "cg_pass_kernel": cgk[0] if cgk else None,
+           "cg_pass_algorithmic_bytes_per_launch": 144 * sites,
+           "cg_pass_hbm_bytes_per_launch": kernels[cgk[0]]["hbm_bytes"] if cgk else None,
            "kernels": kernels}
     with open(os.path.join(pdir, f"{tag}_dslash_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
