@@ -144,6 +144,43 @@ def make_large(name, nx, nt, sigma, m0, ranks, workdir, mpirun):
     return meta
 
 
+def large_spread(name, ranks, workdir_root, mpirun):
+    """The reference's own reduction-order spread for a large fixture: rerun
+    its fixture mode on the same inputs with another MPI decomposition (the
+    operators are decomposition-invariant bitwise; the dots sum in another
+    order) and record the iteration counts and ||x_a - x_b|| / ||x_a||. This
+    is the band inside which two correct fp64 CG solves of this system differ
+    from each other by rounding order alone."""
+    nx, nt = next((e[1], e[2]) for e in LARGE if e[0] == name)
+    base = os.path.join(workdir_root, name)
+    rx, rt = ranks
+    alt = os.path.join(workdir_root, f"{name}_{rx}x{rt}")
+    os.makedirs(alt, exist_ok=True)
+    for k in ("U", "psi", "chi"):
+        dst = os.path.join(alt, k + ".bin")
+        if not os.path.exists(dst):
+            os.symlink(os.path.join(base, k + ".bin"), dst)
+    mpath = os.path.join(alt, "meta.json")
+    if os.path.exists(mpath) and os.path.getsize(mpath) > 0:
+        with open(mpath) as f:
+            meta2 = json.load(f)
+    else:
+        exe = os.path.join(REF_DIR, f"sm_ref_{nx}x{nt}")
+        with open(os.path.join(base, "meta.json")) as f:
+            m0 = json.load(f)["m0"]
+        cmd = [exe, "fixture", alt, str(rx), str(rt), repr(m0), "1e-10", "10000"]
+        if rx * rt > 1:
+            cmd = [mpirun, "-n", str(rx * rt)] + cmd
+        meta2 = json.loads(run(cmd))
+        with open(mpath, "w") as f:
+            json.dump(meta2, f)
+    xa = np.fromfile(os.path.join(base, "ref_cgx.bin"), dtype=np.float64)
+    xb = np.fromfile(os.path.join(alt, "ref_cgx.bin"), dtype=np.float64)
+    return {"ranks_x": rx, "ranks_t": rt, "cg_iters": meta2["cg_iters"],
+            "cg_true_relres": meta2["cg_true_relres"],
+            "x_rel_to_fixture": float(np.linalg.norm(xa - xb) / np.linalg.norm(xa))}
+
+
 def make_jackknife():
     """Reference Jackknife_error(dat, 20) and mean(dat) (src/statistics.cpp)
     on seeded series, including lengths that are not multiples of the 20 bins
@@ -297,6 +334,9 @@ def main():
     ap.add_argument("--large", nargs="+", default=None, metavar="NAME",
                     help="(re)make only these summary fixtures (LARGE names): 1024^2 ~4 min on one core, "
                          "4096^2 ~70 min on one core, 8192^2 ~2-3 h on 2x2 ranks")
+    ap.add_argument("--spread", nargs=3, default=None, metavar=("NAME", "RX", "RT"),
+                    help="rerun a finished large fixture's reference solve on RX x RT ranks and record the "
+                         "reference's own decomposition spread in the manifest")
     ap.add_argument("--large-workdir", default="/tmp/sm_large",
                     help="parent of the per-fixture reference run directories (resumable)")
     ap.add_argument("--mpirun", default="/opt/conda/bin/mpirun")
@@ -307,6 +347,17 @@ def main():
                     help="run this many more independent reference HMC chains in parallel (~4 min) into hmc_stat_chains")
     ap.add_argument("--conf-only", action="store_true", help="regenerate only the SaveConf fixtures")
     args = ap.parse_args()
+    if args.spread:
+        name, rx, rt = args.spread[0], int(args.spread[1]), int(args.spread[2])
+        sp = large_spread(name, (rx, rt), args.large_workdir, args.mpirun)
+        path = os.path.join(HERE, "manifest.json")
+        with open(path) as f:
+            manifest = json.load(f)
+        manifest["large"][name].setdefault("reference_decomposition_spread", []).append(sp)
+        with open(path, "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+        print(name, json.dumps(sp), file=sys.stderr)
+        return
     if args.large:
         todo = [e for e in LARGE if e[0] in args.large]
         if len(todo) != len(args.large):
