@@ -327,6 +327,47 @@ def run_eocg(name, result_path, dist, rank, world):
     dist.destroy_process_group()
 
 
+def run_angles(name, result_path, dist, rank, world):
+    """mode "angles": the link-angle choice of the recompute-Ad CG is
+    collective on t-shards. name = gen:<Nx>x<Nt>:<sigma>:<m0>:<wish>
+    where wish is one 0/1 digit per rank for sm_cg_link_angles. Each rank
+    solves twice (the second solve re-decides after U is re-uploaded) and
+    reports (converged, iterations, in_use) per solve; nothing may hang."""
+    import schwingermodel_amd as sm
+    from schwingermodel_amd import dist as smd
+    _, dims, sigma, m0s, wish = name.split(":")
+    Nx, Nt = (int(v) for v in dims.split("x"))
+    sigma, m0 = float(sigma), float(m0s)
+    S = Nx * Nt
+    g = {k: np.empty(4 * S) for k in ("U", "psi")}
+    sm.lib.sm_fill_gauge(4321, sigma, Nt, 0, Nx, 0, Nt, g["U"].ctypes.data, g["U"][2 * S:].ctypes.data)
+    sm.lib.sm_fill_spinor(5678, Nt, 0, Nx, 0, Nt, g["psi"].ctypes.data, g["psi"][2 * S:].ctypes.data)
+    t0, Wt = ctypes.c_int(), ctypes.c_int()
+    sm.check(sm.lib.sm_shard_plan(Nt, world, rank, ctypes.byref(t0), ctypes.byref(Wt)))
+    U, p = (shard_field(g[k], Nx, Nt, t0.value, Wt.value) for k in ("U", "psi"))
+    P_ = lambda x: ctypes.c_void_p(x.ctypes.data)  # noqa: E731
+    ctx, tr = smd.create_hosted_context(Nx, Nt, device=int(os.environ.get("SM_DEVICE", "0")))
+    sm.check(sm.lib.sm_tune_cg(ctx, 5, 0))
+    sm.check(sm.lib.sm_cg_link_angles(ctx, int(wish[rank]), None))
+    out = []
+    for _ in range(2):
+        sm.check(sm.lib.sm_upload_gauge(ctx, P_(U[0]), P_(U[1])))
+        x0, x1 = np.empty(Nx * Wt.value, complex), np.empty(Nx * Wt.value, complex)
+        res = sm.CGResult()
+        sm.check(sm.lib.sm_cg(ctx, P_(p[0]), P_(p[1]), P_(x0), P_(x1), m0, 1e-10, 10000, ctypes.byref(res)))
+        used = ctypes.c_int(-1)
+        sm.check(sm.lib.sm_cg_link_angles(ctx, -1, ctypes.byref(used)))
+        out.append([int(res.converged), int(res.iterations), int(used.value)])
+    sm.lib.sm_destroy(ctx)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, out)
+    if rank == 0:
+        with open(result_path, "w") as f:
+            json.dump({"world": world, "solves": gathered}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def fill_block(sm, Nx, Nt, t0, Wt, sigma, seeds=(4321, 5678, 91011), nthreads=8):
     """U, psi, chi of the t-block [t0, t0+Wt) of the global synthetic fields
     (counter-based, row-separable: row blocks are filled in threads)."""
@@ -472,6 +513,8 @@ def main():
         return run_eo(name, result_path, dist, rank, world)
     if mode == "eocg":
         return run_eocg(name, result_path, dist, rank, world)
+    if mode == "angles":
+        return run_angles(name, result_path, dist, rank, world)
     if mode == "big":
         return run_big(name, result_path, dist, rank, world)
     from conftest import bits_equal, load_fixture

@@ -144,3 +144,18 @@ def test_sharded_even_odd_cg_schedules(tmp_path, red, max_iter):
     if max_iter < 10000:
         assert conv1 == 0 and it1 == max_iter, rep
     assert rep["x_rel"] <= 1e-10, rep
+
+
+@pytest.mark.parametrize("wish,expect", [("11", 1), ("10", 0), ("01", 0), ("00", 0)])
+def test_link_angle_choice_is_collective(tmp_path, wish, expect):
+    """sm_cg_link_angles is per context, but on t-shards the recompute-Ad CG
+    decides collectively (one all-reduce that every shard joins): the angles
+    are used only if every shard asks for them, so ranks that disagree take
+    the same path instead of one of them skipping a collective the others
+    enter. Two solves per rank (U re-uploaded in between, which
+    re-opens the decision): all converge in the same count, none hangs."""
+    rep = run_world("angles", f"gen:64x512:0.3246:-0.05:{wish}", 2, tmp_path, timeout=120)
+    solves = [s for r in rep["solves"] for s in r]
+    assert all(conv == 1 for conv, it, used in solves), rep
+    assert len({it for conv, it, used in solves}) == 1, rep
+    assert all(used == expect for conv, it, used in solves), rep
