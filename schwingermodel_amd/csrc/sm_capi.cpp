@@ -431,6 +431,7 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //   edge_xchunk=N       t-shards: rows per edge block (0: the interior's)
 //   ra_red_max_blocks=N one shard: redundant scalars up to N blocks
 //   fold=0|1|2          recompute-Ad pass arithmetic (2: fused multiply-adds)
+//   rev=0               recompute-Ad pass: odd passes march forward too
 //   link_angles=0|1     recompute-Ad pass reads the links as angles
 //   bt=64|128|256       Dirac apply t-columns per block
 //   eo_fused=0, eo_cg_td=0, eo_cg_folded=1   even-odd operator / CG forms
@@ -469,6 +470,8 @@ static int apply_test_opts(sm_ctx *c) {
             c->cg_ra_red_max_blocks = iv;
         } else if (k == "fold") {
             c->racfg.fold = iv;
+        } else if (k == "rev") {
+            c->racfg.rev_odd = iv;
         } else if (k == "link_angles") {
             c->link_angles = iv ? 1 : 0;
         } else if (k == "bt") {

@@ -196,7 +196,7 @@ void launch_cg_ra_flush_sums(hipStream_t s, CGScalars *sc, long pass) {
     hipLaunchKernelGGL(cg_ra_flush_sums_kernel, dim3(1), dim3(1), 0, s, sc, pass);
 }
 
-template <int SH, int XP, int FOLD, int RED = 0, int UC = 0, int TK = 0>
+template <int SH, int XP, int FOLD, int RED = 0, int UC = 0, int TK = 0, int REV = 0>
 __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
     __shared__ double2 sh[4];
     extern __shared__ double2 rlds[];  // r_j ring: 3 slots x 2 planes x blockDim (dynamic: sized by waves per block)
@@ -243,9 +243,14 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
     int tb, tbr, xc;
     {
         int w = blockIdx.x;
+        const int n = a.tbn * a.XB;
         if (a.remap) {  // consecutive ids of one XCD take x-adjacent tiles (L2 reuse of halo rows)
-            const int n = a.tbn * a.XB, q = n >> 3, rr = n & 7, xcd = w & 7;
-            w = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (w >> 3);
+            const int q = n >> 3, rr = n & 7, xcd = w & 7;
+            const int len = xcd < rr ? q + 1 : q;
+            const int i = REV ? len - 1 - (w >> 3) : (w >> 3);  // REV: the XCD's tiles in reverse order
+            w = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + i;
+        } else if (REV) {
+            w = n - 1 - w;
         }
         tbr = w % a.tbn;
         tb = a.tb0 + tbr;
@@ -276,27 +281,36 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
         }();
         const int cx = c < 0 ? 0 : (c >= Wt ? Wt - 1 : c);
         auto wrap = [Nx](int x) { int w = x % Nx; return w < 0 ? w + Nx : w; };
+        // REV marches the chunk from its last row to its first: virtual row v
+        // (the march order, x0 - 6 .. xe - 1 as forward) is physical row
+        // x0 + xe - 1 - v. The x-hops then swap roles (the physical x + 1
+        // neighbour is the row BEHIND in the march), and U_x is loaded one
+        // physical row up (U_x(X - 1) for virtual row v), so each stage's two
+        // x-links are again the current and the previous register row.
+        auto phys = [x0, xe](int v) { return REV ? x0 + xe - 1 - v : v; };
         // d_{j-1}: rows x0-4 .. xe+3; U: x0-4 .. xe+2; d_{j-2}: x0-2 .. xe+1; x: owned rows
         auto ld1 = [&](int xr, Sp &d) {
-            const double2 *p = S1.p + (long)wrap(min(xr, xe + 3)) * S1.xs;
+            const double2 *p = S1.p + (long)wrap(phys(min(xr, xe + 3))) * S1.xs;
             d.a = p[0];
             d.b = p[S1.ps];
         };
         auto ldu = [&](int xr, LU &ut, LU &ux) {
-            const LU *p = SU.p + (long)wrap(min(xr, xe + 2)) * SU.xs;
+            const int X = phys(min(xr, xe + 2));
+            const LU *p = SU.p + (long)wrap(X) * SU.xs;
             ut = p[0];
-            ux = p[SU.ps];
+            if (REV) ux = SU.p[(long)wrap(X - 1) * SU.xs + SU.ps];
+            else ux = p[SU.ps];
         };
         auto cvu = [](LU v) -> double2 {
             if constexpr (UC != 0) return u_of(v);
             else return v;
         };
         auto ld2 = [&](int xr, Sp &q, Sp &xv) {
-            const double2 *p = S2.p + (long)wrap(min(max(xr, x0 - 2), xe + 1)) * S2.xs;
+            const double2 *p = S2.p + (long)wrap(phys(min(max(xr, x0 - 2), xe + 1))) * S2.xs;
             q.a = p[0];
             q.b = p[S2.ps];
-            if (XP && (xr & 1) == a.xpar) {  // wave-uniform: only the rows this pass updates
-                const long n = (long)wrap(min(max(xr, x0), xe - 1)) * Wt + cx;
+            if (XP && (phys(xr) & 1) == a.xpar) {  // wave-uniform: only the rows this pass updates
+                const long n = (long)wrap(phys(min(max(xr, x0), xe - 1))) * Wt + cx;
                 xv.a = a.x[n];
                 xv.b = a.x[n + a.V];
             }
@@ -332,10 +346,12 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
             ld1(y + 5, Ld);
             ldu(y + 4, Lut, Lux);
             __builtin_amdgcn_sched_barrier(0);  // keep the next rows' loads issued here
-            const Sp P3 = ra_site<FOLD, 1>(mass, sr0, sl0, D3, D2, D4, Ut3, Ux3, Ux2);  // S1: T'(y+3)
+            const Sp P3 = REV ? ra_site<FOLD, 1>(mass, sr0, sl0, D3, D4, D2, Ut3, Ux2, Ux3)
+                              : ra_site<FOLD, 1>(mass, sr0, sl0, D3, D2, D4, Ut3, Ux3, Ux2);  // S1: T'(y+3)
             Sp J2 = zs, Q2 = zs;
             if constexpr ((M & 1) != 0) {
-                const Sp A = ra_site<FOLD, 0>(mass, sr0, sl0, P2, P1, P3, Ut2, Ux2, Ux1);  // S2: Ad_{j-1}(y+2)
+                const Sp A = REV ? ra_site<FOLD, 0>(mass, sr0, sl0, P2, P3, P1, Ut2, Ux1, Ux2)
+                                 : ra_site<FOLD, 0>(mass, sr0, sl0, P2, P1, P3, Ut2, Ux2, Ux1);  // S2: Ad_{j-1}(y+2)
                 // S3: r_j, d_j at row y+2
                 const int xr = y + 2;
                 const Sp Q = Mq, X = Mx;
@@ -347,17 +363,18 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
                 J2.a = cfma<FOLD>(R2.a, D2.a, beta);
                 J2.b = cfma<FOLD>(R2.b, D2.b, beta);
                 if (xr >= x0 && xr < xe && own) {
-                    const long n = (long)xr * Wt + c;
+                    const int Xr = phys(xr);
+                    const long n = (long)Xr * Wt + c;
                     st_nt(a.dn + n, J2.a);
                     st_nt(a.dn + n + a.V, J2.b);
                     if (SH && a.fsend) {  // fused face pack ([col][plane][x], lo: columns 0..3, hi: Wt-4..Wt-1)
                         const int fcol = c < RH ? c : (c >= Wt - RH ? c - (Wt - RH) + RH : -1);
                         if (fcol >= 0) {
-                            a.fsend[(long)(2 * fcol) * Nx + xr] = J2.a;
-                            a.fsend[(long)(2 * fcol + 1) * Nx + xr] = J2.b;
+                            a.fsend[(long)(2 * fcol) * Nx + Xr] = J2.a;
+                            a.fsend[(long)(2 * fcol + 1) * Nx + Xr] = J2.b;
                         }
                     }
-                    if (XP && (xr & 1) == a.xpar) {  // x_j = (x_{j-2} + alpha_{j-2} d_{j-2}) + alpha_{j-1} d_{j-1}
+                    if (XP && (Xr & 1) == a.xpar) {  // x_j = (x_{j-2} + alpha_{j-2} d_{j-2}) + alpha_{j-1} d_{j-1}
                         st_nt(a.x + n, cfma<FOLD>(cfma<FOLD>(X.a, alpha2, Q.a), alpha, D2.a));
                         st_nt(a.x + n + a.V, cfma<FOLD>(cfma<FOLD>(X.b, alpha2, Q.b), alpha, D2.b));
                     }
@@ -368,9 +385,12 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
                 rlds[(2 * s_w + 1) * blockDim.x + threadIdx.x] = R2.b;
             }
             ld2(y + 3, Mq, Mx);  // consumed above: issued now, used next iteration
-            if constexpr ((M & 2) != 0) Q2 = ra_site<FOLD, 1>(mass, sr0, sl0, J1, J0, J2, Ut1, Ux1, Ux0);  // S4: T(y+1)
+            if constexpr ((M & 2) != 0)  // S4: T(y+1)
+                Q2 = REV ? ra_site<FOLD, 1>(mass, sr0, sl0, J1, J2, J0, Ut1, Ux0, Ux1)
+                         : ra_site<FOLD, 1>(mass, sr0, sl0, J1, J0, J2, Ut1, Ux1, Ux0);
             if constexpr ((M & 4) != 0) {
-                const Sp o = ra_site<FOLD, 0>(mass, sr0, sl0, Q1, Q0, Q2, Ut0, Ux0, Uxm);  // S5: Ad_j(y)
+                const Sp o = REV ? ra_site<FOLD, 0>(mass, sr0, sl0, Q1, Q2, Q0, Ut0, Uxm, Ux0)
+                                 : ra_site<FOLD, 0>(mass, sr0, sl0, Q1, Q0, Q2, Ut0, Ux0, Uxm);  // S5: Ad_j(y)
                 if (own) {
                     const Sp R0 = Sp{rlds[(2 * s_r) * blockDim.x + threadIdx.x], rlds[(2 * s_r + 1) * blockDim.x + threadIdx.x]};
                     acc_dA = cfma<FOLD>(acc_dA, J0.a, cconj(o.a));  // dot(d, Ad)
@@ -486,11 +506,19 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
     // (tools/ab_fold.sh, ABBA: 0.513-0.517 vs 0.519-0.520 ms burst, 0.548-0.554
     // vs 0.552-0.557 sustained)
     c.fold = 2;
+    c.rev_odd = 1;
     return c;
 }
 
 template <int SH, int RED, int UC, int F>
-static void ra_go(int xp, int tk, dim3 grid, dim3 block, size_t lds, hipStream_t s, const RAArgs &a) {
+static void ra_go(int xp, int tk, dim3 grid, dim3 block, size_t lds, hipStream_t s, const RAArgs &a, int rev = 0) {
+    if constexpr (F == 2 && SH == 0 && RED == 0) {
+        if (tk && rev) {
+            if (xp) hipLaunchKernelGGL((cg_ra_kernel<SH, 1, F, RED, UC, 1, 1>), grid, block, lds, s, a);
+            else hipLaunchKernelGGL((cg_ra_kernel<SH, 0, F, RED, UC, 1, 1>), grid, block, lds, s, a);
+            return;
+        }
+    }
     if constexpr (F == 2) {
         if (tk) {
             if (xp) hipLaunchKernelGGL((cg_ra_kernel<SH, 1, F, RED, UC, 1>), grid, block, lds, s, a);
@@ -551,13 +579,18 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
         else ra_go<1, 2, 0, 2>(xp, tk, grid, block, lds, s, a);
         return;
     }
+    // one shard with the ticketed tail: odd passes march backwards over the
+    // tiles in reverse order, so a pass starts on the rows its predecessor
+    // touched last (still in the XCD's L2 / the Infinity Cache) instead of
+    // the ones it touched first
+    const int rev = !sh && tk && (pass & 1) && c.rev_odd;
     if (f == 2) {
         if (uc) {
             if (sh) ra_go<1, 0, 1, 2>(xp, tk, grid, block, lds, s, a);
-            else ra_go<0, 0, 1, 2>(xp, tk, grid, block, lds, s, a);
+            else ra_go<0, 0, 1, 2>(xp, tk, grid, block, lds, s, a, rev);
         } else {
             if (sh) ra_go<1, 0, 0, 2>(xp, tk, grid, block, lds, s, a);
-            else ra_go<0, 0, 0, 2>(xp, tk, grid, block, lds, s, a);
+            else ra_go<0, 0, 0, 2>(xp, tk, grid, block, lds, s, a, rev);
         }
     } else if (f == 1) {
         if (sh) ra_go<1, 0, 0, 1>(xp, 0, grid, block, lds, s, a);

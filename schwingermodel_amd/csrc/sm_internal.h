@@ -116,6 +116,7 @@ struct CGFusedCfg {
     int remap;
     int fold = 0;        // sm_cgra.hip: folded hopping-bracket arithmetic (dirac_bracket_folded)
     int wpb = 4;         // sm_cgra.hip: waves per block (1, 2, 4)
+    int rev_odd = 0;     // sm_cgra.hip: odd one-shard tail passes march backwards over reversed tiles
 };
 CGFusedCfg cg_fused_config(const Geometry &g);
 int cg_fused_blocks(const CGFusedCfg &c);
