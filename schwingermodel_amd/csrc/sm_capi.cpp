@@ -431,7 +431,9 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //   edge_xchunk=N       t-shards: rows per edge block (0: the interior's)
 //   ra_red_max_blocks=N one shard: redundant scalars up to N blocks
 //   fold=0|1|2          recompute-Ad pass arithmetic (2: fused multiply-adds)
-//   rev=0               recompute-Ad pass: odd passes march forward too
+//   rev=0|1|2           recompute-Ad pass march schedule (0 all forward; 1 odd
+//                       passes backward; 2, the default, x-adjacent chunks in
+//                       opposite directions and odd passes flipped)
 //   link_angles=0|1     recompute-Ad pass reads the links as angles
 //   bt=64|128|256       Dirac apply t-columns per block
 //   eo_fused=0, eo_cg_td=0, eo_cg_folded=1   even-odd operator / CG forms

@@ -88,6 +88,10 @@ struct RAArgs {
     unsigned *tick;
     int ntiles;
     double2 *gsum, *out3;
+    // one-shard tail passes (REV kernels): flip = this pass reverses the
+    // dispatch order of its tiles and the march direction; alt = x-adjacent
+    // chunks march in opposite directions
+    int flip, alt;
 };
 
 // U(1) link from its angle (UC): cos and sin of theta in [-pi, pi]
@@ -196,74 +200,12 @@ void launch_cg_ra_flush_sums(hipStream_t s, CGScalars *sc, long pass) {
     hipLaunchKernelGGL(cg_ra_flush_sums_kernel, dim3(1), dim3(1), 0, s, sc, pass);
 }
 
-template <int SH, int XP, int FOLD, int RED = 0, int UC = 0, int TK = 0, int REV = 0>
-__global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
-    __shared__ double2 sh[4];
-    extern __shared__ double2 rlds[];  // r_j ring: 3 slots x 2 planes x blockDim (dynamic: sized by waves per block)
-    CGScalars *sc = a.sc;
-    // Passes 0 and 1 take zero multipliers instead of branches: pass 0 has
-    // d_0 = r_0 (alpha = beta = 0), pass 1 has r_0 = d_0 (beta2 = 0). The
-    // products by zero leave every value unchanged up to the sign of an exact zero.
-    const double2 z2 = make_double2(0.0, 0.0);
-    const bool first = a.first != 0, rebuild = a.rebuild != 0;
-    double2 alpha, beta, alpha2, beta2;  // alpha_{j-1}, beta_{j-1}, alpha_{j-2}, beta_{j-2}
-    if (RED) {  // every block evaluates pass j-1's scalars itself (same sums, same order)
-        __shared__ double2 s_ab[4];
-        __shared__ int s_stop;
-        if (!first && RED == 2) {
-            if (threadIdx.x == 0) ra_scalars_from_sums(sc, a.pass, s_ab, &s_stop);
-        } else if (!first) {
-            const CGRed s = cg1_redundant(sc, a.prev, a.TBk * a.XB, a.pass, sh);
-            if (threadIdx.x == 0) {
-                s_ab[0] = s.alpha;
-                s_ab[1] = s.beta;
-                s_ab[2] = s.alpha2;
-                s_ab[3] = s.beta2;
-                s_stop = s.done;
-            }
-        } else if (threadIdx.x == 0) {
-            s_ab[0] = s_ab[1] = s_ab[2] = s_ab[3] = z2;
-            s_stop = 0;
-        }
-        __syncthreads();
-        if (s_stop) return;  // block-uniform
-        // block-uniform values: into scalar registers, as the sc loads of the
-        // non-redundant path are (not 16 VGPRs held across the march)
-        alpha = first ? z2 : uniform_d2(s_ab[0]);
-        beta = first ? z2 : uniform_d2(s_ab[1]);
-        alpha2 = uniform_d2(s_ab[2]);
-        beta2 = rebuild ? uniform_d2(s_ab[3]) : z2;
-    } else {
-        if (sc->done) return;  // grid-uniform: converged (or max_iter) in an earlier pass
-        alpha = first ? z2 : sc->alpha;
-        beta = first ? z2 : sc->beta;
-        alpha2 = sc->alpha2;
-        beta2 = rebuild ? sc->beta2 : z2;
-    }
-    int tb, tbr, xc;
-    {
-        int w = blockIdx.x;
-        const int n = a.tbn * a.XB;
-        if (a.remap) {  // consecutive ids of one XCD take x-adjacent tiles (L2 reuse of halo rows)
-            const int q = n >> 3, rr = n & 7, xcd = w & 7;
-            const int len = xcd < rr ? q + 1 : q;
-            const int i = REV ? len - 1 - (w >> 3) : (w >> 3);  // REV: the XCD's tiles in reverse order
-            w = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + i;
-        } else if (REV) {
-            w = n - 1 - w;
-        }
-        tbr = w % a.tbn;
-        tb = a.tb0 + tbr;
-        if (tb >= a.TBk) tb -= a.TBk;  // edge block-columns TBk-1 and 0 in one launch
-        xc = w / a.tbn;
-    }
-    const int lane = threadIdx.x & 63;
-    const int g = tb * a.wpb + (threadIdx.x >> 6);
-    const int x0 = xc * a.xchunk;
-    const int xe = min(a.Nx, x0 + a.xchunk);
-    double2 acc_dA = make_double2(0.0, 0.0), acc_rA = make_double2(0.0, 0.0);
-    double2 acc_n = make_double2(0.0, 0.0);  // (|r|^2, |Ad|^2)
-    if (g < a.NWT && x0 < xe) {
+// The row march of one tile (the kernel's body; see the header). REV = 1
+// marches the chunk from its last row to its first (ra_march_dir below).
+template <int SH, int XP, int FOLD, int UC, int REV>
+__device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x0, int xe, double2 alpha,
+                                         double2 beta, double2 alpha2, double2 beta2, double2 *rlds,
+                                         double2 &acc_dA, double2 &acc_rA, double2 &acc_n) {
         const int Nx = a.Nx, Wt = a.Wt;
         const int c = g * RW - RH + lane;
         const bool own = lane >= RH && lane < RW + RH && c < Wt;
@@ -432,6 +374,84 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
         }
         for (; y < xe; ++y) step(y, std::integral_constant<int, 7>());
     }
+
+template <int SH, int XP, int FOLD, int RED = 0, int UC = 0, int TK = 0, int REV = 0>
+__global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
+    __shared__ double2 sh[4];
+    extern __shared__ double2 rlds[];  // r_j ring: 3 slots x 2 planes x blockDim (dynamic: sized by waves per block)
+    CGScalars *sc = a.sc;
+    // Passes 0 and 1 take zero multipliers instead of branches: pass 0 has
+    // d_0 = r_0 (alpha = beta = 0), pass 1 has r_0 = d_0 (beta2 = 0). The
+    // products by zero leave every value unchanged up to the sign of an exact zero.
+    const double2 z2 = make_double2(0.0, 0.0);
+    const bool first = a.first != 0, rebuild = a.rebuild != 0;
+    double2 alpha, beta, alpha2, beta2;  // alpha_{j-1}, beta_{j-1}, alpha_{j-2}, beta_{j-2}
+    if (RED) {  // every block evaluates pass j-1's scalars itself (same sums, same order)
+        __shared__ double2 s_ab[4];
+        __shared__ int s_stop;
+        if (!first && RED == 2) {
+            if (threadIdx.x == 0) ra_scalars_from_sums(sc, a.pass, s_ab, &s_stop);
+        } else if (!first) {
+            const CGRed s = cg1_redundant(sc, a.prev, a.TBk * a.XB, a.pass, sh);
+            if (threadIdx.x == 0) {
+                s_ab[0] = s.alpha;
+                s_ab[1] = s.beta;
+                s_ab[2] = s.alpha2;
+                s_ab[3] = s.beta2;
+                s_stop = s.done;
+            }
+        } else if (threadIdx.x == 0) {
+            s_ab[0] = s_ab[1] = s_ab[2] = s_ab[3] = z2;
+            s_stop = 0;
+        }
+        __syncthreads();
+        if (s_stop) return;  // block-uniform
+        // block-uniform values: into scalar registers, as the sc loads of the
+        // non-redundant path are (not 16 VGPRs held across the march)
+        alpha = first ? z2 : uniform_d2(s_ab[0]);
+        beta = first ? z2 : uniform_d2(s_ab[1]);
+        alpha2 = uniform_d2(s_ab[2]);
+        beta2 = rebuild ? uniform_d2(s_ab[3]) : z2;
+    } else {
+        if (sc->done) return;  // grid-uniform: converged (or max_iter) in an earlier pass
+        alpha = first ? z2 : sc->alpha;
+        beta = first ? z2 : sc->beta;
+        alpha2 = sc->alpha2;
+        beta2 = rebuild ? sc->beta2 : z2;
+    }
+    int tb, tbr, xc;
+    {
+        int w = blockIdx.x;
+        const int n = a.tbn * a.XB;
+        if (a.remap) {  // consecutive ids of one XCD take t-adjacent tiles of its x-chunks (L2 reuse of halo columns)
+            const int q = n >> 3, rr = n & 7, xcd = w & 7;
+            const int len = xcd < rr ? q + 1 : q;
+            const int i = a.flip ? len - 1 - (w >> 3) : (w >> 3);  // flip: the XCD's tiles in reverse order
+            w = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + i;
+        } else if (a.flip) {
+            w = n - 1 - w;
+        }
+        tbr = w % a.tbn;
+        xc = w / a.tbn;
+        tb = a.tb0 + tbr;
+        if (tb >= a.TBk) tb -= a.TBk;  // edge block-columns TBk-1 and 0 in one launch
+    }
+    const int lane = threadIdx.x & 63;
+    const int g = tb * a.wpb + (threadIdx.x >> 6);
+    const int x0 = xc * a.xchunk;
+    const int xe = min(a.Nx, x0 + a.xchunk);
+    double2 acc_dA = make_double2(0.0, 0.0), acc_rA = make_double2(0.0, 0.0);
+    double2 acc_n = make_double2(0.0, 0.0);  // (|r|^2, |Ad|^2)
+    if (g < a.NWT && x0 < xe) {
+        // REV 0 / 1: every tile forward / backward; REV 2: per tile, backward
+        // iff (x-chunk parity & alt) ^ flip, so x-adjacent chunks march
+        // towards their shared boundary rows at the same time (alt = 1)
+        const bool back = REV == 1 || (REV == 2 && (((xc & a.alt) ^ a.flip) & 1));
+        if (REV != 0 && back)
+            ra_march<SH, XP, FOLD, UC, 1>(a, g, lane, x0, xe, alpha, beta, alpha2, beta2, rlds, acc_dA, acc_rA, acc_n);
+        else if (REV != 1)
+            ra_march<SH, XP, FOLD, UC, 0>(a, g, lane, x0, xe, alpha, beta, alpha2, beta2, rlds, acc_dA, acc_rA, acc_n);
+    }
     const double2 s0 = block_sum(acc_dA, sh);
     __syncthreads();
     const double2 s1 = block_sum(acc_rA, sh);
@@ -506,16 +526,21 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
     // (tools/ab_fold.sh, ABBA: 0.513-0.517 vs 0.519-0.520 ms burst, 0.548-0.554
     // vs 0.552-0.557 sustained)
     c.fold = 2;
-    c.rev_odd = 1;
+    c.rev_odd = 2;
     return c;
 }
 
 template <int SH, int RED, int UC, int F>
 static void ra_go(int xp, int tk, dim3 grid, dim3 block, size_t lds, hipStream_t s, const RAArgs &a, int rev = 0) {
     if constexpr (F == 2 && SH == 0 && RED == 0) {
-        if (tk && rev) {
+        if (tk && rev == 1) {
             if (xp) hipLaunchKernelGGL((cg_ra_kernel<SH, 1, F, RED, UC, 1, 1>), grid, block, lds, s, a);
             else hipLaunchKernelGGL((cg_ra_kernel<SH, 0, F, RED, UC, 1, 1>), grid, block, lds, s, a);
+            return;
+        }
+        if (tk && rev == 2) {
+            if (xp) hipLaunchKernelGGL((cg_ra_kernel<SH, 1, F, RED, UC, 1, 2>), grid, block, lds, s, a);
+            else hipLaunchKernelGGL((cg_ra_kernel<SH, 0, F, RED, UC, 1, 2>), grid, block, lds, s, a);
             return;
         }
     }
@@ -558,6 +583,8 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
     a.ntiles = ntiles;
     a.gsum = gsum;
     a.out3 = out3;
+    a.flip = 0;
+    a.alt = 0;
     const dim3 grid(tbn * c.XB), block(64 * c.wpb);
     const size_t lds = sizeof(double2) * 6 * 64 * c.wpb;  // the r_j ring
     // x takes passes j-1 and j together, on the rows of parity j & 1: every
@@ -579,11 +606,24 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
         else ra_go<1, 2, 0, 2>(xp, tk, grid, block, lds, s, a);
         return;
     }
-    // one shard with the ticketed tail: odd passes march backwards over the
-    // tiles in reverse order, so a pass starts on the rows its predecessor
-    // touched last (still in the XCD's L2 / the Infinity Cache) instead of
-    // the ones it touched first
-    const int rev = !sh && tk && (pass & 1) && c.rev_odd;
+    // one shard with the ticketed tail: odd passes take the tiles in reverse
+    // order and flip the march direction, so a pass starts on the rows its
+    // predecessor touched last (still in the XCD's L2 / the Infinity Cache)
+    // instead of the ones it touched first. rev_odd 1: every tile of an odd
+    // pass marches backwards (REV 1 kernel); rev_odd 2: x-adjacent chunks
+    // also march in opposite directions, towards / away from their shared
+    // halo rows together (REV 2 kernel, both marches)
+    int rev = 0;
+    a.flip = 0;
+    a.alt = 0;
+    if (!sh && tk && f == 2 && c.rev_odd == 1 && (pass & 1)) {
+        rev = 1;
+        a.flip = 1;
+    } else if (!sh && tk && f == 2 && c.rev_odd == 2) {
+        rev = 2;
+        a.flip = (int)(pass & 1);
+        a.alt = 1;
+    }
     if (f == 2) {
         if (uc) {
             if (sh) ra_go<1, 0, 1, 2>(xp, tk, grid, block, lds, s, a);
