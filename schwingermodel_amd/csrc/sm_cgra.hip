@@ -503,15 +503,23 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
     // vs 1/40 0.146; the others unchanged. At 4096 columns chunk lengths that
     // are not powers of two are ~10 % slower (48 / 80 / 96 rows 0.538-0.541
     // against 0.488 for 32 and 64).
-    static const int kShapes[][4] = {  // Nx, Wt, waves per block, rows per block
-        {4096, 4096, 1, 64}, {4096, 2048, 1, 32}, {4096, 1024, 1, 40}, {4096, 512, 1, 48},
-        {8192, 8192, 4, 32}, {8192, 1024, 1, 32}, {2048, 2048, 1, 64},
+    // March schedule (one shard, ticketed tail; round 3, interleaved bench
+    // runs on one box): 1 = odd passes reversed, 2 = alternating x-chunks as
+    // well. 4096^2: 2090 / 2090 it/s for 2 against 2065 / 2061 for 1 and
+    // 2049 / 2044 all forward; 8192^2 (config 5, 4-wave blocks): 7.92-7.95 s
+    // for 1 against 8.24 s for 2 and 8.48 s all forward
+    // (profiles/r03_ij_march_schedule_ab.jsonl, r03_n_c5_march_schedule.jsonl).
+    c.rev_odd = 1;
+    static const int kShapes[][5] = {  // Nx, Wt, waves per block, rows per block, march schedule
+        {4096, 4096, 1, 64, 2}, {4096, 2048, 1, 32, 1}, {4096, 1024, 1, 40, 1}, {4096, 512, 1, 48, 1},
+        {8192, 8192, 4, 32, 1}, {8192, 1024, 1, 32, 1}, {2048, 2048, 1, 64, 1},
     };
     bool known = false;
     for (const auto &k : kShapes)
         if (k[0] == g.Nx && k[1] == g.Wt) {
             c.wpb = k[2];
             c.xchunk = k[3];
+            c.rev_odd = k[4];
             known = true;
         }
     if (!known && g.Nx >= 2048 && g.Wt >= 256) {
@@ -526,7 +534,6 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
     // (tools/ab_fold.sh, ABBA: 0.513-0.517 vs 0.519-0.520 ms burst, 0.548-0.554
     // vs 0.552-0.557 sustained)
     c.fold = 2;
-    c.rev_odd = 2;
     return c;
 }
 
