@@ -71,7 +71,7 @@ def main():
     dslash = [k for k in kernels if "dslash_kernel" in k and "<0, 0>" in k]
     # the CG pass behind bench.py's value: one shard, x rows, fused multiply-
     # adds, in-kernel scalars off, link angles, ticketed tail (sm_cgra.hip)
-    cgk = [k for k in kernels if "cg_ra_kernel<0, 1, 2, 0, 1, 1>" in k]
+    cgk = [k for k in kernels if "cg_ra_kernel<0, 1, 2, 0, 1, 1" in k]  # any march-schedule suffix
     out = {"Nx": a.nx, "Nt": a.nt, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes",
            "correction": "reads = 2 x FETCH_SIZE KiB (gfx950), writes = WRITE_SIZE KiB",
            "algorithmic_bytes_per_launch": 96 * sites,
