@@ -343,7 +343,13 @@ def max_over_ranks(rt, vals):
 
 
 def time_applies(rt, sh, m0, n):
-    """Dirac apply D, HIP events on the stream the kernel is launched on."""
+    """Dirac apply D, HIP events on the stream the kernel is launched on.
+    Returns a function that reads the time per apply: the events are read
+    after the CG timing, so the CG warmup passes queue right behind the
+    applies and the GPU never idles between the two timed phases (an idle
+    gap of a few ms before a solve sends the chip into a ~40-pass clock
+    transient, 10-25 % slower passes: tools/cg_transient.py,
+    profiles/r03_q_cg_transient.jsonl)."""
     import torch
     sm = sh.sm
     for _ in range(10):
@@ -354,8 +360,7 @@ def time_applies(rt, sh, m0, n):
     for _ in range(n):
         sm.check(sm.lib.sm_dirac_dev(sh.L.ctx, sh.p(sh.phi), sh.p(sh.out), m0, 0))
     e1.record(rt["stream"])
-    barrier(rt)
-    return e0.elapsed_time(e1) / 1e3 / n
+    return lambda: e0.elapsed_time(e1) / 1e3 / n
 
 
 def cg_bytes_per_site(sh, cg_path):
@@ -366,14 +371,23 @@ def cg_bytes_per_site(sh, cg_path):
     return BYTES_PER_SITE_CG_ANGLES if (cg_path == "recompute" and u.value) else BYTES_PER_SITE_CG[cg_path]
 
 
-def time_cg_steps(rt, sh, m0, cg_path, warmup, steps, link_angles_off=False):
-    """K CG iterations (tol = 0: never converges, the full work every step)
-    bracketed by a barrier + device synchronisation on both sides."""
-    import torch
+def begin_cg(sh, m0, cg_path, link_angles_off=False):
+    """sm_cg_begin of the timed solve (x0 = phi, r0, d0; the link angles are
+    built here, with a host read of their check): CG setup, not timed."""
     sm = sh.sm
     sm.check(sm.lib.sm_tune_cg(sh.L.ctx, CG_PATH_ID[cg_path], 0))
     sm.check(sm.lib.sm_cg_link_angles(sh.L.ctx, 0 if link_angles_off else -1, None))  # -1: the size default
     sm.check(sm.lib.sm_cg_begin(sh.L.ctx, sh.p(sh.phi), sh.p(sh.x), m0, 0.0))
+
+
+def time_cg_steps(rt, sh, m0, cg_path, warmup, steps, link_angles_off=False, begun=False):
+    """K CG iterations (tol = 0: never converges, the full work every step)
+    bracketed by a barrier + device synchronisation on both sides, after W
+    untimed warmup iterations."""
+    import torch
+    sm = sh.sm
+    if not begun:
+        begin_cg(sh, m0, cg_path, link_angles_off)
     sm.check(sm.lib.sm_cg_iterate(sh.L.ctx, warmup))
     barrier(rt)
     c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -436,8 +450,10 @@ def run_config34(args, rt, cfg_id):
     Nx, Nt = args.nx or cfg["Nx"], args.nt or cfg["Nt"]
     m0, world, rank = cfg["m0"], rt["world"], rt["rank"]
     sh = Shard(rt, Nx, Nt, cfg["sigma"])
-    apply_s = time_applies(rt, sh, m0, args.applies)
-    t_cg, cg_bps = time_cg_steps(rt, sh, m0, args.cg_path, args.warmup, args.steps, args.no_link_angles)
+    begin_cg(sh, m0, args.cg_path, args.no_link_angles)
+    apply_time = time_applies(rt, sh, m0, args.applies)
+    t_cg, cg_bps = time_cg_steps(rt, sh, m0, args.cg_path, args.warmup, args.steps, args.no_link_angles, begun=True)
+    apply_s = apply_time()
     t_cg, apply_s = max_over_ranks(rt, [t_cg, apply_s])
     V = sh.V
     sh.close()
