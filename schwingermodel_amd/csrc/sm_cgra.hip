@@ -201,179 +201,179 @@ void launch_cg_ra_flush_sums(hipStream_t s, CGScalars *sc, long pass) {
 }
 
 // The row march of one tile (the kernel's body; see the header). REV = 1
-// marches the chunk from its last row to its first (ra_march_dir below).
+// marches the chunk from its last row to its first (phys below).
 template <int SH, int XP, int FOLD, int UC, int REV>
 __device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x0, int xe, double2 alpha,
                                          double2 beta, double2 alpha2, double2 beta2, double2 *rlds,
                                          double2 &acc_dA, double2 &acc_rA, double2 &acc_n) {
-        const int Nx = a.Nx, Wt = a.Wt;
-        const int c = g * RW - RH + lane;
-        const bool own = lane >= RH && lane < RW + RH && c < Wt;
-        int tg = (a.t0 + c) % a.Ntg;
-        if (tg < 0) tg += a.Ntg;
-        const double sr0 = tg == a.Ntg - 1 ? -1.0 : 1.0;  // SignR[2n], include/dirac_operator.h:53-55
-        const double sl0 = tg == 0 ? -1.0 : 1.0;          // SignL[2n], :56-58
-        const double mass = a.mass;
-        const RSrc<double2> S1 = rsrc<SH>(a.d1, a.f1, c, a);
-        const RSrc<double2> S2 = rsrc<SH>(a.d2, a.f2, c, a);
-        using LU = std::conditional_t<UC != 0, double, double2>;  // a link as loaded: angle or complex
-        const RSrc<LU> SU = [&] {
-            if constexpr (UC != 0) return rsrc<SH>(a.Ua, a.fUa, c, a);
-            else return rsrc<SH>(a.U, a.fU, c, a);
-        }();
-        const int cx = c < 0 ? 0 : (c >= Wt ? Wt - 1 : c);
-        auto wrap = [Nx](int x) { int w = x % Nx; return w < 0 ? w + Nx : w; };
-        // REV marches the chunk from its last row to its first: virtual row v
-        // (the march order, x0 - 6 .. xe - 1 as forward) is physical row
-        // x0 + xe - 1 - v. The x-hops then swap roles (the physical x + 1
-        // neighbour is the row BEHIND in the march), and U_x is loaded one
-        // physical row up (U_x(X - 1) for virtual row v), so each stage's two
-        // x-links are again the current and the previous register row.
-        auto phys = [x0, xe](int v) { return REV ? x0 + xe - 1 - v : v; };
-        // d_{j-1}: rows x0-4 .. xe+3; U: x0-4 .. xe+2; d_{j-2}: x0-2 .. xe+1; x: owned rows
-        auto ld1 = [&](int xr, Sp &d) {
-            const double2 *p = S1.p + (long)wrap(phys(min(xr, xe + 3))) * S1.xs;
-            d.a = p[0];
-            d.b = p[S1.ps];
-        };
-        auto ldu = [&](int xr, LU &ut, LU &ux) {
-            const int X = phys(min(xr, xe + 2));
-            const LU *p = SU.p + (long)wrap(X) * SU.xs;
-            ut = p[0];
-            if (REV) ux = SU.p[(long)wrap(X - 1) * SU.xs + SU.ps];
-            else ux = p[SU.ps];
-        };
-        auto cvu = [](LU v) -> double2 {
-            if constexpr (UC != 0) return u_of(v);
-            else return v;
-        };
-        auto ld2 = [&](int xr, Sp &q, Sp &xv) {
-            const double2 *p = S2.p + (long)wrap(phys(min(max(xr, x0 - 2), xe + 1))) * S2.xs;
-            q.a = p[0];
-            q.b = p[S2.ps];
-            if (XP && (phys(xr) & 1) == a.xpar) {  // wave-uniform: only the rows this pass updates
-                const long n = (long)wrap(phys(min(max(xr, x0), xe - 1))) * Wt + cx;
-                xv.a = a.x[n];
-                xv.b = a.x[n + a.V];
-            }
-        };
-        const double2 z = make_double2(0.0, 0.0);
-        const Sp zs = Sp{z, z};
-        // state at the top of iteration y (see the header)
-        Sp D2, D3, Ld;                                   // d_{j-1}(y+2), (y+3); in flight (y+4)
-        LU Lut, Lux;                                     // in flight U(y+3)
-        Sp Mq, Mx = zs;                                  // in flight d_{j-2}(y+2), x(y+2)
-        double2 Ut0 = z, Ut1 = z, Ut2, Ux0 = z, Ux1 = z, Ux2, Uxm = z;  // U_t(y..y+2), U_x(y-1..y+2)
-        Sp P1 = zs, P2 = zs;                             // T'(y+1), T'(y+2)
-        Sp J0 = zs, J1 = zs;                             // d_j at rows y, y+1
-        Sp Q0 = zs, Q1 = zs;                             // T(y-1), T(y)
-        const int y0 = x0 - 6;
-        ld1(y0 + 2, D2);
-        ld1(y0 + 3, D3);
-        {
-            LU t2, x2;
-            ldu(y0 + 2, t2, x2);
-            Ut2 = cvu(t2);
-            Ux2 = cvu(x2);
+    const int Nx = a.Nx, Wt = a.Wt;
+    const int c = g * RW - RH + lane;
+    const bool own = lane >= RH && lane < RW + RH && c < Wt;
+    int tg = (a.t0 + c) % a.Ntg;
+    if (tg < 0) tg += a.Ntg;
+    const double sr0 = tg == a.Ntg - 1 ? -1.0 : 1.0;  // SignR[2n], include/dirac_operator.h:53-55
+    const double sl0 = tg == 0 ? -1.0 : 1.0;          // SignL[2n], :56-58
+    const double mass = a.mass;
+    const RSrc<double2> S1 = rsrc<SH>(a.d1, a.f1, c, a);
+    const RSrc<double2> S2 = rsrc<SH>(a.d2, a.f2, c, a);
+    using LU = std::conditional_t<UC != 0, double, double2>;  // a link as loaded: angle or complex
+    const RSrc<LU> SU = [&] {
+        if constexpr (UC != 0) return rsrc<SH>(a.Ua, a.fUa, c, a);
+        else return rsrc<SH>(a.U, a.fU, c, a);
+    }();
+    const int cx = c < 0 ? 0 : (c >= Wt ? Wt - 1 : c);
+    auto wrap = [Nx](int x) { int w = x % Nx; return w < 0 ? w + Nx : w; };
+    // REV marches the chunk from its last row to its first: virtual row v
+    // (the march order, x0 - 6 .. xe - 1 as forward) is physical row
+    // x0 + xe - 1 - v. The x-hops then swap roles (the physical x + 1
+    // neighbour is the row BEHIND in the march), and U_x is loaded one
+    // physical row up (U_x(X - 1) for virtual row v), so each stage's two
+    // x-links are again the current and the previous register row.
+    auto phys = [x0, xe](int v) { return REV ? x0 + xe - 1 - v : v; };
+    // d_{j-1}: rows x0-4 .. xe+3; U: x0-4 .. xe+2; d_{j-2}: x0-2 .. xe+1; x: owned rows
+    auto ld1 = [&](int xr, Sp &d) {
+        const double2 *p = S1.p + (long)wrap(phys(min(xr, xe + 3))) * S1.xs;
+        d.a = p[0];
+        d.b = p[S1.ps];
+    };
+    auto ldu = [&](int xr, LU &ut, LU &ux) {
+        const int X = phys(min(xr, xe + 2));
+        const LU *p = SU.p + (long)wrap(X) * SU.xs;
+        ut = p[0];
+        if (REV) ux = SU.p[(long)wrap(X - 1) * SU.xs + SU.ps];
+        else ux = p[SU.ps];
+    };
+    auto cvu = [](LU v) -> double2 {
+        if constexpr (UC != 0) return u_of(v);
+        else return v;
+    };
+    auto ld2 = [&](int xr, Sp &q, Sp &xv) {
+        const double2 *p = S2.p + (long)wrap(phys(min(max(xr, x0 - 2), xe + 1))) * S2.xs;
+        q.a = p[0];
+        q.b = p[S2.ps];
+        if (XP && (phys(xr) & 1) == a.xpar) {  // wave-uniform: only the rows this pass updates
+            const long n = (long)wrap(phys(min(max(xr, x0), xe - 1))) * Wt + cx;
+            xv.a = a.x[n];
+            xv.b = a.x[n + a.V];
         }
-        ld1(y0 + 4, Ld);
-        ldu(y0 + 3, Lut, Lux);
-        ld2(y0 + 2, Mq, Mx);
-        int s_w = 2, s_r = 0;  // LDS ring slots of r_j rows y+2 (written) and y (read)
-        // stage mask M: bit 0 = S2 + S3, bit 1 = S4, bit 2 = S5 (S1 always)
-        auto step = [&](int y, auto mtag) {
-            constexpr int M = decltype(mtag)::value;
-            const Sp D4 = Ld;
-            const double2 Ut3 = cvu(Lut), Ux3 = cvu(Lux);
-            ld1(y + 5, Ld);
-            ldu(y + 4, Lut, Lux);
-            __builtin_amdgcn_sched_barrier(0);  // keep the next rows' loads issued here
-            const Sp P3 = REV ? ra_site<FOLD, 1>(mass, sr0, sl0, D3, D4, D2, Ut3, Ux2, Ux3)
-                              : ra_site<FOLD, 1>(mass, sr0, sl0, D3, D2, D4, Ut3, Ux3, Ux2);  // S1: T'(y+3)
-            Sp J2 = zs, Q2 = zs;
-            if constexpr ((M & 1) != 0) {
-                const Sp A = REV ? ra_site<FOLD, 0>(mass, sr0, sl0, P2, P3, P1, Ut2, Ux1, Ux2)
-                                 : ra_site<FOLD, 0>(mass, sr0, sl0, P2, P1, P3, Ut2, Ux2, Ux1);  // S2: Ad_{j-1}(y+2)
-                // S3: r_j, d_j at row y+2
-                const int xr = y + 2;
-                const Sp Q = Mq, X = Mx;
-                Sp rp, R2;
-                rp.a = cfms<FOLD>(D2.a, Q.a, beta2);
-                rp.b = cfms<FOLD>(D2.b, Q.b, beta2);
-                R2.a = cfms<FOLD>(rp.a, alpha, A.a);
-                R2.b = cfms<FOLD>(rp.b, alpha, A.b);
-                J2.a = cfma<FOLD>(R2.a, D2.a, beta);
-                J2.b = cfma<FOLD>(R2.b, D2.b, beta);
-                if (xr >= x0 && xr < xe && own) {
-                    const int Xr = phys(xr);
-                    const long n = (long)Xr * Wt + c;
-                    st_nt(a.dn + n, J2.a);
-                    st_nt(a.dn + n + a.V, J2.b);
-                    if (SH && a.fsend) {  // fused face pack ([col][plane][x], lo: columns 0..3, hi: Wt-4..Wt-1)
-                        const int fcol = c < RH ? c : (c >= Wt - RH ? c - (Wt - RH) + RH : -1);
-                        if (fcol >= 0) {
-                            a.fsend[(long)(2 * fcol) * Nx + Xr] = J2.a;
-                            a.fsend[(long)(2 * fcol + 1) * Nx + Xr] = J2.b;
-                        }
-                    }
-                    if (XP && (Xr & 1) == a.xpar) {  // x_j = (x_{j-2} + alpha_{j-2} d_{j-2}) + alpha_{j-1} d_{j-1}
-                        st_nt(a.x + n, cfma<FOLD>(cfma<FOLD>(X.a, alpha2, Q.a), alpha, D2.a));
-                        st_nt(a.x + n + a.V, cfma<FOLD>(cfma<FOLD>(X.b, alpha2, Q.b), alpha, D2.b));
-                    }
-                    acc_n.x = nacc<FOLD>(acc_n.x, R2.a);  // Re dot(r, r), include/variables.h:185-188
-                    acc_n.x = nacc<FOLD>(acc_n.x, R2.b);
-                }
-                rlds[(2 * s_w) * blockDim.x + threadIdx.x] = R2.a;
-                rlds[(2 * s_w + 1) * blockDim.x + threadIdx.x] = R2.b;
-            }
-            ld2(y + 3, Mq, Mx);  // consumed above: issued now, used next iteration
-            if constexpr ((M & 2) != 0)  // S4: T(y+1)
-                Q2 = REV ? ra_site<FOLD, 1>(mass, sr0, sl0, J1, J2, J0, Ut1, Ux0, Ux1)
-                         : ra_site<FOLD, 1>(mass, sr0, sl0, J1, J0, J2, Ut1, Ux1, Ux0);
-            if constexpr ((M & 4) != 0) {
-                const Sp o = REV ? ra_site<FOLD, 0>(mass, sr0, sl0, Q1, Q2, Q0, Ut0, Uxm, Ux0)
-                                 : ra_site<FOLD, 0>(mass, sr0, sl0, Q1, Q0, Q2, Ut0, Ux0, Uxm);  // S5: Ad_j(y)
-                if (own) {
-                    const Sp R0 = Sp{rlds[(2 * s_r) * blockDim.x + threadIdx.x], rlds[(2 * s_r + 1) * blockDim.x + threadIdx.x]};
-                    acc_dA = cfma<FOLD>(acc_dA, J0.a, cconj(o.a));  // dot(d, Ad)
-                    acc_dA = cfma<FOLD>(acc_dA, J0.b, cconj(o.b));
-                    acc_rA = cfma<FOLD>(acc_rA, R0.a, cconj(o.a));  // dot(r, Ad)
-                    acc_rA = cfma<FOLD>(acc_rA, R0.b, cconj(o.b));
-                    acc_n.y = nacc<FOLD>(acc_n.y, o.a);            // |Ad|^2
-                    acc_n.y = nacc<FOLD>(acc_n.y, o.b);
-                }
-            }
-            D2 = D3;
-            D3 = D4;
-            Uxm = Ux0;
-            Ut0 = Ut1;
-            Ux0 = Ux1;
-            Ut1 = Ut2;
-            Ux1 = Ux2;
-            Ut2 = Ut3;
-            Ux2 = Ux3;
-            P1 = P2;
-            P2 = P3;
-            J0 = J1;
-            J1 = J2;
-            Q0 = Q1;
-            Q1 = Q2;
-            s_w = s_w == 2 ? 0 : s_w + 1;
-            s_r = s_r == 2 ? 0 : s_r + 1;
-        };
-        int y = y0;
-        for (; y < x0 - 4; ++y) step(y, std::integral_constant<int, 0>());
-        for (; y < x0 - 2; ++y) step(y, std::integral_constant<int, 1>());
-        for (; y < x0; ++y) step(y, std::integral_constant<int, 3>());
-        // three steps per trip: the period-3 rotations (d_{j-1}, T', d_j, T)
-        // become register renaming instead of copies
-        for (; y + 2 < xe; y += 3) {
-            step(y, std::integral_constant<int, 7>());
-            step(y + 1, std::integral_constant<int, 7>());
-            step(y + 2, std::integral_constant<int, 7>());
-        }
-        for (; y < xe; ++y) step(y, std::integral_constant<int, 7>());
+    };
+    const double2 z = make_double2(0.0, 0.0);
+    const Sp zs = Sp{z, z};
+    // state at the top of iteration y (see the header)
+    Sp D2, D3, Ld;                                   // d_{j-1}(y+2), (y+3); in flight (y+4)
+    LU Lut, Lux;                                     // in flight U(y+3)
+    Sp Mq, Mx = zs;                                  // in flight d_{j-2}(y+2), x(y+2)
+    double2 Ut0 = z, Ut1 = z, Ut2, Ux0 = z, Ux1 = z, Ux2, Uxm = z;  // U_t(y..y+2), U_x(y-1..y+2)
+    Sp P1 = zs, P2 = zs;                             // T'(y+1), T'(y+2)
+    Sp J0 = zs, J1 = zs;                             // d_j at rows y, y+1
+    Sp Q0 = zs, Q1 = zs;                             // T(y-1), T(y)
+    const int y0 = x0 - 6;
+    ld1(y0 + 2, D2);
+    ld1(y0 + 3, D3);
+    {
+        LU t2, x2;
+        ldu(y0 + 2, t2, x2);
+        Ut2 = cvu(t2);
+        Ux2 = cvu(x2);
     }
+    ld1(y0 + 4, Ld);
+    ldu(y0 + 3, Lut, Lux);
+    ld2(y0 + 2, Mq, Mx);
+    int s_w = 2, s_r = 0;  // LDS ring slots of r_j rows y+2 (written) and y (read)
+    // stage mask M: bit 0 = S2 + S3, bit 1 = S4, bit 2 = S5 (S1 always)
+    auto step = [&](int y, auto mtag) {
+        constexpr int M = decltype(mtag)::value;
+        const Sp D4 = Ld;
+        const double2 Ut3 = cvu(Lut), Ux3 = cvu(Lux);
+        ld1(y + 5, Ld);
+        ldu(y + 4, Lut, Lux);
+        __builtin_amdgcn_sched_barrier(0);  // keep the next rows' loads issued here
+        const Sp P3 = REV ? ra_site<FOLD, 1>(mass, sr0, sl0, D3, D4, D2, Ut3, Ux2, Ux3)
+                          : ra_site<FOLD, 1>(mass, sr0, sl0, D3, D2, D4, Ut3, Ux3, Ux2);  // S1: T'(y+3)
+        Sp J2 = zs, Q2 = zs;
+        if constexpr ((M & 1) != 0) {
+            const Sp A = REV ? ra_site<FOLD, 0>(mass, sr0, sl0, P2, P3, P1, Ut2, Ux1, Ux2)
+                             : ra_site<FOLD, 0>(mass, sr0, sl0, P2, P1, P3, Ut2, Ux2, Ux1);  // S2: Ad_{j-1}(y+2)
+            // S3: r_j, d_j at row y+2
+            const int xr = y + 2;
+            const Sp Q = Mq, X = Mx;
+            Sp rp, R2;
+            rp.a = cfms<FOLD>(D2.a, Q.a, beta2);
+            rp.b = cfms<FOLD>(D2.b, Q.b, beta2);
+            R2.a = cfms<FOLD>(rp.a, alpha, A.a);
+            R2.b = cfms<FOLD>(rp.b, alpha, A.b);
+            J2.a = cfma<FOLD>(R2.a, D2.a, beta);
+            J2.b = cfma<FOLD>(R2.b, D2.b, beta);
+            if (xr >= x0 && xr < xe && own) {
+                const int Xr = phys(xr);
+                const long n = (long)Xr * Wt + c;
+                st_nt(a.dn + n, J2.a);
+                st_nt(a.dn + n + a.V, J2.b);
+                if (SH && a.fsend) {  // fused face pack ([col][plane][x], lo: columns 0..3, hi: Wt-4..Wt-1)
+                    const int fcol = c < RH ? c : (c >= Wt - RH ? c - (Wt - RH) + RH : -1);
+                    if (fcol >= 0) {
+                        a.fsend[(long)(2 * fcol) * Nx + Xr] = J2.a;
+                        a.fsend[(long)(2 * fcol + 1) * Nx + Xr] = J2.b;
+                    }
+                }
+                if (XP && (Xr & 1) == a.xpar) {  // x_j = (x_{j-2} + alpha_{j-2} d_{j-2}) + alpha_{j-1} d_{j-1}
+                    st_nt(a.x + n, cfma<FOLD>(cfma<FOLD>(X.a, alpha2, Q.a), alpha, D2.a));
+                    st_nt(a.x + n + a.V, cfma<FOLD>(cfma<FOLD>(X.b, alpha2, Q.b), alpha, D2.b));
+                }
+                acc_n.x = nacc<FOLD>(acc_n.x, R2.a);  // Re dot(r, r), include/variables.h:185-188
+                acc_n.x = nacc<FOLD>(acc_n.x, R2.b);
+            }
+            rlds[(2 * s_w) * blockDim.x + threadIdx.x] = R2.a;
+            rlds[(2 * s_w + 1) * blockDim.x + threadIdx.x] = R2.b;
+        }
+        ld2(y + 3, Mq, Mx);  // consumed above: issued now, used next iteration
+        if constexpr ((M & 2) != 0)  // S4: T(y+1)
+            Q2 = REV ? ra_site<FOLD, 1>(mass, sr0, sl0, J1, J2, J0, Ut1, Ux0, Ux1)
+                     : ra_site<FOLD, 1>(mass, sr0, sl0, J1, J0, J2, Ut1, Ux1, Ux0);
+        if constexpr ((M & 4) != 0) {
+            const Sp o = REV ? ra_site<FOLD, 0>(mass, sr0, sl0, Q1, Q2, Q0, Ut0, Uxm, Ux0)
+                             : ra_site<FOLD, 0>(mass, sr0, sl0, Q1, Q0, Q2, Ut0, Ux0, Uxm);  // S5: Ad_j(y)
+            if (own) {
+                const Sp R0 = Sp{rlds[(2 * s_r) * blockDim.x + threadIdx.x], rlds[(2 * s_r + 1) * blockDim.x + threadIdx.x]};
+                acc_dA = cfma<FOLD>(acc_dA, J0.a, cconj(o.a));  // dot(d, Ad)
+                acc_dA = cfma<FOLD>(acc_dA, J0.b, cconj(o.b));
+                acc_rA = cfma<FOLD>(acc_rA, R0.a, cconj(o.a));  // dot(r, Ad)
+                acc_rA = cfma<FOLD>(acc_rA, R0.b, cconj(o.b));
+                acc_n.y = nacc<FOLD>(acc_n.y, o.a);            // |Ad|^2
+                acc_n.y = nacc<FOLD>(acc_n.y, o.b);
+            }
+        }
+        D2 = D3;
+        D3 = D4;
+        Uxm = Ux0;
+        Ut0 = Ut1;
+        Ux0 = Ux1;
+        Ut1 = Ut2;
+        Ux1 = Ux2;
+        Ut2 = Ut3;
+        Ux2 = Ux3;
+        P1 = P2;
+        P2 = P3;
+        J0 = J1;
+        J1 = J2;
+        Q0 = Q1;
+        Q1 = Q2;
+        s_w = s_w == 2 ? 0 : s_w + 1;
+        s_r = s_r == 2 ? 0 : s_r + 1;
+    };
+    int y = y0;
+    for (; y < x0 - 4; ++y) step(y, std::integral_constant<int, 0>());
+    for (; y < x0 - 2; ++y) step(y, std::integral_constant<int, 1>());
+    for (; y < x0; ++y) step(y, std::integral_constant<int, 3>());
+    // three steps per trip: the period-3 rotations (d_{j-1}, T', d_j, T)
+    // become register renaming instead of copies
+    for (; y + 2 < xe; y += 3) {
+        step(y, std::integral_constant<int, 7>());
+        step(y + 1, std::integral_constant<int, 7>());
+        step(y + 2, std::integral_constant<int, 7>());
+    }
+    for (; y < xe; ++y) step(y, std::integral_constant<int, 7>());
+}
 
 template <int SH, int XP, int FOLD, int RED = 0, int UC = 0, int TK = 0, int REV = 0>
 __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
