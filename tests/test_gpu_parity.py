@@ -208,6 +208,43 @@ def test_recompute_matches_twodir(sm, Nx, Nt, xchunk, fold, red):
     assert rel <= 1e-11, rel
 
 
+@pytest.mark.parametrize("rev", [0, 1, 2])
+@pytest.mark.parametrize("Nx,Nt,xchunk,max_iter", [(96, 120, 0, 10000), (200, 56, 7, 10000), (5, 9, 0, 10000),
+                                                  (64, 64, 64, 10000), (130, 66, 5, 17), (130, 66, 5, 16)])
+def test_march_schedules_match_twodir(sm, Nx, Nt, xchunk, max_iter, rev):
+    """The recompute-Ad pass under each march schedule (test option rev:
+    0 all forward, 1 odd passes backwards over reversed tiles, 2 x-adjacent
+    chunks in opposite directions as well; the ticketed-tail grids take it, so
+    the redundant-scalar path is switched off) against the stored-Ad
+    two-direction pass: same iteration count, x in the reduction-order band,
+    including chunks shorter than the 4-row halo, a last chunk shorter than
+    the others, odd chunk counts, a lattice smaller than one wave's halo, and
+    solves cut off by max_iter after an even / odd pass (the pending x rows
+    of a backward pass)."""
+    S = Nx * Nt
+    with opts_env(rev=rev, ra_red_max_blocks=0):  # read when the context is created
+        L = sm.init(Nx, Nt)
+    U, psi = sm.spinor(S), sm.spinor(S)
+    P = lambda a: a.ctypes.data  # noqa: E731
+    sm.lib.sm_fill_gauge(4321, 0.4242, Nt, 0, Nx, 0, Nt, P(U.mu0), P(U.mu1))
+    sm.lib.sm_fill_spinor(5678, Nt, 0, Nx, 0, Nt, P(psi.mu0), P(psi.mu1))
+    out = {}
+    old = sm.CG.max_iter
+    try:
+        sm.CG.max_iter = max_iter
+        for fused in (4, 5):
+            sm.check(sm.lib.sm_tune_cg(L.ctx, fused, xchunk if fused == 5 else 0))
+            x = sm.spinor(S)
+            conv = sm.conjugate_gradient(U, psi, x, -0.12)
+            out[fused] = (flat(x), L.last_cg.iterations, conv)
+    finally:
+        sm.CG.max_iter = old
+    assert out[5][2] == out[4][2] == (1 if max_iter == 10000 else 0)
+    assert abs(out[5][1] - out[4][1]) <= (1 if max_iter == 10000 else 0), (out[5][1], out[4][1])
+    rel = np.linalg.norm(out[5][0] - out[4][0]) / np.linalg.norm(out[4][0])
+    assert rel <= (1e-11 if max_iter == 10000 else 1e-13), rel
+
+
 def test_cg_nonconvergence_semantics(sm, capsys):
     meta, a = load_fixture("l64x64_b5_m-0p06")
     S = 64 * 64
