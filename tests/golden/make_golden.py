@@ -80,13 +80,13 @@ def run(cmd, **kw):
 # random sites plus global norms; the GPU test regenerates the inputs with the
 # same counter-based generator (bit-exact, tests/test_capi_host.py) and
 # compares. name, Nx, Nt, sigma, m0, (ranks_x, ranks_t) of the reference run.
-# 1 rank is the reference's own sequential dot order; 8192^2 runs on 2x2 MPI
+# 1 rank is the reference's own sequential dot order; 8192^2 runs on 2x4 MPI
 # ranks (a 1-rank solve there takes ~8 h on one core), which changes only the
 # dots' summation order (the operators are decomposition-invariant bitwise,
 # manifest "decomposition_2x2").
 LARGE = [("l1024x1024_b3_m-0p10", 1024, 1024, 0.3246, -0.10, (1, 1)),
          ("l4096x4096_b5_m-0p06", 4096, 4096, 0.2374, -0.06, (1, 1)),
-         ("l8192x8192_b2_m-0p19", 8192, 8192, 0.4242, -0.19, (2, 2))]
+         ("l8192x8192_b2_m-0p19", 8192, 8192, 0.4242, -0.19, (2, 4))]
 SAMPLE_SITES = 4096
 
 
@@ -333,7 +333,7 @@ def main():
     ap.add_argument("--mpi", action="store_true", help="also run 2x2 ranks (mpirun)")
     ap.add_argument("--large", nargs="+", default=None, metavar="NAME",
                     help="(re)make only these summary fixtures (LARGE names): 1024^2 ~4 min on one core, "
-                         "4096^2 ~70 min on one core, 8192^2 ~2-3 h on 2x2 ranks")
+                         "4096^2 ~70 min on one core, 8192^2 ~2 h on 2x4 ranks")
     ap.add_argument("--spread", nargs=3, default=None, metavar=("NAME", "RX", "RT"),
                     help="rerun a finished large fixture's reference solve on RX x RT ranks and record the "
                          "reference's own decomposition spread in the manifest")
