@@ -75,6 +75,26 @@ int down_rank(const sm_ctx *c) { return (c->shard - 1 + c->nshard) % c->nshard; 
 
 ncclComm_t comm_for(const sm_ctx *c, hipStream_t s) { return s == c->comm_stream ? c->comm_side : c->comm; }
 
+// Allocation size of a buffer the CG pass streams every iteration (the three
+// direction buffers, x, the link angles). Buffers of 256 MiB and more get an
+// allocation of their own of at least 2 GiB (a power of two), of which they
+// use the start. The CG pass at 4096^2 (tools/stride_probe.hip,
+// profiles/r03_v_stride_probe.jsonl) takes 476-493 us when its fields are
+// carved out of one pool (at every relative offset tried, 0 .. 1 GiB) or sit
+// in allocations of their own size, and 441-457 us (sometimes 468-484) in
+// allocations of 2-8 GiB; 8192^2 likewise (26.2-26.5 against 28.0-28.3
+// ps/site). Only the placement differs, not the kernel: the backing and
+// translation the memory system gives large allocations. bench.py, 3
+// interleaved pairs per box on 4 boxes (profiles/r03_w_padded_alloc_ab.jsonl):
+// 2230 / 2248 against 2091 / 2082 it/s where the old layout ran slow, equal
+// where it happened to run fast.
+size_t stream_alloc_bytes(size_t bytes) {
+    if (bytes < (size_t(256) << 20)) return bytes;
+    size_t a = size_t(2) << 30;
+    while (a < bytes) a <<= 1;
+    return a;
+}
+
 int exchange_faces_on(sm_ctx *c, hipStream_t s, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi,
                       size_t cnt) {
     if (cnt > kMaxFaceDoubles * (size_t)c->g.Nx) return fail(SM_ERR_ARG, "face too large (%zu)", cnt);
@@ -298,7 +318,7 @@ int ensure_link_angles(sm_ctx *c) {
     if (c->cg_fused != 5 || c->racfg.fold < 2 || !cg_ra_ok(c) || c->uang_state != 0) return SM_OK;
     if (!c->link_angles && !c->sharded()) return SM_OK;
     if (c->link_angles) {
-        if (!c->Uang) HIP_TRY(hipMalloc(&c->Uang, sizeof(double) * 2 * (size_t)c->g.V));
+        if (!c->Uang) HIP_TRY(hipMalloc(&c->Uang, stream_alloc_bytes(sizeof(double) * 2 * (size_t)c->g.V)));
         if (c->sharded() && !c->Uang_face)
             HIP_TRY(hipMalloc(&c->Uang_face, sizeof(double) * 16 * (size_t)c->g.Nx));
         const int nb = launch_link_angles(c->stream, 2 * c->g.V, c->U, c->Uang, c->partials);
@@ -578,7 +598,12 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     }
     chk(hipMalloc(&c->U, fb));
     chk(hipMalloc(&c->ghostU, sizeof(double2) * (size_t)Nx));
-    chk(hipMalloc(&c->fields, fb * NFIELDS));
+    for (int i = 0; i < NFIELDS; ++i) {
+        // the recompute-Ad pass's three direction buffers and the x it updates
+        const bool hot = i == F_D || i == F_D2 || i == F_R || i == F_X;
+        chk(hipMalloc(&c->fields[i], hot ? stream_alloc_bytes(fb) : fb));
+    }
+    c->x_internal = stream_alloc_bytes(fb) != fb;
     chk(hipMalloc(&c->faces, sizeof(double2) * 2 * (size_t)Nx * 8));
     chk(hipMalloc(&c->faces2, sizeof(double2) * 56 * (size_t)Nx));
     chk(hipMalloc(&c->faces4, sizeof(double2) * 64 * (size_t)Nx));
@@ -656,7 +681,12 @@ int sm_destroy(sm_ctx *c) {
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);  // e.g. a CG's trailing face exchange
     if (c->comm_side) ncclCommDestroy(c->comm_side);
     if (c->comm) ncclCommDestroy(c->comm);
-    void *dev[] = {c->U, c->ghostU, c->fields, c->faces, c->faces2, c->faces4, c->partials, c->sums, c->Fbuf, c->sc,
+    for (double2 *&f : c->fields)
+        if (f) {
+            (void)hipFree(f);
+            f = nullptr;
+        }
+    void *dev[] = {c->U, c->ghostU, c->faces, c->faces2, c->faces4, c->partials, c->sums, c->Fbuf, c->sc,
                    c->U_alt, c->Pmd, c->Fmd, c->eo, c->Ucb, c->eo_faces, c->eo_faces4, c->Uang, c->Uang_face,
                    c->tick, c->gsum};
     for (void *p : dev)
@@ -827,6 +857,14 @@ int sm_cg_begin(sm_ctx *c, const double *phi, double *x, double m0, double tol) 
     double2 *xx = (double2 *)x;
     c->cg_mass = m0 + 2;
     c->cg_phi = ph;
+    // On large fields the passes update x in F_X, an allocation laid out like
+    // the direction buffers (stream_alloc_bytes), and sm_cg_finish copies it
+    // to the caller's x: the caller's buffer is wherever its allocator put it.
+    c->cg_x_user = nullptr;
+    if (c->x_internal && xx != c->field(F_X) && ph != c->field(F_X)) {
+        c->cg_x_user = xx;
+        xx = c->field(F_X);
+    }
     c->cg_x = xx;
     double2 *r = c->field(F_R), *d = c->field(F_D), *Ad = c->field(F_AD), *t = c->field(F_T);
     if ((const double2 *)xx != ph) launch_copy(c->stream, n, ph, xx);          // x = phi
@@ -1091,6 +1129,11 @@ int sm_cg_finish(sm_ctx *c, sm_cg_result *res) {
         launch_cg_td_finish_x(c->stream, 2 * c->g.V, c->cg_x, cg_dbuf(c, 0), cg_dbuf(c, 1), cg_dbuf(c, 2), c->sc);
         HIP_TRY(hipGetLastError());
         c->cg_pending_x = 0;
+    }
+    if (c->cg_active && c->cg_x_user) {
+        launch_copy(c->stream, 2 * c->g.V, c->cg_x, c->cg_x_user);
+        HIP_TRY(hipGetLastError());
+        c->cg_x_user = nullptr;
     }
     c->cg_active = 0;
     return sm_cg_status(c, res);

@@ -107,7 +107,7 @@ struct sm_ctx {
     bool have_gauge = false;
     double2 *U = nullptr;          // 2V
     double2 *ghostU = nullptr;     // Nx: U_t at local t = -1 (lower neighbour's last column)
-    double2 *fields = nullptr;     // NFIELDS * 2V
+    double2 *fields[NFIELDS] = {};  // 2V each, one allocation per field (stream_alloc_bytes)
     double2 *faces = nullptr;      // 4 * 2Nx per spinor being exchanged (x2 for force)
     double2 *faces2 = nullptr;     // 2-deep faces: send lo/hi of 2 fields (4Nx each), recv d, r, U (8Nx each)
     double2 *faces4 = nullptr;     // 4-deep faces (sm_capi.cpp face4_*): send lo/hi, recv d x2 (by pass parity), U
@@ -135,12 +135,15 @@ struct sm_ctx {
     // active CG
     double cg_mass = 0.0;
     const double2 *cg_phi = nullptr;
-    double2 *cg_x = nullptr;
+    double2 *cg_x = nullptr;        // the x the passes update: the caller's, or F_X (cg_x_user != null)
+    double2 *cg_x_user = nullptr;   // the caller's x when the passes run on F_X (copied back by sm_cg_finish)
+    bool x_internal = false;        // fields of >= 256 MiB: a solve runs on F_X (stream_alloc_bytes) and
+                                    // copies x to the caller's buffer at sm_cg_finish
     int cg_active = 0;
     long cg_issued = 0;             // iterations enqueued since sm_cg_begin
     int cg_pending_x = 0;           // fused path: last x update deferred to sm_cg_finish
 
-    double2 *field(int i) { return fields + (size_t)i * 2 * g.V; }
+    double2 *field(int i) { return fields[i]; }
 };
 
 namespace sm_host {

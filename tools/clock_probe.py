@@ -61,6 +61,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=3.5)
     ap.add_argument("--chunk", type=int, default=100)
+    ap.add_argument("--shape", default="4096x4096", help="NxxNt of the lattice (config 3's field and m0)")
+    ap.add_argument("--no-apply", action="store_true")
     a = ap.parse_args()
     import torch
     import bench
@@ -69,8 +71,10 @@ def main():
     torch.cuda.set_stream(s)
     rt["stream"] = s
     cfg = bench.CONFIGS[3]
-    sh = bench.Shard(rt, cfg["Nx"], cfg["Nt"], cfg["sigma"])
+    Nx, Nt = map(int, a.shape.split("x"))
+    sh = bench.Shard(rt, Nx, Nt, cfg["sigma"])
     sm, m0 = sh.sm, cfg["m0"]
+    scale = Nx * Nt / 4096 ** 2
 
     def run(kind, launch, per_launch_s):
         n_chunks = max(2, int(a.seconds / (per_launch_s * a.chunk)))
@@ -90,7 +94,7 @@ def main():
         smp.stop.set()
         smp.join(30)
         us = [round(ev[i].elapsed_time(ev[i + 1]) * 1e3 / a.chunk, 1) for i in range(n_chunks)]
-        print(json.dumps({"kind": kind, "chunk": a.chunk, "us_per_launch": us, "load_start": round(t0, 3),
+        print(json.dumps({"kind": kind, "shape": a.shape, "chunk": a.chunk, "us_per_launch": us, "load_start": round(t0, 3),
                           "load_end": round(t1, 3), "smi": [compact(x) for x in smp.samples]}), flush=True)
 
     def cg(n):
@@ -103,8 +107,9 @@ def main():
     sm.check(sm.lib.sm_cg_link_angles(sh.L.ctx, 1, None))
     sm.check(sm.lib.sm_cg_begin(sh.L.ctx, sh.p(sh.phi), sh.p(sh.x), m0, 0.0))
     torch.cuda.synchronize()
-    run("cg_pass", cg, 450e-6)
-    run("dirac_apply", apply, 285e-6)
+    run("cg_pass", cg, 450e-6 * scale)
+    if not a.no_apply:
+        run("dirac_apply", apply, 285e-6 * scale)
     sh.close()
 
 
