@@ -198,7 +198,9 @@ int sm_cg_iterate(sm_ctx *ctx, int n);
 int sm_cg_status(sm_ctx *ctx, sm_cg_result *res);
 /* End a stepwise solve: apply the x update the fused iteration defers to the
  * next pass (x += alpha_{k-1} d_{k-1}), then report like sm_cg_status. Until
- * then x lags one update behind the reference's x. */
+ * then x lags one update behind the reference's x; on fields of 256 MiB and
+ * more (4096^2 / 2 planes and up) the passes work on an internal x, and the
+ * caller's x holds the solution only after this call. */
 int sm_cg_finish(sm_ctx *ctx, sm_cg_result *res);
 
 /* ==== gauge field, molecular dynamics and HMC =====
