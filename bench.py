@@ -249,17 +249,26 @@ def cpu_baseline(cfg, threads, ncg):
             "sample": f"{it.value} CG iterations (incl. initial DD^dag) at {Nx}x{Nt}, oracle/sm_oracle.c"}
 
 
+# The PMC summary of the current build (tools/gpu_r03_final.sh +
+# tools/summarize_prof.py); other shapes fall back to the newest file.
+PMC_SUMMARY = "r03_final2_dslash_pmc.json"
+
+
 def load_traffic(nx, nt):
     """HBM bytes per launch of the Dirac apply and of the CG pass from the
     committed rocprofv3 PMC summary (profiles/*_dslash_pmc.json, FETCH_SIZE +
-    WRITE_SIZE with the gfx950 rule); the newest file for this local shape
-    wins. Returns (file, apply bytes, CG pass bytes or None)."""
+    WRITE_SIZE with the gfx950 rule): PMC_SUMMARY if it holds this local
+    shape, else the newest file (natural order) that does. Returns (file,
+    apply bytes, CG pass bytes or None)."""
     best = None
     pdir = os.path.join(REPO, "profiles")
     if os.path.isdir(pdir):
         def natural(f):
             return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", f)]
-        for f in sorted(os.listdir(pdir), key=natural):
+        names = sorted(os.listdir(pdir), key=natural)
+        if PMC_SUMMARY in names:
+            names = [f for f in names if f != PMC_SUMMARY] + [PMC_SUMMARY]
+        for f in names:
             if f.endswith("_dslash_pmc.json"):
                 try:
                     with open(os.path.join(pdir, f)) as fh:
