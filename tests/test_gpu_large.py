@@ -6,7 +6,7 @@ fixture run, `oracle/_ref/sm_ref_<N>x<N> fixture`):
   * l4096x4096_b5_m-0p06  config 3 (the bench workload): beta=5 field,
                           m0 = -0.06, 1 rank
   * l8192x8192_b2_m-0p19  config 5: beta=2 field, m0 = -0.19 (near m_crit),
-                          2x2 MPI ranks (the reference's dots then sum in a
+                          2x4 MPI ranks (the reference's dots then sum in a
                           different order than on 1 rank; its operators are
                           decomposition-invariant bitwise)
 Each keeps the reference's outputs at 4096 seeded random sites plus a SHA-256
