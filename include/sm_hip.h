@@ -140,17 +140,18 @@ int sm_tune_cg(sm_ctx *ctx, int fused, int xchunk);
  * (1, 2 or 4; each wave owns 56 t-columns) and rows marched per block.
  * Values <= 0 keep the current setting. */
 int sm_tune_cg_geometry(sm_ctx *ctx, int waves_per_block, int xchunk);
-/* Link angles in the recompute-Ad CG pass (fused = 5, on by default): the
- * pass reads each link as its angle theta = atan2(Im U, Re U) (16 instead of
- * 32 B/site; 144 instead of 160 B/site per iteration) and rebuilds
- * U = (cos theta, sin theta) in registers, within ~1 ulp per component of the
- * stored link. The angles are rebuilt at the first solve after U changes, and
+/* Compact links in the recompute-Ad CG pass (fused = 5, on by default; the
+ * name is historical: round 2 stored each link's angle): the pass reads each
+ * link as ONE double, its smaller component with two flag bits (16 instead of
+ * 32 B/site; 144 instead of 160 B/site per iteration), and rebuilds the other
+ * component as +-sqrt(1 - v^2) in registers, within 3 ulp (3.3e-16) per
+ * component of the stored link (schwingermodel_amd/csrc/sm_linkcode.h). The codes are rebuilt at the first solve after U changes, and
  * only used when every link satisfies | |U|^2 - 1 | <= 1e-14 (the reference's
  * links are exp(i theta), src/gauge_conf.cpp); otherwise the pass reads the
  * complex links. D, D^dag and the force always use the stored links bitwise.
  * on: 1 / 0 enable / disable, < 0 keep; *in_use (may be NULL): 1 if the last
- * sm_cg_begin / sm_cg set the angles up for the active path. On t-shards the
- * choice is collective at the next solve: the angles are used only if every
+ * sm_cg_begin / sm_cg set the codes up for the active path. On t-shards the
+ * choice is collective at the next solve: the codes are used only if every
  * shard asks for them (one all-reduce, which every shard joins). */
 int sm_cg_link_angles(sm_ctx *ctx, int on, int *in_use);
 /* Streaming-bandwidth ceiling on the ctx stream (measured roofline reference):

@@ -76,7 +76,7 @@ int down_rank(const sm_ctx *c) { return (c->shard - 1 + c->nshard) % c->nshard; 
 ncclComm_t comm_for(const sm_ctx *c, hipStream_t s) { return s == c->comm_stream ? c->comm_side : c->comm; }
 
 // Allocation size of a buffer the CG pass streams every iteration (the three
-// direction buffers, x, the link angles). Buffers of 256 MiB and more get an
+// direction buffers, x, the link codes). Buffers of 256 MiB and more get an
 // allocation of their own of at least 2 GiB (a power of two), of which they
 // use the start. The CG pass at 4096^2 (tools/stride_probe.hip,
 // profiles/r03_v_stride_probe.jsonl) takes 476-493 us when its fields are
@@ -292,7 +292,7 @@ static int halo4(sm_ctx *c, hipStream_t s, const double2 *field, double2 *recv) 
 }
 
 int exchange_ghost_U(sm_ctx *c) {
-    c->uang_state = 0;  // every change of U comes through here: the link angles are stale
+    c->uang_state = 0;  // every change of U comes through here: the link codes are stale
     if (!c->sharded()) return SM_OK;
     // U_t(x, Wt-1) (plane 0 of my hi face) is the up-neighbour's U_t(x, -1)
     double2 *slo = face_buf(c, 1, 0), *shi = face_buf(c, 1, 1);
@@ -307,12 +307,12 @@ int exchange_ghost_U(sm_ctx *c) {
 }
 
 
-// Link angles for the recompute-Ad pass (cg_ra_kernel UC), rebuilt at the
+// Link codes for the recompute-Ad pass (cg_ra_kernel UC, sm_linkcode.h), rebuilt at the
 // first solve after U changed. On t-shards the decision is collective: the
 // path conditions below are rank-uniform (shape rules, the same test options
 // everywhere), but the link_angles wish is per context (sm_cg_link_angles),
-// so every shard whose angles are stale takes part in ONE all-reduce of
-// (links off the unit circle, shards not asking for angles) and the angles
+// so every shard whose codes are stale takes part in ONE all-reduce of
+// (links off the unit circle, shards not asking for codes) and the codes
 // are used only when both sums are 0.
 int ensure_link_angles(sm_ctx *c) {
     if (c->cg_fused != 5 || c->racfg.fold < 2 || !cg_ra_ok(c) || c->uang_state != 0) return SM_OK;
@@ -321,7 +321,7 @@ int ensure_link_angles(sm_ctx *c) {
         if (!c->Uang) HIP_TRY(hipMalloc(&c->Uang, stream_alloc_bytes(sizeof(double) * 2 * (size_t)c->g.V)));
         if (c->sharded() && !c->Uang_face)
             HIP_TRY(hipMalloc(&c->Uang_face, sizeof(double) * 16 * (size_t)c->g.Nx));
-        const int nb = launch_link_angles(c->stream, 2 * c->g.V, c->U, c->Uang, c->partials);
+        const int nb = launch_link_codes(c->stream, 2 * c->g.V, c->U, c->Uang, c->partials);
         launch_sum_partials(c->stream, nb, c->partials, c->sums);  // (links off the circle, 0)
     } else {
         c->h_sums[1] = make_double2(0.0, 1.0);                      // (0, this shard declines)
@@ -331,7 +331,7 @@ int ensure_link_angles(sm_ctx *c) {
     HIP_TRY(hipMemcpyAsync(c->h_sums, c->sums, sizeof(double2), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->uang_state = c->h_sums[0].x == 0.0 && c->h_sums[0].y == 0.0 ? 1 : 2;
-    if (c->uang_state == 1 && c->sharded()) launch_angles_of(c->stream, 16 * (long)c->g.Nx, face4_recv_U(c), c->Uang_face);
+    if (c->uang_state == 1 && c->sharded()) launch_codes_of(c->stream, 16 * (long)c->g.Nx, face4_recv_U(c), c->Uang_face);
     HIP_TRY(hipGetLastError());
     return SM_OK;
 }
@@ -454,7 +454,7 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //   rev=0|1|2           recompute-Ad pass march schedule (0 all forward; 1 odd
 //                       passes backward; 2, the default, x-adjacent chunks in
 //                       opposite directions and odd passes flipped)
-//   link_angles=0|1     recompute-Ad pass reads the links as angles
+//   link_angles=0|1     recompute-Ad pass reads the links as one-double codes
 //   bt=64|128|256       Dirac apply t-columns per block
 //   eo_fused=0, eo_cg_td=0, eo_cg_folded=1   even-odd operator / CG forms
 //   debug_cg=1          CG host loops print their status (stderr)

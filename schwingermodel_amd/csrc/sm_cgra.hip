@@ -14,7 +14,7 @@
 // used for its dots. A pass reads d_{j-1}, d_{j-2}, U (96 B/site) and writes
 // d_j (32), plus x on half the rows (32 on average): 160 B/site against 224
 // for mode 4 and 576 for the reference's sequence; 144 with
-// the links read as angles (UC). Each x row takes its two updates together
+// the links read as one-double codes (UC). Each x row takes its two updates together
 // every other pass, the even rows on even passes and the odd rows on odd
 // ones, so every pass moves the same bytes (with all of x on even passes the
 // odd pass was VALU-bound and the even one HBM-bound). The price of the
@@ -54,7 +54,7 @@
 
 #include "sm_device.h"
 #include "sm_internal.h"
-#include "sm_sincos.h"
+#include "sm_linkcode.h"
 
 #pragma clang fp contract(off)
 
@@ -78,7 +78,7 @@ struct RAArgs {
     double mass;
     const double2 *prev;  // RED: pass j-1's partials
     long pass;
-    const double *Ua, *fUa;  // UC: link angles theta_t, theta_x (plane stride V) and their 4-deep faces
+    const double *Ua, *fUa;  // UC: link codes of U_t, U_x (plane stride V, sm_linkcode.h) and their 4-deep faces
     int xpar;                // XP: this pass updates x on the rows of parity xpar (= pass & 1)
     int pbase;               // partial slots: tile pbase + (t-block - tb0) * XB + x-chunk
     double2 *fsend;          // SH: != null -> the edge blocks also write d_j's 4-deep send faces
@@ -94,17 +94,13 @@ struct RAArgs {
     int flip, alt;
 };
 
-// U(1) link from its angle (UC): cos and sin of theta in [-pi, pi]
-// (sm_sincos.h: reduced-range fdlibm kernels, within 1 ulp) in place of a
-// 16-B load.
-__device__ __forceinline__ double2 u_of(double th) {
-#ifdef SM_PROBE_NO_SINCOS  // timing probe only (tools/): the link load without its sincos
-    return make_double2(th, th);
-#else
+// U(1) link from its one-double code (UC; sm_linkcode.h: the smaller
+// component as stored, the other one by a square root, within 3 ulp) in place
+// of a 16-B load.
+__device__ __forceinline__ double2 u_of(double code) {
     double c, s;
-    sm_cos_sin_pi(th, &c, &s);
+    sm_link_decode(code, &c, &s);
     return make_double2(c, s);
-#endif
 }
 
 template <typename T>
@@ -216,7 +212,7 @@ __device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x
     const double mass = a.mass;
     const RSrc<double2> S1 = rsrc<SH>(a.d1, a.f1, c, a);
     const RSrc<double2> S2 = rsrc<SH>(a.d2, a.f2, c, a);
-    using LU = std::conditional_t<UC != 0, double, double2>;  // a link as loaded: angle or complex
+    using LU = std::conditional_t<UC != 0, double, double2>;  // a link as loaded: code or complex
     const RSrc<LU> SU = [&] {
         if constexpr (UC != 0) return rsrc<SH>(a.Ua, a.fUa, c, a);
         else return rsrc<SH>(a.U, a.fU, c, a);
@@ -600,7 +596,7 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
     a.xpar = (int)(pass & 1);
     // one kernel per (shards, x pass, fold, scalar mode, link form, tail) combination
     const int f = c.fold >= 2 ? 2 : (c.fold ? 1 : 0);
-    const int uc = Uang && f == 2;  // link angles: with the fused multiply-add fold only
+    const int uc = Uang && f == 2;  // link codes: with the fused multiply-add fold only
     const int tk = tick != nullptr && f == 2;
     if (prev_partials && nshard == 1 && f == 2 && tb0 == 0 && tbn == c.TBk) {
         if (uc) ra_go<0, 1, 1, 2>(xp, 0, grid, block, lds, s, a);
@@ -648,16 +644,15 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
     }
 }
 
-// Link angles for the UC passes: theta = atan2(Im U, Re U) for each of the n
-// links (both planes), and per block the count of links whose |U|^2 is off 1
-// by more than 1e-14 (such fields keep the complex-link passes, sm_capi.cpp).
-// cos/sin of the angle give back a unit link within ~1 ulp per component.
-__global__ void __launch_bounds__(256) link_angle_kernel(long n, const double2 *U, double *Ua, double2 *part) {
+// Link codes for the UC passes (sm_linkcode.h) for each of the n links (both
+// planes), and per block the count of links whose |U|^2 is off 1 by more than
+// 1e-14 (such fields keep the complex-link passes, sm_capi.cpp).
+__global__ void __launch_bounds__(256) link_code_kernel(long n, const double2 *U, double *Ua, double2 *part) {
     __shared__ double2 sh[4];
     double bad = 0.0;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
         const double2 u = U[i];
-        Ua[i] = atan2(u.y, u.x);
+        Ua[i] = sm_link_encode(u.x, u.y);
         const double m = u.x * u.x + u.y * u.y - 1.0;
         if (!(fabs(m) <= 1e-14)) bad += 1.0;  // NaN counts as off the circle
     }
@@ -665,19 +660,19 @@ __global__ void __launch_bounds__(256) link_angle_kernel(long n, const double2 *
     if (threadIdx.x == 0) part[blockIdx.x] = b;
 }
 
-int launch_link_angles(hipStream_t s, long n, const double2 *U, double *Ua, double2 *partials) {
+int launch_link_codes(hipStream_t s, long n, const double2 *U, double *Ua, double2 *partials) {
     const int nb = reduce_blocks(n);
-    hipLaunchKernelGGL(link_angle_kernel, dim3(nb), dim3(256), 0, s, n, U, Ua, partials);
+    hipLaunchKernelGGL(link_code_kernel, dim3(nb), dim3(256), 0, s, n, U, Ua, partials);
     return nb;
 }
 
-__global__ void __launch_bounds__(256) angles_of_kernel(long n, const double2 *U, double *Ua) {
+__global__ void __launch_bounds__(256) codes_of_kernel(long n, const double2 *U, double *Ua) {
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-        Ua[i] = atan2(U[i].y, U[i].x);
+        Ua[i] = sm_link_encode(U[i].x, U[i].y);
 }
 
-void launch_angles_of(hipStream_t s, long n, const double2 *U, double *Ua) {
-    hipLaunchKernelGGL(angles_of_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, U, Ua);
+void launch_codes_of(hipStream_t s, long n, const double2 *U, double *Ua) {
+    hipLaunchKernelGGL(codes_of_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, U, Ua);
 }
 
 // After the last pass J = k of the recompute-Ad CG, the rows of parity

@@ -70,14 +70,14 @@ struct sm_ctx {
     long cg_flush_pass = -1;        // last one-pass pass whose scalars still await evaluation
     int cg_flush_nparts = 0;        // its partial count (the one-pass or the recompute-Ad grid)
     int cg_ra_red_max_blocks = 512; // recompute-Ad pass: redundant scalars up to this many blocks (one shard)
-    // recompute-Ad pass with link angles (sm_cgra.hip UC): U enters the CG as
-    // theta_t, theta_x (16 B/site) and is rebuilt as (cos, sin) in registers.
+    // recompute-Ad pass with compact links (sm_cgra.hip UC): U enters the CG as
+    // one double per link (sm_linkcode.h, 16 B/site), rebuilt in registers.
     // Built at the first solve after U changes (uang_state 0); state 1 = in
     // use, 2 = some link is off the unit circle, so the complex links are used.
     int link_angles = 1;
     int uang_state = 0;
-    double *Uang = nullptr;         // 2V angles (plane mu0 then mu1)
-    double *Uang_face = nullptr;    // t-shards: angles of the 4-deep ghost links (16 Nx)
+    double *Uang = nullptr;         // 2V link codes (plane mu0 then mu1)
+    double *Uang_face = nullptr;    // t-shards: codes of the 4-deep ghost links (16 Nx)
     hipStream_t own_stream = nullptr, stream = nullptr;
     hipStream_t comm_stream = nullptr;  // halo exchange overlapped with interior compute (hosted: == stream)
     bool own_comm_stream = false;       // comm_stream created by (and destroyed with) this context

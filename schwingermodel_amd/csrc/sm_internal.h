@@ -149,11 +149,12 @@ constexpr int kMaxTickGroups = 1024;
 // (partial slot of a tile: pbase + (t-block - tb0) * XB + x-chunk; fsend (t-shards):
 // the blocks owning columns 0..3 / Wt-4..Wt-1 also write d_j's 4-deep send
 // faces, lo at fsend and hi at fsend + 8 Nx, as launch_pack_faces_k would)
-// Link angles of U for the passes above (Uang: 16 instead of 32 B/site of
-// links): writes theta = atan2(Im, Re) of n links and, per block, the count of
-// links off the unit circle (> 1e-14 in |U|^2) to partials; returns the block count.
-int launch_link_angles(hipStream_t s, long n, const double2 *U, double *Ua, double2 *partials);
-void launch_angles_of(hipStream_t s, long n, const double2 *U, double *Ua);  // faces: angles only
+// Link codes of U for the passes above (Uang: 16 instead of 32 B/site of
+// links, sm_linkcode.h): writes the one-double code of n links and, per block,
+// the count of links off the unit circle (> 1e-14 in |U|^2) to partials;
+// returns the block count.
+int launch_link_codes(hipStream_t s, long n, const double2 *U, double *Ua, double2 *partials);
+void launch_codes_of(hipStream_t s, long n, const double2 *U, double *Ua);  // faces: codes only
 // Recompute-Ad CG: after the last pass add alpha_{k-1} d_{k-1} to the rows
 // whose x update is still pending (parity != k & 1; x row = site / Wt).
 void launch_cg_ra_finish_x(hipStream_t s, const Geometry &g, double2 *x, const double2 *d0, const double2 *d1,

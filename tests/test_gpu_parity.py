@@ -309,9 +309,10 @@ def _angles_in_use(sm, L):
 
 @pytest.mark.parametrize("name", NAMES)
 def test_link_angles_vs_complex_links(sm, name):
-    """The recompute-Ad pass reading each link as its angle (16 instead of 32
-    B/site, the default) against the same pass reading the complex links: the
-    angle form rebuilds U = (cos, sin) within ~1 ulp, so the iteration counts
+    """The recompute-Ad pass reading each link as its one-double code (16
+    instead of 32 B/site, the default; sm_linkcode.h) against the same pass
+    reading the complex links: the code form rebuilds U within 3 ulp per
+    component (tests/test_linkcode_host.py), so the iteration counts
     agree (+-1) and x to 1e-12; both meet the reference's solution to 1e-12
     (test_cg_vs_reference runs the default)."""
     meta, a = load_fixture(name)
@@ -338,9 +339,9 @@ def test_link_angles_vs_complex_links(sm, name):
 
 
 def test_link_angles_follow_gauge_updates(sm):
-    """Angles are rebuilt after every change of U (upload, MD update), never
-    reused stale, and a field with a link off the unit circle keeps the
-    complex-link pass: its x is bitwise the angles-off solve's."""
+    """Link codes are rebuilt after every change of U (upload, MD update),
+    never reused stale, and a field with a link off the unit circle keeps the
+    complex-link pass: its x is bitwise the codes-off solve's."""
     Nx, Nt = 96, 64
     S = Nx * Nt
     L = sm.init(Nx, Nt)
