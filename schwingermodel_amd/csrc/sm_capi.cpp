@@ -561,10 +561,12 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     //   2048 (RCCL loopback, us per apply: 4096x1024 79 vs 91 split; 4096x2048
     //   166 vs 164, 4096^2 296 vs 292; profiles/r02_v8_apply_split.log).
     c->apply_split = c->g.Wt >= 2048 ? 1 : 0;
-    // * link angles from 4M sites per shard: below, the fields of a pass sit
+    // * link codes from 4M sites per shard: below, the fields of a pass sit
     //   largely in the 256 MB MALL and the pass is bound by its VALU work,
-    //   where the sincos costs more than the 16 B it saves (tools/tune_shapes.py:
-    //   4096x512 0.080 vs 0.068 ms per iteration, 4096x1024 0.141 vs 0.147).
+    //   where decoding the links cost more than the 16 B it saves (round 2's
+    //   angle form, tools/tune_shapes.py: 4096x512 0.080 vs 0.068 ms per
+    //   iteration, 4096x1024 0.141 vs 0.147; tools/link_probe.py re-measures
+    //   it for the codes).
     c->link_angles = c->g.V >= (1L << 22) ? 1 : 0;
     if (int rc = apply_test_opts(c); rc != SM_OK) {
         delete c;
