@@ -249,31 +249,35 @@ def cpu_baseline(cfg, threads, ncg):
             "sample": f"{it.value} CG iterations (incl. initial DD^dag) at {Nx}x{Nt}, oracle/sm_oracle.c"}
 
 
-# The PMC summary of the current build (tools/gpu_r03_final.sh +
-# tools/summarize_prof.py); other shapes fall back to the newest file.
-PMC_SUMMARY = "r03_final2_dslash_pmc.json"
+def lib_build_id():
+    """sm_build_id() of the library this process runs (schwingermodel_amd/build.py
+    source_id: a hash of its sources and flags); None for a build without it."""
+    import schwingermodel_amd as sm
+    fn = getattr(sm.lib, "sm_build_id", None)
+    if fn is None:
+        return None
+    fn.restype = ctypes.c_char_p
+    return fn().decode()
 
 
-def load_traffic(nx, nt):
-    """HBM bytes per launch of the Dirac apply and of the CG pass from the
+def load_traffic(nx, nt, build_id):
+    """HBM bytes per launch of the Dirac apply and of the CG pass from a
     committed rocprofv3 PMC summary (profiles/*_dslash_pmc.json, FETCH_SIZE +
-    WRITE_SIZE with the gfx950 rule): PMC_SUMMARY if it holds this local
-    shape, else the newest file (natural order) that does. Returns (file,
-    apply bytes, CG pass bytes or None)."""
+    WRITE_SIZE with the gfx950 rule, tools/summarize_prof.py) of THIS build:
+    the newest summary (natural order) whose build_id is the running
+    library's and which holds this local shape. A summary of another build is
+    never cited. Returns (file, apply bytes, CG pass bytes) or None."""
     best = None
     pdir = os.path.join(REPO, "profiles")
-    if os.path.isdir(pdir):
+    if build_id and os.path.isdir(pdir):
         def natural(f):
             return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", f)]
-        names = sorted(os.listdir(pdir), key=natural)
-        if PMC_SUMMARY in names:
-            names = [f for f in names if f != PMC_SUMMARY] + [PMC_SUMMARY]
-        for f in names:
+        for f in sorted(os.listdir(pdir), key=natural):
             if f.endswith("_dslash_pmc.json"):
                 try:
                     with open(os.path.join(pdir, f)) as fh:
                         d = json.load(fh)
-                    if d.get("Nx") == nx and d.get("Nt") == nt:
+                    if d.get("build_id") == build_id and d.get("Nx") == nx and d.get("Nt") == nt:
                         best = (f, d.get("hbm_bytes_per_launch"), d.get("cg_pass_hbm_bytes_per_launch"))
                 except Exception:  # noqa: BLE001
                     pass
@@ -489,17 +493,22 @@ def run_config34(args, rt, cfg_id):
         "ms_per_step": round(1e3 * t_cg / args.steps, 4),
         "scaling": "strong",
     })
+    # the CPU reference beside every N (north_star: "next to the reference MPI
+    # path timed on the same box's host cores"), on rank 0 after the GPU
+    # timing: the same whole lattice, a bounded sample
     cpu = None
-    if world == 1 and not args.no_cpu_baseline:
+    if not args.no_cpu_baseline:
         cpu = cpu_baseline(dict(cfg, Nx=Nx, Nt=Nt), args.cpu_threads or cpu_share(), args.cpu_iters)
-    tr = load_traffic(Nx, sh.Wt)
+    bid = lib_build_id()
+    tr = load_traffic(Nx, sh.Wt, bid)
     line.update({
         "dirac_apply_GBps": round(apply_GBps, 1),
         "dirac_apply_us": round(apply_s * 1e6, 2),
         "roofline": {"bound": "hbm", "achieved": round(apply_GBps, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(apply_GBps / HBM_PEAK_GBPS, 4),
                      "traffic": tr[1] if tr else None,
-                     "traffic_source": tr[0] if tr else None,
+                     "traffic_source": tr[0] if tr else f"no PMC summary of build {bid} under profiles/",
+                     "build_id": bid,
                      "kernel": f"dslash_kernel<D>, {BYTES_PER_SITE_APPLY} B/site algorithmic x {V} sites per launch"},
         "cpu_baseline": cpu,
         # the CG iteration's own streaming rate (informational; the graded

@@ -140,26 +140,44 @@ int sm_tune_cg(sm_ctx *ctx, int fused, int xchunk);
  * (1, 2 or 4; each wave owns 56 t-columns) and rows marched per block.
  * Values <= 0 keep the current setting. */
 int sm_tune_cg_geometry(sm_ctx *ctx, int waves_per_block, int xchunk);
-/* Compact links in the recompute-Ad CG pass (fused = 5, on by default; the
- * name is historical: round 2 stored each link's angle): the pass reads each
- * link as ONE double, its smaller component with two flag bits (16 instead of
- * 32 B/site; 144 instead of 160 B/site per iteration), and rebuilds the other
- * component as +-sqrt(1 - v^2) in registers, within 3 ulp (3.3e-16) per
- * component of the stored link (schwingermodel_amd/csrc/sm_linkcode.h). The codes are rebuilt at the first solve after U changes, and
- * only used when every link satisfies | |U|^2 - 1 | <= 1e-14 (the reference's
- * links are exp(i theta), src/gauge_conf.cpp); otherwise the pass reads the
- * complex links. D, D^dag and the force always use the stored links bitwise.
+/* Compact links in the recompute-Ad CG pass (fused = 5, on by default): the
+ * pass reads each link as ONE double, its smaller component with two flag
+ * bits (16 instead of 32 B/site; 144 instead of 160 B/site per iteration),
+ * and rebuilds the other component as +-sqrt(1 - v^2) in registers
+ * (schwingermodel_amd/csrc/sm_linkcode.h). The codes are rebuilt at the first
+ * solve after U changes, by a kernel that also decodes every code with the
+ * pass's own decoder; they are used only if EVERY link comes back within
+ * 2^-51 (4.4e-16) per component of the stored link (fresh exp(i theta)
+ * links, as the reference's, src/gauge_conf.cpp:23-29, all do), else the
+ * pass reads the complex links. D, D^dag and the force always use the
+ * stored links bitwise. sm_cg_link_angles is the round-2 name of the same
+ * call (the code was then the link's angle). */
+int sm_cg_link_codes(sm_ctx *ctx, int on, int *in_use);
+/* Round-2 name of sm_cg_link_codes; same behaviour, kept for old callers.
  * on: 1 / 0 enable / disable, < 0 keep; *in_use (may be NULL): 1 if the last
  * sm_cg_begin / sm_cg set the codes up for the active path. On t-shards the
- * choice is collective at the next solve: the codes are used only if every
- * shard asks for them (one all-reduce, which every shard joins). */
+ * choice is collective at the next solve: every solve all-reduces the count
+ * of shards whose codes are stale (a new U, or a changed wish on any one
+ * rank); if it is not 0 every shard rebuilds and the codes are used only if
+ * every shard asks for them (one more all-reduce, which every shard joins). */
 int sm_cg_link_angles(sm_ctx *ctx, int on, int *in_use);
+/* Diagnostic (tests): encode every link of the context's current U and decode
+ * it again ON THE DEVICE with the CG pass's own functions. Writes the rebuilt
+ * links to U_out_dev (device, the layout of sm_upload_gauge_dev; may be NULL),
+ * the largest per-component |rebuilt - stored| to *max_err and the count of
+ * links beyond 2^-51 to *n_bad (this shard only). Synchronous. */
+int sm_link_code_check(sm_ctx *ctx, double *U_out_dev, double *max_err, long *n_bad);
 /* Streaming-bandwidth ceiling on the ctx stream (measured roofline reference):
  * out = a + b (two_reads = 1: the stencil's 2-read/1-write byte mix) or
  * out = a, over n complex<double> device elements. */
 int sm_bench_stream(sm_ctx *ctx, int two_reads, long n, const double *a, const double *b, double *out,
                     int blocks);
 int sm_local_sites(const sm_ctx *ctx, long *V, int *Nx, int *Wt, int *t0);
+/* Build id of this library: 16 hex digits of the SHA-256 of its sources,
+ * headers and compile flags (schwingermodel_amd/build.py source_id). Profile
+ * summaries under profiles/ record it, and bench.py cites only a summary of
+ * the build that runs. */
+const char *sm_build_id(void);
 
 /* Gauge field (host / device). Must precede every operator call; re-upload
  * whenever the caller changes U (the reference mutates U between calls,

@@ -50,6 +50,7 @@ def _load():
         raise ImportError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`"
                           " (the HIP path has no CPU fallback)")
     lib = ctypes.CDLL(LIB_PATH)
+    ab_override = bool(os.environ.get("SM_LIB_PATH"))
     vp, ci, cd, cl = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_long
     u64 = ctypes.c_uint64
     sig = {
@@ -89,7 +90,10 @@ def _load():
         "sm_cg_status": ([vp, ctypes.POINTER(CGResult)], ci),
         "sm_cg_finish": ([vp, ctypes.POINTER(CGResult)], ci),
         "sm_tune_cg": ([vp, ci, ci], ci),
+        "sm_build_id": ([], ctypes.c_char_p),
+        "sm_cg_link_codes": ([vp, ci, ctypes.POINTER(ci)], ci),
         "sm_cg_link_angles": ([vp, ci, ctypes.POINTER(ci)], ci),
+        "sm_link_code_check": ([vp, vp, ctypes.POINTER(cd), ctypes.POINTER(ctypes.c_long)], ci),
         "sm_tune_cg_geometry": ([vp, ci, ci], ci),
         # gauge field / molecular dynamics / HMC
         "sm_download_gauge": ([vp, vp, vp], ci),
@@ -113,7 +117,9 @@ def _load():
         "sm_eo_cg": ([vp, vp, vp, vp, vp, cd, cd, ci, ctypes.POINTER(CGResult)], ci),
     }
     for name, (args, res) in sig.items():
-        fn = getattr(lib, name)
+        if ab_override and not hasattr(lib, name):
+            continue  # an older build under an A/B override may predate newer entry points
+        fn = getattr(lib, name)  # the product library must export every entry point
         fn.argtypes = args
         fn.restype = res
     return lib

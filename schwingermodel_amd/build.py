@@ -35,6 +35,24 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def source_id():
+    """Build id of the library: SHA-256 (16 hex) of its sources, headers and
+    compile flags. Compiled into the library (sm_build_id()) so a profile
+    summary recorded with one build can be matched to the build that runs
+    (bench.py's roofline.traffic_source), independent of whether the compiler
+    output is byte-reproducible."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in SOURCES + HEADERS:
+        h.update(name.encode())
+        with open(os.path.join(CSRC, name), "rb") as f:
+            h.update(f.read())
+    with open(os.path.join(REPO, "include", "sm_hip.h"), "rb") as f:
+        h.update(f.read())
+    h.update(" ".join(CFLAGS + LDFLAGS).encode())
+    return h.hexdigest()[:16]
+
+
 def build_library(force=False, verbose=True):
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
     deps.append(os.path.join(REPO, "include", "sm_hip.h"))
@@ -63,8 +81,14 @@ def build_library(force=False, verbose=True):
             sys.stderr.write(p.stderr)
         if p.returncode:
             raise subprocess.CalledProcessError(p.returncode, c)
+    bid_src = os.path.join(objdir, "sm_build_id.cpp")
+    with open(bid_src, "w") as f:
+        f.write(f'extern "C" const char *sm_build_id(void) {{ return "{source_id()}"; }}\n')
+    bid_obj = bid_src + ".o"
+    subprocess.run(["g++", "-O2", "-fPIC", "-c", bid_src, "-o", bid_obj], check=True)
     tmp = LIB + ".tmp"
-    cmd = [HIPCC, f"--offload-arch={ARCH}"] + [os.path.join(objdir, s + ".o") for s in SOURCES] + ["-o", tmp] + LDFLAGS
+    cmd = ([HIPCC, f"--offload-arch={ARCH}"] + [os.path.join(objdir, s + ".o") for s in SOURCES] + [bid_obj]
+           + ["-o", tmp] + LDFLAGS)
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "sm_fields.h"
 #include "sm_ctx.h"
@@ -73,6 +74,17 @@ int down_rank(const sm_ctx *c) { return (c->shard - 1 + c->nshard) % c->nshard; 
 // column goes down (the down-neighbour's t = Wt). The face buffers are
 // [plane][x], 4*Nx doubles.
 
+// One communicator per stream. Co-residency assumption: while a
+// pass's pipelined face exchange runs on comm_side (comm stream), the main
+// stream's all-reduce on comm may be in flight too. RCCL documents that two
+// communicators with blocking kernels in flight at once can deadlock if those
+// kernels cannot be resident together on the GPU. Here each is ONE small
+// kernel (a send/recv pair of <= 1 MiB and a 48-byte all-reduce, one channel's
+// worth of blocks each) next to at most the CG pass's interior launch, whose
+// blocks retire on their own (no spin on other kernels), so both collective
+// kernels always find room as the pass drains; every rank issues them in the
+// same order. The multi-process RCCL run that exercises this is the driver's
+// N > 1 bench; the one-rank loopback tests cover the code path.
 ncclComm_t comm_for(const sm_ctx *c, hipStream_t s) { return s == c->comm_stream ? c->comm_side : c->comm; }
 
 // Allocation size of a buffer the CG pass streams every iteration (the three
@@ -311,18 +323,30 @@ int exchange_ghost_U(sm_ctx *c) {
 // first solve after U changed. On t-shards the decision is collective: the
 // path conditions below are rank-uniform (shape rules, the same test options
 // everywhere), but the link_angles wish is per context (sm_cg_link_angles),
-// so every shard whose codes are stale takes part in ONE all-reduce of
-// (links off the unit circle, shards not asking for codes) and the codes
-// are used only when both sums are 0.
+// and so is its staleness (a wish change on one rank marks only that rank's
+// codes stale). So every solve on t-shards first all-reduces the count of
+// stale shards; when it is not 0, EVERY shard rebuilds and joins ONE
+// all-reduce of (links off the unit circle, shards not asking for codes), and
+// the codes are used only when both sums are 0. Every rank thus issues the
+// same collectives in the same order, whichever rank changed its wish.
 int ensure_link_angles(sm_ctx *c) {
-    if (c->cg_fused != 5 || c->racfg.fold < 2 || !cg_ra_ok(c) || c->uang_state != 0) return SM_OK;
-    if (!c->link_angles && !c->sharded()) return SM_OK;
+    if (c->cg_fused != 5 || c->racfg.fold < 2 || !cg_ra_ok(c)) return SM_OK;
+    if (c->sharded()) {
+        c->h_sums[1] = make_double2(c->uang_state == 0 ? 1.0 : 0.0, 0.0);  // (this shard is stale, 0)
+        HIP_TRY(hipMemcpyAsync(c->sums, c->h_sums + 1, sizeof(double2), hipMemcpyHostToDevice, c->stream));
+        TRY(allreduce_dev(c, (double *)c->sums, 2));
+        HIP_TRY(hipMemcpyAsync(c->h_sums, c->sums, sizeof(double2), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (c->h_sums[0].x == 0.0) return SM_OK;  // rank-uniform: no shard is stale
+    } else if (c->uang_state != 0 || !c->link_angles) {
+        return SM_OK;
+    }
     if (c->link_angles) {
         if (!c->Uang) HIP_TRY(hipMalloc(&c->Uang, stream_alloc_bytes(sizeof(double) * 2 * (size_t)c->g.V)));
         if (c->sharded() && !c->Uang_face)
             HIP_TRY(hipMalloc(&c->Uang_face, sizeof(double) * 16 * (size_t)c->g.Nx));
         const int nb = launch_link_codes(c->stream, 2 * c->g.V, c->U, c->Uang, c->partials);
-        launch_sum_partials(c->stream, nb, c->partials, c->sums);  // (links off the circle, 0)
+        launch_sum_partials(c->stream, nb, c->partials, c->sums);  // (links beyond SM_LINKCODE_TOL, 0)
     } else {
         c->h_sums[1] = make_double2(0.0, 1.0);                      // (0, this shard declines)
         HIP_TRY(hipMemcpyAsync(c->sums, c->h_sums + 1, sizeof(double2), hipMemcpyHostToDevice, c->stream));
@@ -494,6 +518,7 @@ static int apply_test_opts(sm_ctx *c) {
             c->racfg.fold = iv;
         } else if (k == "rev") {
             c->racfg.rev_odd = iv;
+
         } else if (k == "link_angles") {
             c->link_angles = iv ? 1 : 0;
         } else if (k == "bt") {
@@ -605,7 +630,10 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
         const bool hot = i == F_D || i == F_D2 || i == F_R || i == F_X;
         chk(hipMalloc(&c->fields[i], hot ? stream_alloc_bytes(fb) : fb));
     }
-    c->x_internal = stream_alloc_bytes(fb) != fb;
+    // the passes update F_X (placed as above) on every field from 256 MiB up,
+    // including fields that are themselves a power of two >= 2 GiB (8192^2 on
+    // one GPU): the caller's x is wherever its allocator put it
+    c->x_internal = fb >= (size_t(256) << 20);
     chk(hipMalloc(&c->faces, sizeof(double2) * 2 * (size_t)Nx * 8));
     chk(hipMalloc(&c->faces2, sizeof(double2) * 56 * (size_t)Nx));
     chk(hipMalloc(&c->faces4, sizeof(double2) * 64 * (size_t)Nx));
@@ -738,7 +766,27 @@ int sm_tune_cg_geometry(sm_ctx *c, int waves_per_block, int xchunk) {
     return SM_OK;
 }
 
-int sm_cg_link_angles(sm_ctx *c, int on, int *in_use) {
+int sm_cg_link_angles(sm_ctx *c, int on, int *in_use) { return sm_cg_link_codes(c, on, in_use); }
+
+int sm_link_code_check(sm_ctx *c, double *U_out, double *max_err, long *n_bad) {
+    TRY(check_ready(c));
+    if (!max_err || !n_bad) return fail(SM_ERR_ARG, "null argument");
+    // per block: (links beyond the bound, largest error)
+    const int nb = launch_link_code_check(c->stream, 2 * c->g.V, c->U, (double2 *)U_out, c->partials);
+    std::vector<double2> h(nb);
+    HIP_TRY(hipMemcpyAsync(h.data(), c->partials, sizeof(double2) * nb, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    double bad = 0.0, mx = 0.0;
+    for (const double2 &b : h) {
+        bad += b.x;
+        mx = b.y > mx || b.y != b.y ? b.y : mx;  // a NaN error stays NaN
+    }
+    *n_bad = (long)bad;
+    *max_err = mx;
+    return SM_OK;
+}
+
+int sm_cg_link_codes(sm_ctx *c, int on, int *in_use) {
     if (!c) return fail(SM_ERR_ARG, "null context");
     if (on >= 0 && (on ? 1 : 0) != c->link_angles) {
         c->link_angles = on ? 1 : 0;

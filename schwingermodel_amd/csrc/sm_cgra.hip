@@ -147,11 +147,40 @@ __device__ __forceinline__ RSrc<T> rsrc(const T *base, const T *face, int c, con
 // commutes exactly with the rounded products and sums, so C = sl0 * that
 // product equals the folded form's (U*sl0)^* combo up to the sign of an exact
 // zero: the values are dirac_site_folded's.
+//
+// FOLD = 2 also takes its links pre-scaled (ra_march): U_t by -sr0/2 and U_x
+// by -1/2, so A, B, C, E come out as -h/2's terms exactly (a power-of-two and
+// sign scale commutes with every rounding) and the output is ONE fma,
+// mass p + (-h/2), instead of a product and an fma. The backward hop's sign
+// needs no product either: the receiving lane's SignL is -1 exactly when the
+// sending lane t - 1 is at global t = Nt - 1, i.e. when the sender's SignR is,
+// so the sender's scaled U_t already carries it. 8 fp64 operations less per
+// stage.
 template <int FOLD, int DAG>
 __device__ __forceinline__ Sp ra_site(double mass, double sr0, double sl0, const Sp &p, const Sp &pxm, const Sp &pxp,
                                       double2 ut, double2 ux, double2 uxm) {
     Sp o;
-    if (FOLD) {
+    if (FOLD == 2) {  // pre-scaled links: ut = -sr0 U_t / 2, ux = -U_x / 2, uxm = -U_x(x-1) / 2
+        const double2 qf = DAG ? cadd(p.a, p.b) : csub(p.a, p.b);
+        const double2 qb = DAG ? csub(p.a, p.b) : cadd(p.a, p.b);
+        const double2 C = dpp_shr1(cm<FOLD>(make_double2(ut.x, -ut.y), qb));  // lane t-1's -sl0 conj(U_t) qb / 2
+        const double2 A = cm<FOLD>(ut, dpp_shl1(qf));
+        const double2 e = make_double2(uxm.x, -uxm.y);
+        double2 h0, h1;  // -h / 2
+        if (!DAG) {
+            const double2 B = cm<FOLD>(ux, make_double2(pxp.a.x - pxp.b.y, pxp.a.y + pxp.b.x));
+            const double2 E = cm<FOLD>(e, make_double2(pxm.a.x + pxm.b.y, pxm.a.y - pxm.b.x));
+            h0 = cadd(cadd(cadd(A, B), C), E);
+            h1 = cadd(cadd(cadd(cneg(A), mul_mi(B)), C), mul_i(E));
+        } else {
+            const double2 E = cm<FOLD>(e, make_double2(pxm.a.x - pxm.b.y, pxm.a.y + pxm.b.x));
+            const double2 B = cm<FOLD>(ux, make_double2(pxp.a.x + pxp.b.y, pxp.a.y - pxp.b.x));
+            h0 = cadd(cadd(cadd(C, E), A), B);
+            h1 = cadd(cadd(cadd(cneg(C), mul_mi(E)), A), mul_i(B));
+        }
+        o.a = make_double2(__builtin_fma(mass, p.a.x, h0.x), __builtin_fma(mass, p.a.y, h0.y));
+        o.b = make_double2(__builtin_fma(mass, p.b.x, h1.x), __builtin_fma(mass, p.b.y, h1.y));
+    } else if (FOLD) {
         const double2 qf = DAG ? cadd(p.a, p.b) : csub(p.a, p.b);  // forward-hop combination at this site
         const double2 qb = DAG ? csub(p.a, p.b) : cadd(p.a, p.b);  // backward-hop combination at this site
         const double2 Cb = cm<FOLD>(make_double2(ut.x, -ut.y), qb);  // conj(U_t) * qb, for lane t+1
@@ -203,6 +232,13 @@ __device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x
                                          double2 beta, double2 alpha2, double2 beta2, double2 *rlds,
                                          double2 &acc_dA, double2 &acc_rA, double2 &acc_n) {
     const int Nx = a.Nx, Wt = a.Wt;
+    // The wave owns columns [g RW, g RW + RW): its stores (lanes RH .. RW+RH-1)
+    // start on a 128-B line (RW double2 = 7 lines), its 64-lane loads 64 B
+    // before one (9 lines per row and plane). Shifting the window by RH so
+    // the loads cover 8 lines misaligns the stores instead: 154.5 against
+    // 153.3 B/site of counter bytes and 2092 against 2205 it/s (round 4,
+    // interleaved bench.py, profiles/r04_a_window_shift_ab.jsonl). Partial
+    // line writes cost more than a ninth line read through L2.
     const int c = g * RW - RH + lane;
     const bool own = lane >= RH && lane < RW + RH && c < Wt;
     int tg = (a.t0 + c) % a.Ntg;
@@ -243,6 +279,16 @@ __device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x
         if constexpr (UC != 0) return u_of(v);
         else return v;
     };
+    // FOLD 2 takes pre-scaled links (ra_site): U_t by -sr0/2, U_x by -1/2
+    const double kt = FOLD == 2 ? -0.5 * sr0 : 1.0, kx = FOLD == 2 ? -0.5 : 1.0;
+    auto cvt = [&](LU v) -> double2 {
+        const double2 u = cvu(v);
+        return FOLD == 2 ? make_double2(u.x * kt, u.y * kt) : u;
+    };
+    auto cvx = [&](LU v) -> double2 {
+        const double2 u = cvu(v);
+        return FOLD == 2 ? make_double2(u.x * kx, u.y * kx) : u;
+    };
     auto ld2 = [&](int xr, Sp &q, Sp &xv) {
         const double2 *p = S2.p + (long)wrap(phys(min(max(xr, x0 - 2), xe + 1))) * S2.xs;
         q.a = p[0];
@@ -269,8 +315,8 @@ __device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x
     {
         LU t2, x2;
         ldu(y0 + 2, t2, x2);
-        Ut2 = cvu(t2);
-        Ux2 = cvu(x2);
+        Ut2 = cvt(t2);
+        Ux2 = cvx(x2);
     }
     ld1(y0 + 4, Ld);
     ldu(y0 + 3, Lut, Lux);
@@ -280,7 +326,7 @@ __device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x
     auto step = [&](int y, auto mtag) {
         constexpr int M = decltype(mtag)::value;
         const Sp D4 = Ld;
-        const double2 Ut3 = cvu(Lut), Ux3 = cvu(Lux);
+        const double2 Ut3 = cvt(Lut), Ux3 = cvx(Lux);
         ld1(y + 5, Ld);
         ldu(y + 4, Lut, Lux);
         __builtin_amdgcn_sched_barrier(0);  // keep the next rows' loads issued here
@@ -645,16 +691,18 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
 }
 
 // Link codes for the UC passes (sm_linkcode.h) for each of the n links (both
-// planes), and per block the count of links whose |U|^2 is off 1 by more than
-// 1e-14 (such fields keep the complex-link passes, sm_capi.cpp).
+// planes), and per block the count of links whose code does not decode to
+// within SM_LINKCODE_TOL of the stored link in both components (the pass's
+// own decoder, so the bound holds for every link the pass rebuilds; one such
+// link and the field keeps the complex-link passes, sm_capi.cpp).
 __global__ void __launch_bounds__(256) link_code_kernel(long n, const double2 *U, double *Ua, double2 *part) {
     __shared__ double2 sh[4];
     double bad = 0.0;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
         const double2 u = U[i];
-        Ua[i] = sm_link_encode(u.x, u.y);
-        const double m = u.x * u.x + u.y * u.y - 1.0;
-        if (!(fabs(m) <= 1e-14)) bad += 1.0;  // NaN counts as off the circle
+        const double e = sm_link_encode(u.x, u.y);
+        Ua[i] = e;
+        if (!sm_link_code_ok(u.x, u.y, e)) bad += 1.0;  // NaN links too
     }
     const double2 b = block_sum(make_double2(bad, 0.0), sh);
     if (threadIdx.x == 0) part[blockIdx.x] = b;
@@ -663,6 +711,37 @@ __global__ void __launch_bounds__(256) link_code_kernel(long n, const double2 *U
 int launch_link_codes(hipStream_t s, long n, const double2 *U, double *Ua, double2 *partials) {
     const int nb = reduce_blocks(n);
     hipLaunchKernelGGL(link_code_kernel, dim3(nb), dim3(256), 0, s, n, U, Ua, partials);
+    return nb;
+}
+
+__global__ void __launch_bounds__(256) link_code_check_kernel(long n, const double2 *U, double2 *out,
+                                                             double2 *part) {
+    __shared__ double2 sh[4];
+    __shared__ double shm[256];
+    double bad = 0.0, mx = 0.0;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const double2 u = U[i];
+        const double e = sm_link_encode(u.x, u.y);
+        double c2, s2;
+        sm_link_decode(e, &c2, &s2);
+        if (out) out[i] = make_double2(c2, s2);
+        const double err = fmax(fabs(c2 - u.x), fabs(s2 - u.y));
+        if (!sm_link_code_ok(u.x, u.y, e)) bad += 1.0;
+        mx = err > mx || err != err ? err : mx;
+    }
+    shm[threadIdx.x] = mx;
+    const double2 b = block_sum(make_double2(bad, 0.0), sh);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double m = 0.0;
+        for (int t = 0; t < (int)blockDim.x; ++t) m = shm[t] > m || shm[t] != shm[t] ? shm[t] : m;
+        part[blockIdx.x] = make_double2(b.x, m);
+    }
+}
+
+int launch_link_code_check(hipStream_t s, long n, const double2 *U, double2 *out, double2 *partials) {
+    const int nb = reduce_blocks(n);
+    hipLaunchKernelGGL(link_code_check_kernel, dim3(nb), dim3(256), 0, s, n, U, out, partials);
     return nb;
 }
 

@@ -164,27 +164,17 @@ int main(int argc, char **argv) {
         Datfile << std::setw(30) << max_iter << std::setw(30) << std::setprecision(17) << tol << "\n";
         Datfile << "#m0\n" << std::setw(30) << std::setprecision(17) << m0 << "\n";
         Datfile.close();
-        std::cout << "**********************************************************************" << std::endl;
-        std::cout << "*                              PARAMETERS" << std::endl;
-        std::cout << "* Nx = " << Nx << ", Nt = " << Nt << std::endl;
-        std::cout << "* m0 = " << m0 << ", kappa = " << 1 / (2 * (m0 + 2)) << std::endl;
-        std::cout << "* beta = " << beta << std::endl;
-        std::cout << "* Thermalization confs = " << Ntherm << std::endl;
-        std::cout << "* Measurement confs = " << Nmeas << std::endl;
-        std::cout << "* Decorrelation steps (confs dropped between measurements) = " << Nsteps << std::endl;
-        std::cout << "* Trajectory length = " << trajectory_length << ", Leapfrog steps = " << MD_steps
-                  << ", Integration step = " << trajectory_length / MD_steps << std::endl;
-        std::cout << "* CG max iterations = " << max_iter << ", CG tolerance = " << tol << std::endl;
-        std::cout << "* Number of ranks on x = " << ranks_x << ", Number of ranks on t = " << ranks_t << std::endl;
-        std::cout << "* Total number of MPI ranks = " << size << std::endl;
+        // One-line run summary (key=value, for logs); the SimData file above
+        // is the interface other tools read.
         long V = 0;
         sm_local_sites(ctx, &V, nullptr, nullptr, nullptr);
-        std::cout << "* Each rank has " << V << " lattice sites" << std::endl;
-        std::cout << "* Host: " << (hostname ? hostname : "unknown") << std::endl;
-        std::cout << "* Start time: " << start_time_str << std::endl;
-        std::cout << "* Seed (counter-based draws) = " << seed << ", GPUs = " << size
-                  << (even_odd ? ", even-odd preconditioned action" : "") << std::endl;
-        std::cout << "**********************************************************************" << std::endl;
+        std::cout << "sm_hmc run: lattice=" << Nx << "x" << Nt << " m0=" << m0 << " kappa=" << 1 / (2 * (m0 + 2))
+                  << " beta=" << beta << " therm=" << Ntherm << " meas=" << Nmeas << " skip=" << Nsteps
+                  << " tau=" << trajectory_length << " md_steps=" << MD_steps
+                  << " eps=" << trajectory_length / MD_steps << " cg_max_iter=" << max_iter << " cg_tol=" << tol
+                  << " ranks=" << ranks_x << "x" << ranks_t << " sites_per_rank=" << V
+                  << " action=" << (even_odd ? "even-odd" : "full") << " seed=" << seed
+                  << " host=" << (hostname ? hostname : "unknown") << " start=" << start_time_str << std::endl;
     }
 
     sm_hmc_params p;

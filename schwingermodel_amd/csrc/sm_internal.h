@@ -151,10 +151,15 @@ constexpr int kMaxTickGroups = 1024;
 // faces, lo at fsend and hi at fsend + 8 Nx, as launch_pack_faces_k would)
 // Link codes of U for the passes above (Uang: 16 instead of 32 B/site of
 // links, sm_linkcode.h): writes the one-double code of n links and, per block,
-// the count of links off the unit circle (> 1e-14 in |U|^2) to partials;
+// the count of links whose code does not rebuild them to within
+// SM_LINKCODE_TOL (sm_linkcode.h) to partials;
 // returns the block count.
 int launch_link_codes(hipStream_t s, long n, const double2 *U, double *Ua, double2 *partials);
 void launch_codes_of(hipStream_t s, long n, const double2 *U, double *Ua);  // faces: codes only
+// Diagnostic: encode + decode each of n links (the pass's functions) into
+// out (may be null); per block (count beyond SM_LINKCODE_TOL, largest
+// per-component error) to partials; returns the block count.
+int launch_link_code_check(hipStream_t s, long n, const double2 *U, double2 *out, double2 *partials);
 // Recompute-Ad CG: after the last pass add alpha_{k-1} d_{k-1} to the rows
 // whose x update is still pending (parity != k & 1; x row = site / Wt).
 void launch_cg_ra_finish_x(hipStream_t s, const Geometry &g, double2 *x, const double2 *d0, const double2 *d1,

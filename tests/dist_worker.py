@@ -332,10 +332,15 @@ def run_angles(name, result_path, dist, rank, world):
     collective on t-shards. name = gen:<Nx>x<Nt>:<sigma>:<m0>:<wish>
     where wish is one 0/1 digit per rank for sm_cg_link_angles. Each rank
     solves twice (the second solve re-decides after U is re-uploaded) and
-    reports (converged, iterations, in_use) per solve; nothing may hang."""
+    reports (converged, iterations, in_use) per solve; nothing may hang.
+    With a sixth field (gen:...:<wish>:<wish2>) the ranks set
+    wish2 between the solves and do NOT re-upload U, so only the ranks whose
+    wish changed have stale codes at the second solve."""
     import schwingermodel_amd as sm
     from schwingermodel_amd import dist as smd
-    _, dims, sigma, m0s, wish = name.split(":")
+    parts = name.split(":")
+    _, dims, sigma, m0s, wish = parts[:5]
+    wish2 = parts[5] if len(parts) > 5 else None
     Nx, Nt = (int(v) for v in dims.split("x"))
     sigma, m0 = float(sigma), float(m0s)
     S = Nx * Nt
@@ -350,8 +355,11 @@ def run_angles(name, result_path, dist, rank, world):
     sm.check(sm.lib.sm_tune_cg(ctx, 5, 0))
     sm.check(sm.lib.sm_cg_link_angles(ctx, int(wish[rank]), None))
     out = []
-    for _ in range(2):
-        sm.check(sm.lib.sm_upload_gauge(ctx, P_(U[0]), P_(U[1])))
+    for k in range(2):
+        if k == 0 or wish2 is None:
+            sm.check(sm.lib.sm_upload_gauge(ctx, P_(U[0]), P_(U[1])))
+        else:
+            sm.check(sm.lib.sm_cg_link_angles(ctx, int(wish2[rank]), None))
         x0, x1 = np.empty(Nx * Wt.value, complex), np.empty(Nx * Wt.value, complex)
         res = sm.CGResult()
         sm.check(sm.lib.sm_cg(ctx, P_(p[0]), P_(p[1]), P_(x0), P_(x1), m0, 1e-10, 10000, ctypes.byref(res)))

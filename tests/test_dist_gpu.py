@@ -159,3 +159,22 @@ def test_link_angle_choice_is_collective(tmp_path, wish, expect):
     assert all(conv == 1 for conv, it, used in solves), rep
     assert len({it for conv, it, used in solves}) == 1, rep
     assert all(used == expect for conv, it, used in solves), rep
+
+
+@pytest.mark.parametrize("wish,wish2", [("11", "01"), ("01", "11"), ("11", "10"), ("00", "10")])
+def test_link_angle_toggle_on_one_rank(tmp_path, wish, wish2):
+    """one rank changes its sm_cg_link_angles wish between two
+    solves WITHOUT a new gauge upload, so only that rank's codes are stale at
+    the second solve. Every rank still takes part in the same collectives
+    (a stale-count all-reduce at every t-shard solve, then the decision), so
+    nothing hangs or mixes sums: both solves converge in one iteration count
+    on every rank, and the second uses the codes iff every rank asks."""
+    rep = run_world("angles", f"gen:64x512:0.3246:-0.05:{wish}:{wish2}", 2, tmp_path, timeout=120)
+    first = [r[0] for r in rep["solves"]]
+    second = [r[1] for r in rep["solves"]]
+    assert all(conv == 1 for conv, it, used in first + second), rep
+    for solve in (first, second):  # one count on every rank; codes or not, within 1 %
+        assert len({it for conv, it, used in solve}) == 1, rep
+    assert abs(first[0][1] - second[0][1]) <= max(1, first[0][1] // 100), rep
+    assert all(used == (1 if wish == "11" else 0) for conv, it, used in first), rep
+    assert all(used == (1 if wish2 == "11" else 0) for conv, it, used in second), rep

@@ -377,6 +377,134 @@ def test_link_angles_follow_gauge_updates(sm):
         sm.check(sm.lib.sm_cg_link_angles(L.ctx, 1, None))
 
 
+LINKCODE_TOL = 2.0 ** -51  # sm_linkcode.h SM_LINKCODE_TOL: per component, absolute
+
+
+def _code_check(sm, L, out=None):
+    err, bad = ctypes.c_double(-1.0), ctypes.c_long(-1)
+    sm.check(sm.lib.sm_link_code_check(L.ctx, out, ctypes.byref(err), ctypes.byref(bad)))
+    return err.value, bad.value
+
+
+def test_link_codes_decode_on_device_config3(sm):
+    """the codes of the bench field (config 3: 4096^2,
+    beta = 5 Gaussian theta, the counter-based generator on the device),
+    encoded and decoded ON THE DEVICE with the CG pass's own functions
+    (v_rsq_f64 seed): no link beyond the acceptance bound 2^-51 per
+    component, so the solve uses the codes (measured round 4: the largest
+    error is 2^-51 itself, 4.44e-16 -- the device-generated links sit a few
+    ulp off the circle, where the host-libm links of
+    tests/test_linkcode_host.py come back within 3.5e-16)."""
+    Nx = Nt = 4096
+    L = sm.init(Nx, Nt)
+    try:
+        sm.check(sm.lib.sm_fill_gauge_dev(L.ctx, 4321, 0.2374))
+        err, bad = _code_check(sm, L)
+        print(f"config-3 field: largest |rebuilt - stored| component {err:.3e}, links beyond 2^-51: {bad}")
+        assert bad == 0 and err <= LINKCODE_TOL, (err, bad)
+    finally:
+        L.close()
+
+
+def test_link_codes_device_decode_matches_stored_links(sm):
+    """The rebuilt links themselves, downloaded: on a generated field every
+    component is within 2^-51 of the stored link and the reported maximum
+    is the true one; on fields pushed off the unit circle (one link by 1e-15,
+    every link by a few ulp) the device flags exactly the links beyond 2^-51,
+    and the solve uses the codes iff it flags none (else x is bitwise the
+    complex-link solve's)."""
+    Nx, Nt = 96, 64
+    S = Nx * Nt
+    L = sm.init(Nx, Nt)
+    sm.check(sm.lib.sm_tune_cg(L.ctx, 5, 0))
+    P = lambda a: a.ctypes.data  # noqa: E731
+    U, psi = sm.spinor(S), sm.spinor(S)
+    sm.lib.sm_fill_gauge(11, 0.4, Nt, 0, Nx, 0, Nt, P(U.mu0), P(U.mu1))
+    sm.lib.sm_fill_spinor(13, Nt, 0, Nx, 0, Nt, P(psi.mu0), P(psi.mu1))
+    hip = _Hip()
+    rng = np.random.default_rng(7)
+    drift = U.copy()
+    f = 1.0 + rng.integers(-6, 7, 2 * S) * 2.0 ** -53  # |U|^2 - 1 up to ~1.3e-15
+    drift.mu0 *= f[:S]
+    drift.mu1 *= f[S:]
+    one = U.copy()
+    one.mu0[123] *= 1.0 + 1e-15
+    try:
+        for field, expect_clean in ((U, True), (one, False), (drift, None)):
+            host = np.concatenate([field.mu0, field.mu1])
+            dU = hip.upload(host)
+            dout = hip.upload(np.zeros(2 * S, dtype=np.complex128))
+            sm.check(sm.lib.sm_upload_gauge_dev(L.ctx, dU))
+            err, bad = _code_check(sm, L, dout)
+            back = hip.download(dout, np.empty(2 * S, dtype=np.complex128))
+            comp = np.maximum(np.abs(back.real - host.real), np.abs(back.imag - host.imag))
+            assert err == comp.max(), (err, comp.max())
+            assert bad == int((comp > LINKCODE_TOL).sum()), (bad, int((comp > LINKCODE_TOL).sum()))
+            if expect_clean is True:
+                assert bad == 0 and err <= LINKCODE_TOL, err
+            if expect_clean is False:
+                assert bad >= 1
+            # the solve: codes iff no link is flagged
+            xs = {}
+            for on in (1, 0):
+                sm.check(sm.lib.sm_cg_link_codes(L.ctx, on, None))
+                x = sm.spinor(S)
+                assert sm.conjugate_gradient(field, psi, x, -0.1) == 1
+                u = ctypes.c_int(-1)
+                sm.check(sm.lib.sm_cg_link_codes(L.ctx, -1, ctypes.byref(u)))
+                xs[on] = (flat(x), u.value)
+            assert xs[1][1] == (1 if bad == 0 else 0), (bad, xs[1][1])
+            if bad:
+                assert bits_equal(xs[1][0], xs[0][0])
+            else:
+                assert np.linalg.norm(xs[1][0] - xs[0][0]) / np.linalg.norm(xs[0][0]) <= 1e-12
+    finally:
+        sm.check(sm.lib.sm_cg_link_codes(L.ctx, 1, None))
+
+
+def test_link_codes_after_hmc_trajectories(sm):
+    """Links after HMC updates (U <- U exp(i eps P), src/hmc.cpp:69-99, so
+    |U| drifts by rounding): the device check and the solve's choice agree
+    (codes iff no link beyond 2^-51), and whenever the codes are used the
+    solution equals the complex-link solve's to 1e-12."""
+    Nx, Nt = 64, 64
+    S = Nx * Nt
+    L = sm.init(Nx, Nt)
+    sm.check(sm.lib.sm_tune_cg(L.ctx, 5, 0))
+    prm = sm.HMCParams(m0=0.0, beta=2.0, tau=1.0, md_steps=10, cg_tol=1e-10, cg_max_iter=10000, seed=99,
+                       even_odd=0)
+    P = lambda a: a.ctypes.data  # noqa: E731
+    U, psi = sm.spinor(S), sm.spinor(S)
+    sm.lib.sm_fill_gauge(4321, 0.4242, Nt, 0, Nx, 0, Nt, P(U.mu0), P(U.mu1))
+    sm.lib.sm_fill_spinor(13, Nt, 0, Nx, 0, Nt, P(psi.mu0), P(psi.mu1))
+    sm.check(sm.lib.sm_upload_gauge(L.ctx, P(U.mu0), P(U.mu1)))
+    seen = []
+    try:
+        for block in range(3):
+            for t in range(10):
+                res = sm.HMCResult()
+                sm.check(sm.lib.sm_hmc_trajectory(L.ctx, ctypes.byref(prm), 10 * block + t, ctypes.byref(res)))
+            err, bad = _code_check(sm, L)
+            cur = sm.spinor(S)
+            sm.check(sm.lib.sm_download_gauge(L.ctx, P(cur.mu0), P(cur.mu1)))
+            xs = {}
+            for on in (1, 0):
+                sm.check(sm.lib.sm_cg_link_codes(L.ctx, on, None))
+                x = sm.spinor(S)
+                assert sm.conjugate_gradient(cur, psi, x, 0.0) == 1
+                u = ctypes.c_int(-1)
+                sm.check(sm.lib.sm_cg_link_codes(L.ctx, -1, ctypes.byref(u)))
+                xs[on] = (flat(x), u.value)
+            assert xs[1][1] == (1 if bad == 0 else 0), (bad, err)
+            if bad == 0:
+                assert err <= LINKCODE_TOL
+                assert np.linalg.norm(xs[1][0] - xs[0][0]) / np.linalg.norm(xs[0][0]) <= 1e-12
+            seen.append((err, bad))
+    finally:
+        sm.check(sm.lib.sm_cg_link_codes(L.ctx, 1, None))
+    print("link-code check after 10/20/30 trajectories (max err, links beyond 2^-51):", seen)
+
+
 @pytest.mark.parametrize("wpb,xchunk", [(1, 0), (2, 0), (1, 5), (2, 64), (4, 40), (1, 300)])
 def test_recompute_launch_geometries_agree(sm, wpb, xchunk):
     """The recompute-Ad pass under every launch geometry sm_tune_cg_geometry

@@ -1,11 +1,25 @@
 """The compact-link CG pass stores each U(1) link as one double and rebuilds it
-with schwingermodel_amd/csrc/sm_linkcode.h. The header is plain C as well:
-compiled here for the host (gcc, explicit fma, no contraction) it runs the
-device's arithmetic (sqrt and fma are correctly rounded on both). Over unit
-links of every quadrant, the axes and the diagonal ties, the rebuilt link is
-within 3 ulp per component of the stored one and within 3.5e-16 absolute."""
+with schwingermodel_amd/csrc/sm_linkcode.h. The header is plain C as well and
+is compiled here for the host (gcc, explicit fma, no contraction).
+
+The host build is NOT bit-for-bit the device's: the device seeds the square
+root with the hardware reciprocal square root (v_rsq_f64, __builtin_amdgcn_rsq),
+the host with 1 / sqrt. The refinement (one Goldschmidt and one Newton step)
+absorbs a seed error far larger than the hardware's, which the host models
+with SM_LC_HOST_SEED_PERTURB (a relative 2^-22 either way, and none). The
+device's own decode is checked on the device (tests/test_gpu_parity.py,
+test_link_codes_*). Here, for each seed model:
+  * unit links of every quadrant, the axes and the diagonal ties come back
+    within 3 ulp per component and 3.5e-16 absolute;
+  * links off the unit circle by delta = | |U|^2 - 1 | come back within
+    3.5e-16 + 0.71 delta (the decoder puts them back on the circle), and the
+    acceptance test sm_link_code_ok passes exactly the links whose rebuilt
+    components are within SM_LINKCODE_TOL = 2^-51 of the stored ones.
+"""
 import os
 import subprocess
+
+import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -20,8 +34,8 @@ static double ulps(double a, double b) {
     return fabs(a - b) / u;
 }
 int main(void) {
-    double mu = 0.0, ma = 0.0;
-    long bad_sign = 0;
+    double mu = 0.0, ma = 0.0, worst_excess = -1.0;
+    long bad_sign = 0, gate_mismatch = 0, accepted_off = 0, rejected_off = 0;
     const double special[] = {0.0, -0.0, M_PI, -M_PI, M_PI / 2, -M_PI / 2, M_PI / 4, -M_PI / 4,
                               3 * M_PI / 4, -3 * M_PI / 4, 1e-300, -1e-20};
     const long n = 4000000;
@@ -31,7 +45,8 @@ int main(void) {
         if (i >= 12 && i < 4000) th = nextafter(((i % 9) - 4) * M_PI_4, (i & 1) ? INFINITY : -INFINITY);
         const double c = cos(th), s = sin(th);
         double c2, s2;
-        sm_link_decode(sm_link_encode(c, s), &c2, &s2);
+        const double e = sm_link_encode(c, s);
+        sm_link_decode(e, &c2, &s2);
         /* ulps against the larger of the component and 2^-53 (a link's scale is 1) */
         const double uc = fabs(c) > 0x1p-2 ? ulps(c2, c) : fabs(c2 - c) / 0x1p-55;
         const double us = fabs(s) > 0x1p-2 ? ulps(s2, s) : fabs(s2 - s) / 0x1p-55;
@@ -40,21 +55,50 @@ int main(void) {
         const double a = fmax(fabs(c2 - c), fabs(s2 - s));
         if (a > ma) ma = a;
         if ((c != 0.0 && signbit(c2) != signbit(c)) || (s != 0.0 && signbit(s2) != signbit(s))) ++bad_sign;
+        if (sm_link_code_ok(c, s, e) != (a <= SM_LINKCODE_TOL)) ++gate_mismatch;
+        /* the same link scaled off the circle by 1 + k 2^-53, k in [-40, 40] */
+        if (i < 400000) {
+            const double k = (double)((i * 7919) % 81 - 40);
+            const double f = 1.0 + k * 0x1p-53;
+            const double cf = c * f, sf = s * f;
+            const double delta = (double)fabsl((long double)cf * cf + (long double)sf * sf - 1.0L);  /* ~exact */
+            const double ef = sm_link_encode(cf, sf);
+            double c3, s3;
+            sm_link_decode(ef, &c3, &s3);
+            const double af = fmax(fabs(c3 - cf), fabs(s3 - sf));
+            const double excess = af - (3.5e-16 + 0.71 * delta);
+            if (excess > worst_excess) worst_excess = excess;
+            const int ok = sm_link_code_ok(cf, sf, ef);
+            if (ok != (af <= SM_LINKCODE_TOL)) ++gate_mismatch;
+            if (delta > 1.6e-15) { if (ok) ++accepted_off; else ++rejected_off; }
+        }
     }
-    printf("%.6f %.6e %ld\n", mu, ma, bad_sign);
+    const double nanc = 0.0 / 0.0;
+    if (sm_link_code_ok(nanc, 0.5, sm_link_encode(nanc, 0.5))) ++gate_mismatch;
+    if (sm_link_code_ok(0.5, INFINITY, sm_link_encode(0.5, INFINITY))) ++gate_mismatch;
+    printf("%.6f %.6e %ld %ld %.6e %ld %ld\n", mu, ma, bad_sign, gate_mismatch, worst_excess, accepted_off,
+           rejected_off);
     return 0;
 }
 """
 
 
-def test_link_code_round_trip(tmp_path):
+@pytest.mark.parametrize("perturb", [None, "0x1p-22", "-0x1p-22"], ids=["exact_seed", "seed_hi", "seed_lo"])
+def test_link_code_round_trip(tmp_path, perturb):
     src = tmp_path / "drv.c"
     src.write_text(DRIVER)
     exe = tmp_path / "drv"
-    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-I", os.path.join(REPO, "schwingermodel_amd", "csrc"),
-                    str(src), "-o", str(exe), "-lm"], check=True)
+    cmd = ["gcc", "-O2", "-ffp-contract=off", "-I", os.path.join(REPO, "schwingermodel_amd", "csrc"),
+           str(src), "-o", str(exe), "-lm"]
+    if perturb:
+        cmd.insert(1, f"-DSM_LC_HOST_SEED_PERTURB={perturb}")
+    subprocess.run(cmd, check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
-    mu, ma, bad_sign = float(out[0]), float(out[1]), int(out[2])
+    mu, ma, bad_sign, gate_mismatch = float(out[0]), float(out[1]), int(out[2]), int(out[3])
+    worst_excess, accepted_off, rejected_off = float(out[4]), int(out[5]), int(out[6])
     assert mu <= 3.0, mu
     assert ma <= 3.5e-16, ma
     assert bad_sign == 0
+    assert gate_mismatch == 0
+    assert worst_excess <= 0.0, worst_excess     # 3.5e-16 + 0.71 delta holds off the circle
+    assert accepted_off == 0 and rejected_off > 0, (accepted_off, rejected_off)  # delta > 1.6e-15 (error >= delta / 2 - 3.5e-16): never accepted

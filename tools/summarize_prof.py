@@ -43,7 +43,15 @@ def main():
     ap.add_argument("--nt", type=int, default=4096)
     ap.add_argument("--tag", default="")
     ap.add_argument("--suffix", default="", help="input dirs prof_stats<suffix> etc. (tools/gpu_round.sh writes _<tag>)")
+    ap.add_argument("--build-id", default=None,
+                    help="sm_build_id() of the profiled library (default: the in-tree libsm_hip.so, which is the "
+                         "one gpurun shipped as long as nothing was rebuilt since)")
     a = ap.parse_args()
+    if a.build_id is None:
+        import ctypes
+        lib = ctypes.CDLL(os.path.join(REPO, "schwingermodel_amd", "libsm_hip.so"))
+        lib.sm_build_id.restype = ctypes.c_char_p
+        a.build_id = lib.sm_build_id().decode()
     pdir = os.path.join(REPO, "profiles")
     os.makedirs(pdir, exist_ok=True)
     tag = f"{a.round}{a.tag}"
@@ -72,7 +80,8 @@ def main():
     # the CG pass behind bench.py's value: one shard, x rows, fused multiply-
     # adds, in-kernel scalars off, link angles, ticketed tail (sm_cgra.hip)
     cgk = [k for k in kernels if "cg_ra_kernel<0, 1, 2, 0, 1, 1" in k]  # any march-schedule suffix
-    out = {"Nx": a.nx, "Nt": a.nt, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes",
+    out = {"Nx": a.nx, "Nt": a.nt, "build_id": a.build_id,
+           "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes",
            "correction": "reads = 2 x FETCH_SIZE KiB (gfx950), writes = WRITE_SIZE KiB",
            "algorithmic_bytes_per_launch": 96 * sites,
            "dslash_kernel": dslash[0] if dslash else None,
