@@ -46,8 +46,9 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_SITE_APPLY = 96  # read psi 32 + U 32, write 32
 # algorithmic HBM bytes per site of one CG iteration, by path
 BYTES_PER_SITE_CG = {"recompute": 160, "twodir": 224, "sixkernel": 576}
-# the recompute-Ad pass reading the links as angles (sm_cg_link_angles): U is
-# 16 instead of 32 B/site of every pass
+# the recompute-Ad pass reading the links as one-double codes (sm_cg_link_codes,
+# csrc/sm_linkcode.h; sm_cg_link_angles is its round-2 name): U is 16 instead
+# of 32 B/site of every pass
 BYTES_PER_SITE_CG_ANGLES = 144
 CG_PATH_ID = {"recompute": 5, "twodir": 4, "sixkernel": 0}
 
@@ -85,8 +86,8 @@ def parse(argv=None):
                     help="seconds before a rank that has not finished (e.g. stuck in ncclCommInitRank or a "
                          "mismatched collective) dumps its stacks and exits 124; the spawner then ends the others")
     ap.add_argument("--no-link-angles", action="store_true",
-                    help="recompute-Ad CG reads the complex links (160 B/site) instead of their angles "
-                         "(144; the default from 4M sites per shard)")
+                    help="recompute-Ad CG reads the complex links (160 B/site) instead of their one-double "
+                         "codes (144; the default from 4M sites per shard)")
     return ap.parse_args(argv)
 
 
@@ -385,8 +386,8 @@ def cg_bytes_per_site(sh, cg_path):
 
 
 def begin_cg(sh, m0, cg_path, link_angles_off=False):
-    """sm_cg_begin of the timed solve (x0 = phi, r0, d0; the link angles are
-    built here, with a host read of their check): CG setup, not timed."""
+    """sm_cg_begin of the timed solve (x0 = phi, r0, d0; the link codes are
+    built here, with a host read of their device check): CG setup, not timed."""
     sm = sh.sm
     sm.check(sm.lib.sm_tune_cg(sh.L.ctx, CG_PATH_ID[cg_path], 0))
     sm.check(sm.lib.sm_cg_link_angles(sh.L.ctx, 0 if link_angles_off else -1, None))  # -1: the size default

@@ -87,24 +87,107 @@ int down_rank(const sm_ctx *c) { return (c->shard - 1 + c->nshard) % c->nshard; 
 // N > 1 bench; the one-rank loopback tests cover the code path.
 ncclComm_t comm_for(const sm_ctx *c, hipStream_t s) { return s == c->comm_stream ? c->comm_side : c->comm; }
 
-// Allocation size of a buffer the CG pass streams every iteration (the three
+// Placement of the buffers the CG pass streams every iteration (the three
 // direction buffers, x, the link codes). Buffers of 256 MiB and more get an
-// allocation of their own of at least 2 GiB (a power of two), of which they
-// use the start. The CG pass at 4096^2 (tools/stride_probe.hip,
-// profiles/r03_v_stride_probe.jsonl) takes 476-493 us when its fields are
-// carved out of one pool (at every relative offset tried, 0 .. 1 GiB) or sit
-// in allocations of their own size, and 441-457 us (sometimes 468-484) in
-// allocations of 2-8 GiB; 8192^2 likewise (26.2-26.5 against 28.0-28.3
-// ps/site). Only the placement differs, not the kernel: the backing and
-// translation the memory system gives large allocations. bench.py, 3
-// interleaved pairs per box on 4 boxes (profiles/r03_w_padded_alloc_ab.jsonl):
-// 2230 / 2248 against 2091 / 2082 it/s where the old layout ran slow, equal
-// where it happened to run fast.
-size_t stream_alloc_bytes(size_t bytes) {
+// allocation of their own of at least 2 GiB (a power of two), requested as
+// physically contiguous, of which they use the start. The pass runs at one of
+// two speeds depending on where the driver puts them (4096^2: ~456 against
+// ~477 us per pass). Round 3 found that >= 2 GiB allocations reach the fast
+// state where own-size ones and carved pools do not
+// (profiles/r03_v_stride_probe.jsonl, r03_w_padded_alloc_ab.jsonl). Round 4
+// (DESIGN §2): it is not address translation (zero UTCL1 misses either way,
+// profiles/r04_b_alloc_counters.jsonl); the fast state issues the same reads
+// with the same mean residency but keeps 5 % more in flight, with 8.5 %
+// fewer DRAM-credit stall cycles (r04_c_alloc_rule_ab.jsonl). Over 60
+// contexts on three boxes (tools/alloc_trials.py, r04_e_alloc_trials.jsonl)
+// the >= 2 GiB allocations WITH the contiguous flag were the fastest rule on
+// every box (2273 / 2172 it/s mean against 2193 / 2135 without the flag);
+// own size, own-size physical memory at 2 GiB-aligned addresses, >= 1 GiB
+// contiguous and one contiguous pool of exactly the buffers' size never
+// reached the fast state.
+size_t stream_alloc_bytes(size_t bytes, size_t floor_bytes = size_t(2) << 30) {
     if (bytes < (size_t(256) << 20)) return bytes;
-    size_t a = size_t(2) << 30;
+    size_t a = floor_bytes;
     while (a < bytes) a <<= 1;
     return a;
+}
+
+static hipError_t contiguous_or_plain(void **p, size_t bytes) {
+    if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
+    (void)hipGetLastError();  // clear the failed request's error state
+    return hipMalloc(p, bytes);
+}
+
+// Allocate a streamed CG buffer by the context's placement rule (sm_ctx
+// pad_alloc; the alternatives are test options for the measurements above).
+static hipError_t stream_malloc(sm_ctx *c, void **p, size_t bytes) {
+    if (bytes < (size_t(256) << 20) || c->pad_alloc == 0) return hipMalloc(p, bytes);
+    switch (c->pad_alloc) {
+        case 2: return hipMalloc(p, stream_alloc_bytes(bytes, size_t(1) << 30));
+        // contiguous requests fall back to a plain allocation of the same size
+        // when the driver cannot find contiguous memory
+        case 3: return contiguous_or_plain(p, bytes);
+        case 5: return contiguous_or_plain(p, stream_alloc_bytes(bytes));
+        case 6: return contiguous_or_plain(p, stream_alloc_bytes(bytes, size_t(1) << 30));
+        case 7: {
+            // the three direction buffers, x and the link codes (half a field)
+            const size_t step = size_t(2) << 20, fb = (bytes + step - 1) / step * step;
+            if (!c->stream_pool) {
+                c->pool_bytes = 4 * fb + (fb / 2 + step - 1) / step * step;
+                hipError_t e = contiguous_or_plain((void **)&c->stream_pool, c->pool_bytes);
+                if (e != hipSuccess) return e;
+                c->pool_used = 0;
+            }
+            if (c->pool_used + bytes > c->pool_bytes) return hipErrorOutOfMemory;
+            *p = c->stream_pool + c->pool_used;
+            c->pool_used += (bytes + step - 1) / step * step;
+            return hipSuccess;
+        }
+        case 4: {
+            hipMemAllocationProp prop = {};
+            prop.type = hipMemAllocationTypePinned;
+            prop.location.type = hipMemLocationTypeDevice;
+            prop.location.id = c->device;
+            size_t gran = 0;
+            hipError_t e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
+            if (e != hipSuccess) return e;
+            const size_t phys = (bytes + gran - 1) / gran * gran;
+            sm_ctx::VmmMap m = {nullptr, stream_alloc_bytes(phys), phys, {}};
+            if ((e = hipMemAddressReserve(&m.ptr, m.va_bytes, size_t(2) << 30, nullptr, 0)) != hipSuccess) return e;
+            if ((e = hipMemCreate(&m.handle, phys, &prop, 0)) != hipSuccess) {
+                (void)hipMemAddressFree(m.ptr, m.va_bytes);
+                return e;
+            }
+            hipMemAccessDesc acc = {};
+            acc.location = prop.location;
+            acc.flags = hipMemAccessFlagsProtReadWrite;
+            if ((e = hipMemMap(m.ptr, phys, 0, m.handle, 0)) != hipSuccess ||
+                (e = hipMemSetAccess(m.ptr, phys, &acc, 1)) != hipSuccess) {
+                (void)hipMemUnmap(m.ptr, phys);
+                (void)hipMemRelease(m.handle);
+                (void)hipMemAddressFree(m.ptr, m.va_bytes);
+                return e;
+            }
+            c->vmm.push_back(m);
+            *p = m.ptr;
+            return hipSuccess;
+        }
+        default: return hipMalloc(p, stream_alloc_bytes(bytes));
+    }
+}
+
+static void stream_free(sm_ctx *c, void *p) {
+    if (!p) return;
+    if (c->stream_pool && (char *)p >= c->stream_pool && (char *)p < c->stream_pool + c->pool_bytes) return;
+    for (size_t i = 0; i < c->vmm.size(); ++i)
+        if (c->vmm[i].ptr == p) {
+            (void)hipMemUnmap(p, c->vmm[i].phys_bytes);
+            (void)hipMemRelease(c->vmm[i].handle);
+            (void)hipMemAddressFree(p, c->vmm[i].va_bytes);
+            c->vmm.erase(c->vmm.begin() + (long)i);
+            return;
+        }
+    (void)hipFree(p);
 }
 
 int exchange_faces_on(sm_ctx *c, hipStream_t s, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi,
@@ -342,7 +425,7 @@ int ensure_link_angles(sm_ctx *c) {
         return SM_OK;
     }
     if (c->link_angles) {
-        if (!c->Uang) HIP_TRY(hipMalloc(&c->Uang, stream_alloc_bytes(sizeof(double) * 2 * (size_t)c->g.V)));
+        if (!c->Uang) HIP_TRY(stream_malloc(c, (void **)&c->Uang, sizeof(double) * 2 * (size_t)c->g.V));
         if (c->sharded() && !c->Uang_face)
             HIP_TRY(hipMalloc(&c->Uang_face, sizeof(double) * 16 * (size_t)c->g.Nx));
         const int nb = launch_link_codes(c->stream, 2 * c->g.V, c->U, c->Uang, c->partials);
@@ -478,6 +561,12 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //   rev=0|1|2           recompute-Ad pass march schedule (0 all forward; 1 odd
 //                       passes backward; 2, the default, x-adjacent chunks in
 //                       opposite directions and odd passes flipped)
+//   pad_alloc=0..7      placement of the streamed CG buffers (sm_ctx.h:
+//                       5 >= 2 GiB each + contiguous flag, the default;
+//                       1 >= 2 GiB plain; 0 own size; 2 >= 1 GiB; 3 own size
+//                       contiguous; 4 own-size physical memory at a 2 GiB-
+//                       aligned address; 6 >= 1 GiB contiguous; 7 one
+//                       contiguous pool of exactly the buffers' size)
 //   link_angles=0|1     recompute-Ad pass reads the links as one-double codes
 //   bt=64|128|256       Dirac apply t-columns per block
 //   eo_fused=0, eo_cg_td=0, eo_cg_folded=1   even-odd operator / CG forms
@@ -519,6 +608,9 @@ static int apply_test_opts(sm_ctx *c) {
         } else if (k == "rev") {
             c->racfg.rev_odd = iv;
 
+        } else if (k == "pad_alloc") {
+            if (iv < 0 || iv > 7) return fail(SM_ERR_ARG, "SM_TEST_OPTS: pad_alloc must be 0..7");
+            c->pad_alloc = iv;
         } else if (k == "link_angles") {
             c->link_angles = iv ? 1 : 0;
         } else if (k == "bt") {
@@ -628,7 +720,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     for (int i = 0; i < NFIELDS; ++i) {
         // the recompute-Ad pass's three direction buffers and the x it updates
         const bool hot = i == F_D || i == F_D2 || i == F_R || i == F_X;
-        chk(hipMalloc(&c->fields[i], hot ? stream_alloc_bytes(fb) : fb));
+        chk(hot ? stream_malloc(c, (void **)&c->fields[i], fb) : hipMalloc(&c->fields[i], fb));
     }
     // the passes update F_X (placed as above) on every field from 256 MiB up,
     // including fields that are themselves a power of two >= 2 GiB (8192^2 on
@@ -713,11 +805,15 @@ int sm_destroy(sm_ctx *c) {
     if (c->comm) ncclCommDestroy(c->comm);
     for (double2 *&f : c->fields)
         if (f) {
-            (void)hipFree(f);
+            stream_free(c, f);
             f = nullptr;
         }
+    stream_free(c, c->Uang);
+    c->Uang = nullptr;
+    if (c->stream_pool) (void)hipFree(c->stream_pool);
+    c->stream_pool = nullptr;
     void *dev[] = {c->U, c->ghostU, c->faces, c->faces2, c->faces4, c->partials, c->sums, c->Fbuf, c->sc,
-                   c->U_alt, c->Pmd, c->Fmd, c->eo, c->Ucb, c->eo_faces, c->eo_faces4, c->Uang, c->Uang_face,
+                   c->U_alt, c->Pmd, c->Fmd, c->eo, c->Ucb, c->eo_faces, c->eo_faces4, c->Uang_face,
                    c->tick, c->gsum};
     for (void *p : dev)
         if (p) (void)hipFree(p);

@@ -9,6 +9,7 @@
 
 #include <cmath>
 #include <cstddef>
+#include <vector>
 
 #include "sm_internal.h"
 
@@ -76,6 +77,24 @@ struct sm_ctx {
     // use, 2 = some link is off the unit circle, so the complex links are used.
     int link_angles = 1;
     int uang_state = 0;
+    // Placement of the buffers the CG pass streams (stream_malloc): 5 = an
+    // allocation of >= 2 GiB each with hipDeviceMallocContiguous (the
+    // default; plain allocation of that size when the driver has no
+    // contiguous memory), 1 = >= 2 GiB plain (the round-3 rule), 0 = own
+    // size, 2 = >= 1 GiB, 3 = own size contiguous, 4 = own-size physical
+    // memory (hipMemCreate) mapped at a 2 GiB-aligned address, 6 = >= 1 GiB
+    // contiguous, 7 = ONE contiguous allocation of exactly the streamed
+    // buffers' size, carved in 2 MiB steps. Test option pad_alloc=N; DESIGN
+    // §2 and profiles/r04_e_alloc_trials.jsonl give the measurements.
+    int pad_alloc = 5;
+    struct VmmMap {
+        void *ptr;
+        size_t va_bytes, phys_bytes;
+        hipMemGenericAllocationHandle_t handle;
+    };
+    std::vector<VmmMap> vmm;        // pad_alloc 4 mappings (released by stream_free)
+    char *stream_pool = nullptr;    // pad_alloc 7: one contiguous allocation carved for every streamed buffer
+    size_t pool_bytes = 0, pool_used = 0;
     double *Uang = nullptr;         // 2V link codes (plane mu0 then mu1)
     double *Uang_face = nullptr;    // t-shards: codes of the 4-deep ghost links (16 Nx)
     hipStream_t own_stream = nullptr, stream = nullptr;

@@ -149,7 +149,7 @@ def test_sharded_even_odd_cg_schedules(tmp_path, red, max_iter):
 @pytest.mark.parametrize("wish,expect", [("11", 1), ("10", 0), ("01", 0), ("00", 0)])
 def test_link_angle_choice_is_collective(tmp_path, wish, expect):
     """sm_cg_link_angles is per context, but on t-shards the recompute-Ad CG
-    decides collectively (one all-reduce that every shard joins): the angles
+    decides collectively (one all-reduce that every shard joins): the codes
     are used only if every shard asks for them, so ranks that disagree take
     the same path instead of one of them skipping a collective the others
     enter. Two solves per rank (U re-uploaded in between, which

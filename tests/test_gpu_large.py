@@ -17,8 +17,9 @@ tests/test_capi_host.py).
 * D, D^dag, D D^dag, force: bitwise at the sampled sites AND the SHA-256 of
   the whole output field equals the reference's (full-field bit equality).
 * CG through the product's default path for the size (the recompute-Ad pass
-  with fused multiply-adds; from 4M sites per shard with the links read as
-  angles): the reference's iteration count (+-1 %), sampled x within 1e-12
+  with fused multiply-adds and pre-scaled links; from 4M sites per shard the
+  links read as one-double codes, csrc/sm_linkcode.h): the reference's
+  iteration count (+-1 %), sampled x within 1e-12
   relative (north_star: "CG residual matching the CPU reference to 1e-12"),
   sum of squares of x within 2e-12 relative, true residual < 1e-10.
   Reference stop rule and recurrence: src/conjugate_gradient.cpp:4-66.
