@@ -377,6 +377,19 @@ def time_applies(rt, sh, m0, n):
     return lambda: e0.elapsed_time(e1) / 1e3 / n
 
 
+def placement_report(sh):
+    """The context's placement probe (sm_placement_report): candidate sets of
+    the CG pass's streamed buffers timed at creation and the one kept."""
+    sm = sh.sm
+    fn = getattr(sm.lib, "sm_placement_report", None)
+    if fn is None:
+        return None
+    us = (ctypes.c_double * 8)()
+    n, chosen = ctypes.c_int(0), ctypes.c_int(-1)
+    sm.check(fn(sh.L.ctx, us, ctypes.byref(n), ctypes.byref(chosen)))
+    return {"sets_timed": n.value, "kept": chosen.value, "us_per_pass": [round(us[k], 1) for k in range(n.value)]}
+
+
 def cg_bytes_per_site(sh, cg_path):
     """Algorithmic bytes per site of the CG iteration the last solve ran."""
     sm = sh.sm
@@ -464,6 +477,7 @@ def run_config34(args, rt, cfg_id):
     Nx, Nt = args.nx or cfg["Nx"], args.nt or cfg["Nt"]
     m0, world, rank = cfg["m0"], rt["world"], rt["rank"]
     sh = Shard(rt, Nx, Nt, cfg["sigma"])
+    placement = placement_report(sh)
     begin_cg(sh, m0, args.cg_path, args.no_link_angles)
     apply_time = time_applies(rt, sh, m0, args.applies)
     t_cg, cg_bps = time_cg_steps(rt, sh, m0, args.cg_path, args.warmup, args.steps, args.no_link_angles, begun=True)
@@ -523,6 +537,7 @@ def run_config34(args, rt, cfg_id):
                          "traffic_bytes_per_site": round(tr[2] / V, 2) if tr and len(tr) > 2 and tr[2] else None,
                          "reference_sequence_bytes_per_site": 576},
         "weak": weak,
+        "placement_probe": placement,
     })
     print(json.dumps(line), flush=True)
 

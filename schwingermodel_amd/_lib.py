@@ -91,6 +91,7 @@ def _load():
         "sm_cg_finish": ([vp, ctypes.POINTER(CGResult)], ci),
         "sm_tune_cg": ([vp, ci, ci], ci),
         "sm_build_id": ([], ctypes.c_char_p),
+        "sm_placement_report": ([vp, vp, ctypes.POINTER(ci), ctypes.POINTER(ci)], ci),
         "sm_cg_link_codes": ([vp, ci, ctypes.POINTER(ci)], ci),
         "sm_cg_link_angles": ([vp, ci, ctypes.POINTER(ci)], ci),
         "sm_link_code_check": ([vp, vp, ctypes.POINTER(cd), ctypes.POINTER(ctypes.c_long)], ci),

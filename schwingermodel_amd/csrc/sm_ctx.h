@@ -95,6 +95,12 @@ struct sm_ctx {
     std::vector<VmmMap> vmm;        // pad_alloc 4 mappings (released by stream_free)
     char *stream_pool = nullptr;    // pad_alloc 7: one contiguous allocation carved for every streamed buffer
     size_t pool_bytes = 0, pool_used = 0;
+    // Placement probe at creation (sm_capi.cpp placement_probe): candidate
+    // sets of the streamed buffers tried, their CG-pass time (us per pass)
+    // and the one kept. Test option place_probe=N (N sets; 1 = no probe).
+    int place_probe = 5;
+    int place_n = 0, place_chosen = -1;
+    double place_us[8] = {};
     double *Uang = nullptr;         // 2V link codes (plane mu0 then mu1)
     double *Uang_face = nullptr;    // t-shards: codes of the 4-deep ghost links (16 Nx)
     hipStream_t own_stream = nullptr, stream = nullptr;

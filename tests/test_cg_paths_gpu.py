@@ -141,3 +141,36 @@ def test_placement_modes_bitwise():
         else:
             assert it == ref[0], (mode, it, ref[0])
             assert np.array_equal(x.view(np.uint64), ref[1].view(np.uint64)), mode
+
+
+def test_placement_probe_report():
+    """Context creation times candidate placements of the streamed CG
+    buffers and keeps the fastest (sm_capi.cpp placement_probe): at a shape
+    that takes the rule (4096 x 2048, 256 MiB fields) the report lists the
+    sets timed (the default 5, fewer only if the device ran short of free
+    memory), a kept set among them with the smallest time, and a solve on
+    the kept set equals the no-probe solve bitwise. Below the rule's size
+    nothing is probed."""
+    import schwingermodel_amd as sm
+
+    def report(L):
+        us = (ctypes.c_double * 8)()
+        n, k = ctypes.c_int(-1), ctypes.c_int(-2)
+        sm.check(sm.lib.sm_placement_report(L.ctx, us, ctypes.byref(n), ctypes.byref(k)))
+        return n.value, k.value, list(us)[:max(0, n.value)]
+
+    L = sm.Lattice(4096, 2048)
+    try:
+        n, k, us = report(L)
+    finally:
+        L.close()
+    assert 1 <= n <= 5 and 0 <= k < n, (n, k)
+    assert all(u > 0 for u in us) and us[k] == min(us), us
+    L = sm.Lattice(512, 512)
+    try:
+        assert report(L)[0] == 0
+    finally:
+        L.close()
+    a = solve(sm, 4096, 2048, 0.2374, 0.3, {})
+    b = solve(sm, 4096, 2048, 0.2374, 0.3, {"place_probe": 1})
+    assert a[0] == b[0] and np.array_equal(a[1].view(np.uint64), b[1].view(np.uint64))
