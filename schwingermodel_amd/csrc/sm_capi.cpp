@@ -647,8 +647,9 @@ static int apply_test_opts(sm_ctx *c) {
 // the first round discarded as warm-up), keeps the fastest set and frees the
 // others. One shard's pass shape is timed on every context (t-shards use the
 // same streams; their faces are a few rows). Only where the rule applies
-// (fields >= 256 MiB, the recompute-Ad pass with fused multiply-adds) and
-// while the device keeps 16 GiB free besides the candidates. The kept set is
+// (fields >= 256 MiB, the recompute-Ad pass with fused multiply-adds; not on
+// host-staged contexts) and while the device keeps 16 GiB free besides the
+// candidates. The kept set is
 // zeroed again afterwards (the probe's iterates are NaN), and the scalars and
 // tickets are reset. sm_placement_report returns the times and the choice.
 static int placement_probe(sm_ctx *c, size_t fb) {
@@ -656,7 +657,11 @@ static int placement_probe(sm_ctx *c, size_t fb) {
     const int K = std::min(c->place_probe, 8);
     c->place_n = 0;
     c->place_chosen = -1;
-    if (K <= 1 || c->pad_alloc == 0 || fb < (size_t(256) << 20) || c->cg_fused != 5 || c->racfg.fold < 2)
+    // not on host-staged contexts: that transport is how several shard
+    // processes share ONE GPU (tests, rehearsals), where eight probes at once
+    // would hold more transient memory than the device has
+    if (K <= 1 || c->hosted || c->pad_alloc == 0 || fb < (size_t(256) << 20) || c->cg_fused != 5 ||
+        c->racfg.fold < 2)
         return SM_OK;
     const size_t ub = sizeof(double) * 2 * (size_t)c->g.V;
     const size_t sizes[kStreams] = {fb, fb, fb, fb, ub};
