@@ -548,6 +548,7 @@ def run_config5(args, rt):
     m0, world, rank = cfg["m0"], rt["world"], rt["rank"]
     sm = None
     sh = Shard(rt, Nx, Nt, cfg["sigma"])
+    placement = placement_report(sh)
     sm = sh.sm
     sm.check(sm.lib.sm_tune_cg(sh.L.ctx, CG_PATH_ID[args.cg_path], 0))
     sm.check(sm.lib.sm_cg_link_angles(sh.L.ctx, 0 if args.no_link_angles else -1, None))
@@ -581,6 +582,7 @@ def run_config5(args, rt):
         "cg_iteration": {"path": args.cg_path, "link_angles": cg_bps == BYTES_PER_SITE_CG_ANGLES,
                          "bytes_per_site": cg_bps,
                          "achieved_GBps_per_gpu": round(cg_bps * V * res.iterations / dt / 1e9, 1)},
+        "placement_probe": placement,
     })
     print(json.dumps(line), flush=True)
     if not res.converged or not rel < 1e-9:
