@@ -130,11 +130,14 @@ static hipError_t stream_malloc(sm_ctx *c, void **p, size_t bytes) {
         case 3: return contiguous_or_plain(p, bytes);
         case 5: return contiguous_or_plain(p, stream_alloc_bytes(bytes));
         case 6: return contiguous_or_plain(p, stream_alloc_bytes(bytes, size_t(1) << 30));
-        case 7: {
-            // the three direction buffers, x and the link codes (half a field)
-            const size_t step = size_t(2) << 20, fb = (bytes + step - 1) / step * step;
+        case 7:
+        case 8: {
+            // the three direction buffers, x and the link codes (half a field);
+            // 7: packed in 2 MiB steps, 8: one 2 GiB-aligned slot each
+            const size_t step = c->pad_alloc == 8 ? stream_alloc_bytes(bytes) : size_t(2) << 20;
+            const size_t fb = (bytes + step - 1) / step * step;
             if (!c->stream_pool) {
-                c->pool_bytes = 4 * fb + (fb / 2 + step - 1) / step * step;
+                c->pool_bytes = 4 * fb + (fb / 2 + step - 1) / step * step;  // 8: 5 slots
                 hipError_t e = contiguous_or_plain((void **)&c->stream_pool, c->pool_bytes);
                 if (e != hipSuccess) return e;
                 c->pool_used = 0;
@@ -567,7 +570,8 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //                       1 >= 2 GiB plain; 0 own size; 2 >= 1 GiB; 3 own size
 //                       contiguous; 4 own-size physical memory at a 2 GiB-
 //                       aligned address; 6 >= 1 GiB contiguous; 7 one
-//                       contiguous pool of exactly the buffers' size)
+//                       contiguous pool of exactly the buffers' size; 8 one
+//                       contiguous pool of 2 GiB slots)
 //   place_probe=N       candidate placements timed at creation (1: none)
 //   link_angles=0|1     recompute-Ad pass reads the links as one-double codes
 //   bt=64|128|256       Dirac apply t-columns per block
@@ -614,7 +618,7 @@ static int apply_test_opts(sm_ctx *c) {
             if (iv < 1 || iv > 8) return fail(SM_ERR_ARG, "SM_TEST_OPTS: place_probe must be 1..8");
             c->place_probe = iv;
         } else if (k == "pad_alloc") {
-            if (iv < 0 || iv > 7) return fail(SM_ERR_ARG, "SM_TEST_OPTS: pad_alloc must be 0..7");
+            if (iv < 0 || iv > 8) return fail(SM_ERR_ARG, "SM_TEST_OPTS: pad_alloc must be 0..8");
             c->pad_alloc = iv;
         } else if (k == "link_angles") {
             c->link_angles = iv ? 1 : 0;

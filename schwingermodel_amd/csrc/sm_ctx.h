@@ -84,7 +84,8 @@ struct sm_ctx {
     // size, 2 = >= 1 GiB, 3 = own size contiguous, 4 = own-size physical
     // memory (hipMemCreate) mapped at a 2 GiB-aligned address, 6 = >= 1 GiB
     // contiguous, 7 = ONE contiguous allocation of exactly the streamed
-    // buffers' size, carved in 2 MiB steps. Test option pad_alloc=N; DESIGN
+    // buffers' size, carved in 2 MiB steps, 8 = the same pool in 2 GiB slots
+    // (for buffers up to 2 GiB). Test option pad_alloc=N; DESIGN
     // §2 and profiles/r04_e_alloc_trials.jsonl give the measurements.
     int pad_alloc = 5;
     struct VmmMap {
