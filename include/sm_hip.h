@@ -180,7 +180,7 @@ int sm_local_sites(const sm_ctx *ctx, long *V, int *Nx, int *Wt, int *t0);
 const char *sm_build_id(void);
 /* Placement probe of the context's creation (fields >= 256 MiB): the CG pass
  * runs at one of two speeds depending on where the driver physically places
- * its streamed buffers, so creation times up to 5 candidate sets and keeps the
+ * its streamed buffers, so creation times up to 8 candidate sets and keeps the
  * fastest (schwingermodel_amd/csrc/sm_capi.cpp placement_probe; not on
  * host-staged contexts, where shard processes share one GPU). *n = sets
  * tried (0: no probe), *chosen = the one kept, us_per_pass[0..n-1] (may be

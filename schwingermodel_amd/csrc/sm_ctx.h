@@ -99,7 +99,7 @@ struct sm_ctx {
     // Placement probe at creation (sm_capi.cpp placement_probe): candidate
     // sets of the streamed buffers tried, their CG-pass time (us per pass)
     // and the one kept. Test option place_probe=N (N sets; 1 = no probe).
-    int place_probe = 5;
+    int place_probe = 8;
     int place_n = 0, place_chosen = -1;
     double place_us[8] = {};
     double *Uang = nullptr;         // 2V link codes (plane mu0 then mu1)
