@@ -128,13 +128,13 @@ def test_even_odd_tshard_redundant_scalars_agree(sm):
 def test_placement_modes_bitwise():
     """The placement rules of the streamed CG buffers (sm_ctx.h pad_alloc:
     own size, >= 1 / 2 GiB, the contiguous flag, own-size physical memory at a
-    2 GiB-aligned address, one contiguous pool) change where the fields live,
+    2 GiB-aligned address, one contiguous pool packed or in 2 GiB slots) change where the fields live,
     never the arithmetic: the same solve is bitwise identical under each, at a
     shape whose fields are 256 MiB (4096 x 2048, the smallest that takes the
     rule). DESIGN §2 gives why the default is what it is."""
     import schwingermodel_amd as sm
     ref = None
-    for mode in (1, 0, 2, 3, 4, 5, 6, 7):
+    for mode in (1, 0, 2, 3, 4, 5, 6, 7, 8):
         it, x = solve(sm, 4096, 2048, 0.2374, 0.3, {"pad_alloc": mode})
         if ref is None:
             ref = (it, x)
