@@ -192,9 +192,9 @@ def cpu_model():
 
 def decompose(threads):
     """ranks_x x ranks_t <= threads, both powers of two (they must divide the
-    power-of-two lattice, include/mpi_setup.h:6-23), ranks_x >= 2 (the reference
-    deadlocks for ranks_x = 1), as square as possible."""
-    p = 1 << (max(2, threads).bit_length() - 1)
+    power-of-two lattice, include/mpi_setup.h:6-23), both >= 2 (the reference
+    deadlocks when either is 1), as square as possible."""
+    p = 1 << (max(4, threads).bit_length() - 1)
     k = p.bit_length() - 1
     rx = 1 << ((k + 1) // 2)
     return rx, p // rx
@@ -210,12 +210,17 @@ def cpu_baseline(cfg, threads, ncg):
     exe = os.path.join(REPO, "oracle", "_ref", f"sm_ref_{Nx}x{Nt}")
     mpirun = "/opt/conda/bin/mpirun"
     model = cpu_model()
-    if os.path.exists(exe) and os.path.exists(mpirun) and threads >= 2:
+    # >= 4 threads: both ranks_x and ranks_t >= 2 (the reference's halos to
+    # itself deadlock under MPICH when either is 1)
+    if os.path.exists(exe) and os.path.exists(mpirun) and threads >= 4:
         rx, rt = decompose(threads)
         cmd = [mpirun, "-n", str(rx * rt), exe, "bench", str(rx), str(rt), str(SEED_U),
                repr(sigma), str(SEED_CHI), repr(m0), "3", str(ncg)]
         try:
-            env = dict(os.environ, HOSTNAME=os.environ.get("HOSTNAME", "localhost"), OMP_NUM_THREADS="1")
+            # the reference's blocking sends rely on eager delivery (tests/golden/make_golden.py
+            # MPI_EAGER_ENV): transport settings only
+            env = dict(os.environ, HOSTNAME=os.environ.get("HOSTNAME", "localhost"), OMP_NUM_THREADS="1",
+                       MPIR_CVAR_NEMESIS_SHM_EAGER_MAX_SZ="1048576", MPIR_CVAR_CH3_EAGER_MAX_MSG_SIZE="1048576")
             out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
             if out.returncode == 0:
                 r = json.loads(out.stdout.strip().splitlines()[-1])

@@ -67,8 +67,18 @@ MD_OUTS = ["ref_plaq", "ref_staple", "ref_gforce", "ref_phi", "ref_mdforce", "re
 SEED_P = 2468
 
 
+# The reference's halo exchange posts all its blocking MPI_Send calls before
+# its MPI_Recv calls (src/dirac_operator.cpp:66-88), so it relies on eager
+# delivery. MPICH's shared-memory eager limit is below 64 KiB, and at 8192^2
+# on 2x4 ranks a column halo is 4096 x 16 B = 64 KiB: every rank then waits in
+# MPI_Send forever (observed round 4: a 6-hour run that never finished its
+# first D_phi). Raising the eager limits changes only the transport, not one
+# arithmetic operation of the reference.
+MPI_EAGER_ENV = {"MPIR_CVAR_NEMESIS_SHM_EAGER_MAX_SZ": "1048576", "MPIR_CVAR_CH3_EAGER_MAX_MSG_SIZE": "1048576"}
+
+
 def run(cmd, **kw):
-    env = dict(os.environ, HOSTNAME=os.environ.get("HOSTNAME", "localhost"))
+    env = dict(os.environ, HOSTNAME=os.environ.get("HOSTNAME", "localhost"), **MPI_EAGER_ENV)
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, **kw)
     if r.returncode != 0:
         raise RuntimeError(f"{cmd} failed: {r.stderr}")
