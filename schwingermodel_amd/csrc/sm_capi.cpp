@@ -641,8 +641,8 @@ static int apply_test_opts(sm_ctx *c) {
     return SM_OK;
 }
 
-// Placement probe (round 4). The CG pass runs at one of two speeds (~456
-// against ~477 us at 4096^2) depending on where the driver physically puts
+// Placement probe (round 4). The CG pass runs at one of two speeds (~428-437
+// against ~455-477 us at 4096^2) depending on where the driver physically puts
 // its five streamed buffers, and the state varies from one allocation to the
 // next within a process (profiles/r04_e_alloc_trials.jsonl). So a
 // context allocates up to place_probe candidate sets of those buffers (the
@@ -653,9 +653,10 @@ static int apply_test_opts(sm_ctx *c) {
 // same streams; their faces are a few rows). Only where the rule applies
 // (fields >= 256 MiB, the recompute-Ad pass with fused multiply-adds; not on
 // host-staged contexts) and while the device keeps 16 GiB free besides the
-// candidates. The kept set is
-// zeroed again afterwards (the probe's iterates are NaN), and the scalars and
-// tickets are reset. sm_placement_report returns the times and the choice.
+// candidates. The kept set is zeroed again afterwards (the probe's iterates
+// are NaN), and the scalars and tickets are reset; on an error every
+// candidate but the context's own fields is freed. sm_placement_report
+// returns the times and the choice.
 static int placement_probe(sm_ctx *c, size_t fb) {
     constexpr int kStreams = 5;  // F_D, F_D2, F_R, F_X, link codes
     const int K = std::min(c->place_probe, 8);
@@ -690,21 +691,35 @@ static int placement_probe(sm_ctx *c, size_t fb) {
         sets.push_back(st);
     }
     const int n = (int)sets.size();
+    // on an error: free every candidate except the context's own fields
+    // (sets[0][0..3], released with the context)
+    auto drop = [&](int rc) {
+        for (int k = 1; k < n; ++k)
+            for (void *q : sets[k]) stream_free(c, q);
+        stream_free(c, sets[0][4]);
+        return rc;
+    };
     for (auto &st : sets)
-        for (int i = 0; i < kStreams; ++i) HIP_TRY(hipMemsetAsync(st[i], 0, sizes[i], c->own_stream));
+        for (int i = 0; i < kStreams; ++i)
+            if (hipMemsetAsync(st[i], 0, sizes[i], c->own_stream) != hipSuccess)
+                return drop(fail(SM_ERR_HIP, "placement probe: memset"));
     CGScalars *h = (CGScalars *)c->h_sc;
     memset(h, 0, sizeof(CGScalars));
     h->max_iter = 1 << 30;
     h->phi_norm = 1.0;
-    HIP_TRY(hipMemcpyAsync(c->sc, h, sizeof(CGScalars), hipMemcpyHostToDevice, c->own_stream));
+    if (hipMemcpyAsync(c->sc, h, sizeof(CGScalars), hipMemcpyHostToDevice, c->own_stream) != hipSuccess)
+        return drop(fail(SM_ERR_HIP, "placement probe: scalars"));
     Geometry g = c->g;
     g.t0 = 0;
     g.Ntg = g.Wt;  // one shard's pass over this shard's streams
     const int nparts = cg_fused_blocks(c->racfg);
     const bool tail = (nparts + 63) / 64 <= kMaxTickGroups;
-    hipEvent_t ev[2];
-    HIP_TRY(hipEventCreate(&ev[0]));
-    HIP_TRY(hipEventCreate(&ev[1]));
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    if (hipEventCreate(&ev[0]) != hipSuccess || hipEventCreate(&ev[1]) != hipSuccess) {
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
+        return drop(fail(SM_ERR_HIP, "placement probe: events"));
+    }
     constexpr int kRounds = 4, kPasses = 6;
     std::vector<std::vector<float>> t(n);
     long j = 2;
@@ -727,8 +742,8 @@ static int placement_probe(sm_ctx *c, size_t fb) {
         }
     (void)hipEventDestroy(ev[0]);
     (void)hipEventDestroy(ev[1]);
-    if (rc != SM_OK) return rc;
-    HIP_TRY(hipGetLastError());
+    if (rc == SM_OK && hipGetLastError() != hipSuccess) rc = fail(SM_ERR_HIP, "placement probe: launch");
+    if (rc != SM_OK) return drop(rc);
     int best = 0;
     for (int k = 0; k < n; ++k) {
         std::sort(t[k].begin(), t[k].end());

@@ -1,6 +1,7 @@
 # Round 4: placement rules 5 (>= 2 GiB + contiguous), 6 (>= 1 GiB +
-# contiguous), 7 (one contiguous pool), 1 (>= 2 GiB) over many contexts,
-# allocations (tools/alloc_trials.py). Tag $1.
+# contiguous), 7 (one contiguous pool), 1 (>= 2 GiB) over many contexts, two
+# processes with held allocations (tools/alloc_trials.py; the first use of
+# this script, tag t2, ran rules 1, 2, 3, 5). Tag $1.
 export TMPDIR=/tmp
 T=${1:-cur}
 mkdir -p gpurun_out
