@@ -573,6 +573,7 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //                       contiguous pool of exactly the buffers' size; 8 one
 //                       contiguous pool of 2 GiB slots)
 //   place_probe=N       candidate placements timed at creation (1: none)
+//   probe_min_mib=N     smallest field (MiB) whose context runs the probe
 //   link_angles=0|1     recompute-Ad pass reads the links as one-double codes
 //   bt=64|128|256       Dirac apply t-columns per block
 //   eo_fused=0, eo_cg_td=0, eo_cg_folded=1   even-odd operator / CG forms
@@ -614,6 +615,9 @@ static int apply_test_opts(sm_ctx *c) {
         } else if (k == "rev") {
             c->racfg.rev_odd = iv;
 
+        } else if (k == "probe_min_mib") {
+            if (iv < 1) return fail(SM_ERR_ARG, "SM_TEST_OPTS: probe_min_mib must be >= 1");
+            c->place_min_mib = iv;
         } else if (k == "place_probe") {
             if (iv < 1 || iv > 8) return fail(SM_ERR_ARG, "SM_TEST_OPTS: place_probe must be 1..8");
             c->place_probe = iv;
@@ -665,7 +669,7 @@ static int placement_probe(sm_ctx *c, size_t fb) {
     // not on host-staged contexts: that transport is how several shard
     // processes share ONE GPU (tests, rehearsals), where eight probes at once
     // would hold more transient memory than the device has
-    if (K <= 1 || c->hosted || c->pad_alloc == 0 || fb < (size_t(256) << 20) || c->cg_fused != 5 ||
+    if (K <= 1 || c->hosted || c->pad_alloc == 0 || fb < (size_t(c->place_min_mib) << 20) || c->cg_fused != 5 ||
         c->racfg.fold < 2)
         return SM_OK;
     const size_t ub = sizeof(double) * 2 * (size_t)c->g.V;

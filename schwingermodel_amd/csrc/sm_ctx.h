@@ -100,6 +100,7 @@ struct sm_ctx {
     // sets of the streamed buffers tried, their CG-pass time (us per pass)
     // and the one kept. Test option place_probe=N (N sets; 1 = no probe).
     int place_probe = 8;
+    long place_min_mib = 256;       // smallest field (MiB) that is probed; test option probe_min_mib=N
     int place_n = 0, place_chosen = -1;
     double place_us[8] = {};
     double *Uang = nullptr;         // 2V link codes (plane mu0 then mu1)
