@@ -186,9 +186,11 @@ def large_spread(name, ranks, workdir_root, mpirun):
             json.dump(meta2, f)
     xa = np.fromfile(os.path.join(base, "ref_cgx.bin"), dtype=np.float64)
     xb = np.fromfile(os.path.join(alt, "ref_cgx.bin"), dtype=np.float64)
+    sa, sb = _fsum_sq(xa), _fsum_sq(xb)
     return {"ranks_x": rx, "ranks_t": rt, "cg_iters": meta2["cg_iters"],
             "cg_true_relres": meta2["cg_true_relres"],
-            "x_rel_to_fixture": float(np.linalg.norm(xa - xb) / np.linalg.norm(xa))}
+            "x_rel_to_fixture": float(np.linalg.norm(xa - xb) / np.linalg.norm(xa)),
+            "sum_x2_rel_to_fixture": abs(sb - sa) / sa}
 
 
 def make_jackknife():
