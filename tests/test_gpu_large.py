@@ -8,10 +8,11 @@ fixture run, `oracle/_ref/sm_ref_<N>x<N> fixture`):
   * l8192x8192_b2_m-0p19  config 5: beta=2 field, m0 = -0.19 (near m_crit),
                           2x4 MPI ranks (the reference's dots then sum in a
                           different order than on 1 rank; its operators are
-                          decomposition-invariant bitwise). Runs only once its
-                          entry is in tests/golden/manifest.json (the cases
-                          are the manifest's "large" entries); until then
-                          config 5 is parity-unpinned against the reference.
+                          decomposition-invariant bitwise). The reference on
+                          4x2 ranks differs from it by 2.2e-12 in x and
+                          4.0e-12 in the sum of squares (manifest
+                          "reference_decomposition_spread"), so this case's
+                          bars are 4.4e-12 and 8.0e-12.
 Each keeps the reference's outputs at 4096 seeded random sites plus a SHA-256
 and an exactly rounded (math.fsum) sum of squares of every full field. The
 inputs are regenerated here with the same counter-based generator (bit-exact,
