@@ -383,16 +383,16 @@ def time_applies(rt, sh, m0, n):
 
 
 def placement_report(sh):
-    """The context's placement probe (sm_placement_report): candidate sets of
-    the CG pass's streamed buffers timed at creation and the one kept."""
+    """The context's placement probe (sm_placement_report): the CG pass time of
+    the initial placement of its streamed buffers and after the search of each
+    buffer (x, d1, d0, d2), and which buffers were re-placed."""
     sm = sh.sm
-    fn = getattr(sm.lib, "sm_placement_report", None)
-    if fn is None:
-        return None
     us = (ctypes.c_double * 8)()
-    n, chosen = ctypes.c_int(0), ctypes.c_int(-1)
-    sm.check(fn(sh.L.ctx, us, ctypes.byref(n), ctypes.byref(chosen)))
-    return {"sets_timed": n.value, "kept": chosen.value, "us_per_pass": [round(us[k], 1) for k in range(n.value)]}
+    n, chosen = ctypes.c_int(0), ctypes.c_int(0)
+    sm.check(sm.lib.sm_placement_report(sh.L.ctx, us, ctypes.byref(n), ctypes.byref(chosen)))
+    names = ("x", "d1", "d0", "d2")
+    return {"us_per_pass": [round(us[k], 1) for k in range(n.value)],
+            "moved": [names[i] for i in range(4) if chosen.value >> i & 1]}
 
 
 def cg_bytes_per_site(sh, cg_path):

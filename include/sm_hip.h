@@ -180,12 +180,20 @@ int sm_local_sites(const sm_ctx *ctx, long *V, int *Nx, int *Wt, int *t0);
 const char *sm_build_id(void);
 /* Placement probe of the context's creation (fields >= 256 MiB): the CG pass
  * runs at one of two speeds depending on where the driver physically places
- * its streamed buffers, so creation times up to 8 candidate sets and keeps the
- * fastest (schwingermodel_amd/csrc/sm_capi.cpp placement_probe; not on
- * host-staged contexts, where shard processes share one GPU). *n = sets
- * tried (0: no probe), *chosen = the one kept, us_per_pass[0..n-1] (may be
- * NULL; room for 8) = median microseconds per pass of each. */
+ * its streamed buffers relative to each other, so creation searches one buffer
+ * at a time (x, then the three direction buffers), trying up to
+ * `candidates` fresh allocations of that buffer and keeping the fastest
+ * (schwingermodel_amd/csrc/sm_capi.cpp placement_probe; not on host-staged
+ * contexts, where shard processes share one GPU). *n = timings (0: no probe,
+ * else 5), us_per_pass[0] (may be NULL; room for 8) = median microseconds
+ * per pass of the initial placement, us_per_pass[i] = after the search of
+ * buffer i; *chosen = bit mask of the buffers that moved (bit 0 x, 1..3 the
+ * direction buffers). */
 int sm_placement_report(const sm_ctx *ctx, double *us_per_pass, int *n, int *chosen);
+/* Candidates per buffer of the placement probe for contexts created after
+ * this call (process-wide; default 3, 0 disables the probe, at most 8).
+ * Transient memory while probing: that many allocations of one buffer. */
+int sm_set_placement_probe(int candidates);
 
 /* Gauge field (host / device). Must precede every operator call; re-upload
  * whenever the caller changes U (the reference mutates U between calls,

@@ -50,7 +50,10 @@ def _load():
         raise ImportError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`"
                           " (the HIP path has no CPU fallback)")
     lib = ctypes.CDLL(LIB_PATH)
-    ab_override = bool(os.environ.get("SM_LIB_PATH"))
+    # Missing entry points are tolerated only when an A/B run says so
+    # explicitly (SM_LIB_AB=1 with SM_LIB_PATH at an older build); any other
+    # load, SM_LIB_PATH included, must export every entry point or fail here.
+    ab_override = bool(os.environ.get("SM_LIB_PATH")) and os.environ.get("SM_LIB_AB") == "1"
     vp, ci, cd, cl = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_long
     u64 = ctypes.c_uint64
     sig = {
@@ -92,6 +95,7 @@ def _load():
         "sm_tune_cg": ([vp, ci, ci], ci),
         "sm_build_id": ([], ctypes.c_char_p),
         "sm_placement_report": ([vp, vp, ctypes.POINTER(ci), ctypes.POINTER(ci)], ci),
+        "sm_set_placement_probe": ([ci], ci),
         "sm_cg_link_codes": ([vp, ci, ctypes.POINTER(ci)], ci),
         "sm_cg_link_angles": ([vp, ci, ctypes.POINTER(ci)], ci),
         "sm_link_code_check": ([vp, vp, ctypes.POINTER(cd), ctypes.POINTER(ctypes.c_long)], ci),

@@ -120,78 +120,17 @@ static hipError_t contiguous_or_plain(void **p, size_t bytes) {
 }
 
 // Allocate a streamed CG buffer by the context's placement rule (sm_ctx
-// pad_alloc; the alternatives are test options for the measurements above).
+// pad_alloc: 5 the default, 0 own size for A/B runs; the other rules measured
+// in rounds 3-4 were slower and are gone, DESIGN Appendix A.4).
 static hipError_t stream_malloc(sm_ctx *c, void **p, size_t bytes) {
     if (bytes < (size_t(256) << 20) || c->pad_alloc == 0) return hipMalloc(p, bytes);
-    switch (c->pad_alloc) {
-        case 2: return hipMalloc(p, stream_alloc_bytes(bytes, size_t(1) << 30));
-        // contiguous requests fall back to a plain allocation of the same size
-        // when the driver cannot find contiguous memory
-        case 3: return contiguous_or_plain(p, bytes);
-        case 5: return contiguous_or_plain(p, stream_alloc_bytes(bytes));
-        case 6: return contiguous_or_plain(p, stream_alloc_bytes(bytes, size_t(1) << 30));
-        case 7:
-        case 8: {
-            // the three direction buffers, x and the link codes (half a field);
-            // 7: packed in 2 MiB steps, 8: one 2 GiB-aligned slot each
-            const size_t step = c->pad_alloc == 8 ? stream_alloc_bytes(bytes) : size_t(2) << 20;
-            const size_t fb = (bytes + step - 1) / step * step;
-            if (!c->stream_pool) {
-                c->pool_bytes = 4 * fb + (fb / 2 + step - 1) / step * step;  // 8: 5 slots
-                hipError_t e = contiguous_or_plain((void **)&c->stream_pool, c->pool_bytes);
-                if (e != hipSuccess) return e;
-                c->pool_used = 0;
-            }
-            if (c->pool_used + bytes > c->pool_bytes) return hipErrorOutOfMemory;
-            *p = c->stream_pool + c->pool_used;
-            c->pool_used += (bytes + step - 1) / step * step;
-            return hipSuccess;
-        }
-        case 4: {
-            hipMemAllocationProp prop = {};
-            prop.type = hipMemAllocationTypePinned;
-            prop.location.type = hipMemLocationTypeDevice;
-            prop.location.id = c->device;
-            size_t gran = 0;
-            hipError_t e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
-            if (e != hipSuccess) return e;
-            const size_t phys = (bytes + gran - 1) / gran * gran;
-            sm_ctx::VmmMap m = {nullptr, stream_alloc_bytes(phys), phys, {}};
-            if ((e = hipMemAddressReserve(&m.ptr, m.va_bytes, size_t(2) << 30, nullptr, 0)) != hipSuccess) return e;
-            if ((e = hipMemCreate(&m.handle, phys, &prop, 0)) != hipSuccess) {
-                (void)hipMemAddressFree(m.ptr, m.va_bytes);
-                return e;
-            }
-            hipMemAccessDesc acc = {};
-            acc.location = prop.location;
-            acc.flags = hipMemAccessFlagsProtReadWrite;
-            if ((e = hipMemMap(m.ptr, phys, 0, m.handle, 0)) != hipSuccess ||
-                (e = hipMemSetAccess(m.ptr, phys, &acc, 1)) != hipSuccess) {
-                (void)hipMemUnmap(m.ptr, phys);
-                (void)hipMemRelease(m.handle);
-                (void)hipMemAddressFree(m.ptr, m.va_bytes);
-                return e;
-            }
-            c->vmm.push_back(m);
-            *p = m.ptr;
-            return hipSuccess;
-        }
-        default: return hipMalloc(p, stream_alloc_bytes(bytes));
-    }
+    // a contiguous request falls back to a plain allocation of the same size
+    // when the driver cannot find contiguous memory
+    return contiguous_or_plain(p, stream_alloc_bytes(bytes));
 }
 
-static void stream_free(sm_ctx *c, void *p) {
-    if (!p) return;
-    if (c->stream_pool && (char *)p >= c->stream_pool && (char *)p < c->stream_pool + c->pool_bytes) return;
-    for (size_t i = 0; i < c->vmm.size(); ++i)
-        if (c->vmm[i].ptr == p) {
-            (void)hipMemUnmap(p, c->vmm[i].phys_bytes);
-            (void)hipMemRelease(c->vmm[i].handle);
-            (void)hipMemAddressFree(p, c->vmm[i].va_bytes);
-            c->vmm.erase(c->vmm.begin() + (long)i);
-            return;
-        }
-    (void)hipFree(p);
+static void stream_free(sm_ctx *, void *p) {
+    if (p) (void)hipFree(p);
 }
 
 int exchange_faces_on(sm_ctx *c, hipStream_t s, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi,
@@ -565,14 +504,11 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //   rev=0|1|2           recompute-Ad pass march schedule (0 all forward; 1 odd
 //                       passes backward; 2, the default, x-adjacent chunks in
 //                       opposite directions and odd passes flipped)
-//   pad_alloc=0..7      placement of the streamed CG buffers (sm_ctx.h:
+//   pad_alloc=0|5       placement of the streamed CG buffers (sm_ctx.h:
 //                       5 >= 2 GiB each + contiguous flag, the default;
-//                       1 >= 2 GiB plain; 0 own size; 2 >= 1 GiB; 3 own size
-//                       contiguous; 4 own-size physical memory at a 2 GiB-
-//                       aligned address; 6 >= 1 GiB contiguous; 7 one
-//                       contiguous pool of exactly the buffers' size; 8 one
-//                       contiguous pool of 2 GiB slots)
-//   place_probe=N       candidate placements timed at creation (1: none)
+//                       0 own size)
+//   place_probe=N       candidates per buffer of the placement probe (0: none;
+//                       sm_set_placement_probe sets the default)
 //   probe_min_mib=N     smallest field (MiB) whose context runs the probe
 //   link_angles=0|1     recompute-Ad pass reads the links as one-double codes
 //   bt=64|128|256       Dirac apply t-columns per block
@@ -619,10 +555,10 @@ static int apply_test_opts(sm_ctx *c) {
             if (iv < 1) return fail(SM_ERR_ARG, "SM_TEST_OPTS: probe_min_mib must be >= 1");
             c->place_min_mib = iv;
         } else if (k == "place_probe") {
-            if (iv < 1 || iv > 8) return fail(SM_ERR_ARG, "SM_TEST_OPTS: place_probe must be 1..8");
+            if (iv < 0 || iv > 8) return fail(SM_ERR_ARG, "SM_TEST_OPTS: place_probe must be 0..8");
             c->place_probe = iv;
         } else if (k == "pad_alloc") {
-            if (iv < 0 || iv > 8) return fail(SM_ERR_ARG, "SM_TEST_OPTS: pad_alloc must be 0..8");
+            if (iv != 0 && iv != 5) return fail(SM_ERR_ARG, "SM_TEST_OPTS: pad_alloc must be 0 or 5");
             c->pad_alloc = iv;
         } else if (k == "link_angles") {
             c->link_angles = iv ? 1 : 0;
@@ -645,138 +581,153 @@ static int apply_test_opts(sm_ctx *c) {
     return SM_OK;
 }
 
-// Placement probe (round 4). The CG pass runs at one of two speeds (~428-437
-// against ~455-477 us at 4096^2) depending on where the driver physically puts
-// its five streamed buffers, and the state varies from one allocation to the
-// next within a process (profiles/r04_e_alloc_trials.jsonl). So a
-// context allocates up to place_probe candidate sets of those buffers (the
-// three direction buffers, x and the link codes), times the real pass
-// launcher on each (interleaved rounds of a few passes on zero-filled data,
-// the first round discarded as warm-up), keeps the fastest set and frees the
-// others. One shard's pass shape is timed on every context (t-shards use the
-// same streams; their faces are a few rows). Only where the rule applies
-// (fields >= 256 MiB, the recompute-Ad pass with fused multiply-adds; not on
-// host-staged contexts) and while the device keeps 16 GiB free besides the
-// candidates. The kept set is zeroed again afterwards (the probe's iterates
-// are NaN), and the scalars and tickets are reset; on an error every
-// candidate but the context's own fields is freed. sm_placement_report
-// returns the times and the choice.
+// Placement probe (round 5: coordinate descent over the buffers). The CG pass
+// runs at one of two speeds (~430-438 against ~455-480 us at 4096^2)
+// depending on where the driver physically puts its streamed buffers. Timing
+// every set that differs from a base set in ONE buffer (tools/place_buffers,
+// profiles/r05_a_place_buffers.jsonl) shows that each of the three direction
+// buffers and x can flip the state while the link codes cannot, and that the
+// effects do not add (the set of every buffer's best alternative was slower
+// than the set of the worst ones on one box): the state belongs to the
+// buffers' placement relative to each other. So the probe keeps the set and
+// searches one buffer at a time -- x, d1, d0, d2 (F_X, F_D2, F_D, F_R) -- with
+// up to place_probe fresh allocations of that buffer (held while it is
+// searched, so the allocator cannot hand the same memory back), takes the
+// fastest candidate if it beats the current set by more than 1 %, and frees
+// the rest before the next buffer. 24 contexts on one box reached 430-439 us
+// from starts of 437-505 this way (r05_b_descent.jsonl). Transient memory:
+// place_probe allocations of one buffer (3 x 2 GiB at 4096^2), and only while
+// 16 GiB stay free besides them; a candidate that cannot be allocated ends
+// that buffer's search (not the context). Only where the rule applies (fields
+// >= 256 MiB, the recompute-Ad pass with fused multiply-adds; not on
+// host-staged contexts, where shard processes share one GPU). The timings run
+// on zero data (NaN iterates), so the kept buffers are zeroed again and the
+// scalars and tickets reset. sm_placement_report returns the pass time of the
+// initial set and after each buffer's search, and which buffers moved.
+static int g_place_probe = 3;  // candidates per buffer for new contexts (sm_set_placement_probe)
+
 static int placement_probe(sm_ctx *c, size_t fb) {
-    constexpr int kStreams = 5;  // F_D, F_D2, F_R, F_X, link codes
-    const int K = std::min(c->place_probe, 8);
+    const int M = c->place_probe;
     c->place_n = 0;
-    c->place_chosen = -1;
-    // not on host-staged contexts: that transport is how several shard
-    // processes share ONE GPU (tests, rehearsals), where eight probes at once
-    // would hold more transient memory than the device has
-    if (K <= 1 || c->hosted || c->pad_alloc == 0 || fb < (size_t(c->place_min_mib) << 20) || c->cg_fused != 5 ||
+    c->place_chosen = 0;
+    if (M < 1 || c->hosted || c->pad_alloc == 0 || fb < (size_t(c->place_min_mib) << 20) || c->cg_fused != 5 ||
         c->racfg.fold < 2)
         return SM_OK;
     const size_t ub = sizeof(double) * 2 * (size_t)c->g.V;
-    const size_t sizes[kStreams] = {fb, fb, fb, fb, ub};
-    std::vector<std::array<void *, kStreams>> sets;
-    sets.push_back({(void *)c->fields[F_D], (void *)c->fields[F_D2], (void *)c->fields[F_R], (void *)c->fields[F_X],
-                    nullptr});
-    HIP_TRY(stream_malloc(c, &sets[0][4], ub));
-    size_t per_set = 0;
-    for (int i = 0; i < kStreams; ++i) per_set += stream_alloc_bytes(sizes[i]);
-    for (int k = 1; k < K; ++k) {
-        size_t free_b = 0, total_b = 0;
-        HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-        if (free_b < per_set + (size_t(16) << 30)) break;
-        std::array<void *, kStreams> st = {};
-        bool ok = true;
-        for (int i = 0; i < kStreams && ok; ++i) ok = stream_malloc(c, &st[i], sizes[i]) == hipSuccess;
-        if (!ok) {
-            (void)hipGetLastError();
-            for (void *q : st) stream_free(c, q);
-            break;
-        }
-        sets.push_back(st);
+    // the link codes are the pass's fifth stream: allocated here so the probe
+    // times the real pass (their placement does not move the state)
+    if (!c->Uang) HIP_TRY(stream_malloc(c, (void **)&c->Uang, ub));
+    HIP_TRY(hipMemsetAsync(c->Uang, 0, ub, c->own_stream));
+    static const int kSlot[4] = {F_D, F_D2, F_R, F_X};  // pass operands d[0..2], x
+    void *cur[4];
+    for (int i = 0; i < 4; ++i) {
+        cur[i] = c->fields[kSlot[i]];
+        HIP_TRY(hipMemsetAsync(cur[i], 0, fb, c->own_stream));
     }
-    const int n = (int)sets.size();
-    // on an error: free every candidate except the context's own fields
-    // (sets[0][0..3], released with the context)
-    auto drop = [&](int rc) {
-        for (int k = 1; k < n; ++k)
-            for (void *q : sets[k]) stream_free(c, q);
-        stream_free(c, sets[0][4]);
-        return rc;
-    };
-    for (auto &st : sets)
-        for (int i = 0; i < kStreams; ++i)
-            if (hipMemsetAsync(st[i], 0, sizes[i], c->own_stream) != hipSuccess)
-                return drop(fail(SM_ERR_HIP, "placement probe: memset"));
     CGScalars *h = (CGScalars *)c->h_sc;
     memset(h, 0, sizeof(CGScalars));
     h->max_iter = 1 << 30;
     h->phi_norm = 1.0;
-    if (hipMemcpyAsync(c->sc, h, sizeof(CGScalars), hipMemcpyHostToDevice, c->own_stream) != hipSuccess)
-        return drop(fail(SM_ERR_HIP, "placement probe: scalars"));
+    HIP_TRY(hipMemcpyAsync(c->sc, h, sizeof(CGScalars), hipMemcpyHostToDevice, c->own_stream));
     Geometry g = c->g;
     g.t0 = 0;
     g.Ntg = g.Wt;  // one shard's pass over this shard's streams
     const int nparts = cg_fused_blocks(c->racfg);
     const bool tail = (nparts + 63) / 64 <= kMaxTickGroups;
     hipEvent_t ev[2] = {nullptr, nullptr};
-    if (hipEventCreate(&ev[0]) != hipSuccess || hipEventCreate(&ev[1]) != hipSuccess) {
+    auto drop_events = [&] {
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
-        return drop(fail(SM_ERR_HIP, "placement probe: events"));
+    };
+    if (hipEventCreate(&ev[0]) != hipSuccess || hipEventCreate(&ev[1]) != hipSuccess) {
+        drop_events();
+        return fail(SM_ERR_HIP, "placement probe: events");
     }
-    constexpr int kRounds = 4, kPasses = 6;
-    std::vector<std::vector<float>> t(n);
     long j = 2;
-    int rc = SM_OK;
-    for (int r = 0; r < kRounds && rc == SM_OK; ++r)
-        for (int k = 0; k < n && rc == SM_OK; ++k) {
-            double2 *d[3] = {(double2 *)sets[k][0], (double2 *)sets[k][1], (double2 *)sets[k][2]};
-            if (hipEventRecord(ev[0], c->own_stream) != hipSuccess) rc = fail(SM_ERR_HIP, "placement probe");
+    // median us per pass of 3 rounds of 6 passes (one warm-up round first)
+    auto time_set = [&](void *const *f, double *us) -> int {
+        constexpr int kRounds = 3, kPasses = 6;
+        float t[kRounds];
+        for (int r = -1; r < kRounds; ++r) {
+            double2 *d[3] = {(double2 *)f[0], (double2 *)f[1], (double2 *)f[2]};
+            if (hipEventRecord(ev[0], c->own_stream) != hipSuccess) return fail(SM_ERR_HIP, "placement probe");
             for (int p = 0; p < kPasses; ++p, ++j)
-                launch_cg_ra(c->own_stream, g, c->racfg, 1, d[(j + 2) % 3], d[(j + 1) % 3], d[j % 3],
-                             (double2 *)sets[k][3], nullptr, nullptr, nullptr, nullptr, 1.94, j, c->sc, c->partials,
-                             0, c->racfg.TBk, nullptr, (const double *)sets[k][4], nullptr, nullptr, 0,
-                             tail ? c->tick : nullptr, nparts, c->gsum, nullptr);
+                launch_cg_ra(c->own_stream, g, c->racfg, 1, d[(j + 2) % 3], d[(j + 1) % 3], d[j % 3], (double2 *)f[3],
+                             nullptr, nullptr, nullptr, nullptr, 1.94, j, c->sc, c->partials, 0, c->racfg.TBk,
+                             nullptr, c->Uang, nullptr, nullptr, 0, tail ? c->tick : nullptr, nparts, c->gsum,
+                             nullptr);
             float ms = 0.f;
-            if (rc == SM_OK && (hipEventRecord(ev[1], c->own_stream) != hipSuccess ||
-                                hipEventSynchronize(ev[1]) != hipSuccess ||
-                                hipEventElapsedTime(&ms, ev[0], ev[1]) != hipSuccess))
-                rc = fail(SM_ERR_HIP, "placement probe timing");
-            if (r > 0) t[k].push_back(ms * 1000.f / kPasses);
+            if (hipEventRecord(ev[1], c->own_stream) != hipSuccess || hipEventSynchronize(ev[1]) != hipSuccess ||
+                hipEventElapsedTime(&ms, ev[0], ev[1]) != hipSuccess || hipGetLastError() != hipSuccess)
+                return fail(SM_ERR_HIP, "placement probe timing");
+            if (r >= 0) t[r] = ms * 1000.f / kPasses;
         }
-    (void)hipEventDestroy(ev[0]);
-    (void)hipEventDestroy(ev[1]);
-    if (rc == SM_OK && hipGetLastError() != hipSuccess) rc = fail(SM_ERR_HIP, "placement probe: launch");
-    if (rc != SM_OK) return drop(rc);
-    int best = 0;
-    for (int k = 0; k < n; ++k) {
-        std::sort(t[k].begin(), t[k].end());
-        c->place_us[k] = t[k][t[k].size() / 2];
-        if (c->place_us[k] < c->place_us[best]) best = k;
+        std::sort(t, t + kRounds);
+        *us = t[kRounds / 2];
+        return SM_OK;
+    };
+    double now = 0.0;
+    int rc = time_set(cur, &now);
+    c->place_us[c->place_n++] = now;
+    const size_t bytes = stream_alloc_bytes(fb);
+    for (int step = 0; step < 4 && rc == SM_OK; ++step) {
+        const int b = (int[]){3, 1, 0, 2}[step];  // x, d1, d0, d2
+        std::vector<void *> cand;
+        int keep = -1;
+        double best = now;
+        for (int m = 0; m < M && rc == SM_OK; ++m) {
+            size_t free_b = 0, total_b = 0;
+            if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b < bytes + (size_t(16) << 30)) break;
+            void *p = nullptr;
+            if (stream_malloc(c, &p, fb) != hipSuccess) {
+                (void)hipGetLastError();  // not fatal: this buffer's search ends
+                break;
+            }
+            cand.push_back(p);
+            if (hipMemsetAsync(p, 0, fb, c->own_stream) != hipSuccess) {
+                rc = fail(SM_ERR_HIP, "placement probe: memset");
+                break;
+            }
+            void *trial[4] = {cur[0], cur[1], cur[2], cur[3]};
+            trial[b] = p;
+            double us = 0.0;
+            rc = time_set(trial, &us);
+            if (rc == SM_OK && us < best) best = us, keep = (int)cand.size() - 1;
+        }
+        if (rc == SM_OK && keep >= 0 && best < 0.99 * now) {
+            stream_free(c, cur[b]);
+            cur[b] = cand[keep];
+            c->fields[kSlot[b]] = (double2 *)cur[b];
+            now = best;
+            c->place_chosen |= 1 << step;
+        }
+        for (void *p : cand)
+            if (p != cur[b]) stream_free(c, p);
+        c->place_us[c->place_n++] = now;
     }
-    c->place_n = n;
-    c->place_chosen = best;
-    for (int k = 0; k < n; ++k)
-        if (k != best)
-            for (void *q : sets[k]) stream_free(c, q);
-    c->fields[F_D] = (double2 *)sets[best][0];
-    c->fields[F_D2] = (double2 *)sets[best][1];
-    c->fields[F_R] = (double2 *)sets[best][2];
-    c->fields[F_X] = (double2 *)sets[best][3];
-    c->Uang = (double *)sets[best][4];
+    drop_events();
+    if (rc != SM_OK) return rc;
     // the probe's iterates are NaN (0/0 scalars on zero data): clear them, as
     // a fresh allocation would be (pass 0 weights d_{-2} by a zero multiplier)
-    for (int i = 0; i < kStreams; ++i) HIP_TRY(hipMemsetAsync(sets[best][i], 0, sizes[i], c->own_stream));
+    for (void *p : cur) HIP_TRY(hipMemsetAsync(p, 0, fb, c->own_stream));
+    HIP_TRY(hipMemsetAsync(c->Uang, 0, ub, c->own_stream));
     HIP_TRY(hipMemsetAsync(c->sc, 0, sizeof(CGScalars), c->own_stream));
     HIP_TRY(hipMemsetAsync(c->tick, 0, sizeof(unsigned) * (1 + kMaxTickGroups), c->own_stream));
     HIP_TRY(hipStreamSynchronize(c->own_stream));
     return SM_OK;
 }
 
+int sm_set_placement_probe(int candidates_per_buffer) {
+    if (candidates_per_buffer < 0 || candidates_per_buffer > 8)
+        return fail(SM_ERR_ARG, "placement probe candidates must be 0..8");
+    g_place_probe = candidates_per_buffer;
+    return SM_OK;
+}
+
 int sm_placement_report(const sm_ctx *c, double *us_per_pass, int *n, int *chosen) {
     if (!c || !n || !chosen) return fail(SM_ERR_ARG, "null argument");
     *n = c->place_n;
-    *chosen = c->place_chosen;
+    *chosen = c->place_chosen;  // bit i: buffer i of the search order (x, d1, d0, d2) moved
     if (us_per_pass)
         for (int k = 0; k < c->place_n; ++k) us_per_pass[k] = c->place_us[k];
     return SM_OK;
@@ -835,6 +786,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     //   iteration, 4096x1024 0.141 vs 0.147; tools/link_probe.py re-measures
     //   it for the codes).
     c->link_angles = c->g.V >= (1L << 22) ? 1 : 0;
+    c->place_probe = g_place_probe;
     if (int rc = apply_test_opts(c); rc != SM_OK) {
         delete c;
         return rc;
@@ -964,8 +916,6 @@ int sm_destroy(sm_ctx *c) {
         }
     stream_free(c, c->Uang);
     c->Uang = nullptr;
-    if (c->stream_pool) (void)hipFree(c->stream_pool);
-    c->stream_pool = nullptr;
     void *dev[] = {c->U, c->ghostU, c->faces, c->faces2, c->faces4, c->partials, c->sums, c->Fbuf, c->sc,
                    c->U_alt, c->Pmd, c->Fmd, c->eo, c->Ucb, c->eo_faces, c->eo_faces4, c->Uang_face,
                    c->tick, c->gsum};

@@ -80,28 +80,16 @@ struct sm_ctx {
     // Placement of the buffers the CG pass streams (stream_malloc): 5 = an
     // allocation of >= 2 GiB each with hipDeviceMallocContiguous (the
     // default; plain allocation of that size when the driver has no
-    // contiguous memory), 1 = >= 2 GiB plain (the round-3 rule), 0 = own
-    // size, 2 = >= 1 GiB, 3 = own size contiguous, 4 = own-size physical
-    // memory (hipMemCreate) mapped at a 2 GiB-aligned address, 6 = >= 1 GiB
-    // contiguous, 7 = ONE contiguous allocation of exactly the streamed
-    // buffers' size, carved in 2 MiB steps, 8 = the same pool in 2 GiB slots
-    // (for buffers up to 2 GiB). Test option pad_alloc=N; DESIGN
+    // contiguous memory), 0 = own size (A/B). Test option pad_alloc=N; DESIGN
     // §2 and profiles/r04_e_alloc_trials.jsonl give the measurements.
     int pad_alloc = 5;
-    struct VmmMap {
-        void *ptr;
-        size_t va_bytes, phys_bytes;
-        hipMemGenericAllocationHandle_t handle;
-    };
-    std::vector<VmmMap> vmm;        // pad_alloc 4 mappings (released by stream_free)
-    char *stream_pool = nullptr;    // pad_alloc 7: one contiguous allocation carved for every streamed buffer
-    size_t pool_bytes = 0, pool_used = 0;
-    // Placement probe at creation (sm_capi.cpp placement_probe): candidate
-    // sets of the streamed buffers tried, their CG-pass time (us per pass)
-    // and the one kept. Test option place_probe=N (N sets; 1 = no probe).
-    int place_probe = 8;
+    // Placement probe at creation (sm_capi.cpp placement_probe): candidates
+    // per streamed buffer (0 = no probe; sm_set_placement_probe, test option
+    // place_probe=N), the pass time of the initial set and after each
+    // buffer's search (us per pass), and which buffers moved (bit mask).
+    int place_probe = 3;
     long place_min_mib = 256;       // smallest field (MiB) that is probed; test option probe_min_mib=N
-    int place_n = 0, place_chosen = -1;
+    int place_n = 0, place_chosen = 0;
     double place_us[8] = {};
     double *Uang = nullptr;         // 2V link codes (plane mu0 then mu1)
     double *Uang_face = nullptr;    // t-shards: codes of the 4-deep ghost links (16 Nx)

@@ -21,6 +21,7 @@ mode "gpu" (one GPU shared by all ranks, gloo host transport): every rank runs
 """
 import ctypes
 import json
+import math
 import os
 import sys
 
@@ -435,6 +436,18 @@ def block_of(a, Nx, Nt, t0, Wt, planes_complex=True):
                            for p in range(2)])
 
 
+def large_fixture(Nx, Nt, sigma, m0):
+    """The reference's full-size summary fixture for these inputs (manifest
+    'large', tests/golden/make_golden.py --large), or None: (meta, arrays)."""
+    with open(os.path.join(REPO, "tests", "golden", "manifest.json")) as fh:
+        large = json.load(fh).get("large", {})
+    for meta in large.values():
+        if (meta["Nx"], meta["Nt"]) == (Nx, Nt) and abs(meta["sigma"] - sigma) < 1e-12 and abs(meta["m0"] - m0) < 1e-12:
+            with np.load(os.path.join(REPO, "tests", "golden", meta["file"]), allow_pickle=False) as z:
+                return meta, {k: z[k].copy() for k in z.files}
+    return None
+
+
 def run_big(name, result_path, dist, rank, world):
     """mode "big": BASELINE configs at their real shard shapes on ONE GPU.
     name = big:<Nx>x<Nt>:<sigma>:<m0>:<ops>, ops 'full' (D, D^dag, force, CG)
@@ -482,6 +495,18 @@ def run_big(name, result_path, dist, rank, world):
     ts = time.time() - ts
     sm.lib.sm_destroy(ctx)
     local = {"cg": mine["cg"], "bitwise": {}}
+    fix = large_fixture(Nx, Nt, sigma, m0)
+    if fix is not None:
+        # this shard's share of the reference fixture's sampled x, and the
+        # exactly rounded sum of squares of its block of x
+        _, ref = fix
+        sites = ref["sites"]
+        gx, gt = sites // Nt, sites % Nt
+        sel = np.nonzero((gt >= t0) & (gt < t0 + Wt))[0]
+        loc = gx[sel] * Wt + (gt[sel] - t0)
+        xc = mine["x"].view(np.complex128)
+        local["fix"] = {"sel": sel.tolist(), "p0": xc[loc].view(np.float64).tolist(),
+                        "p1": xc[V + loc].view(np.float64).tolist(), "sumsq": math.fsum(mine["x"] ** 2)}
     for k in ("Dpsi", "Ddagchi", "force"):
         if k in mine:
             ref = np.load(os.path.join(d, f"one_{k}.npy"), mmap_mode="r")
@@ -501,6 +526,21 @@ def run_big(name, result_path, dist, rank, world):
                "bitwise": {k: all(g["bitwise"][k] for g in gathered) for k in gathered[0]["bitwise"]},
                "x_rel": float((sums[0] / sums[1]) ** 0.5), "relres": float((sums[2] / sums[3]) ** 0.5),
                "seconds_one": one["seconds"], "seconds_sharded": ts}
+        if fix is not None:
+            meta, ref = fix
+            n = len(ref["sites"])
+            samp = np.empty((2, n), np.complex128)
+            for g in gathered:
+                sel = np.asarray(g["fix"]["sel"], np.int64)
+                samp[0, sel] = np.asarray(g["fix"]["p0"]).view(np.complex128)
+                samp[1, sel] = np.asarray(g["fix"]["p1"]).view(np.complex128)
+            xs, xr = samp.reshape(-1).view(np.float64), ref["ref_cgx"]
+            ref_sq = meta["fsum_sq"]["ref_cgx"]
+            sq = math.fsum(g["fix"]["sumsq"] for g in gathered)
+            rep["fixture"] = {"name": meta["file"], "cg_iters": meta["cg_iters"],
+                              "x_rel": float(np.linalg.norm(xs - xr) / np.linalg.norm(xr)),
+                              "sumsq_rel": abs(sq - ref_sq) / ref_sq,
+                              "spread": meta.get("reference_decomposition_spread", [])}
         with open(result_path, "w") as fh:
             json.dump(rep, fh)
     dist.barrier()

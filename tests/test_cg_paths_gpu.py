@@ -127,14 +127,13 @@ def test_even_odd_tshard_redundant_scalars_agree(sm):
 
 def test_placement_modes_bitwise():
     """The placement rules of the streamed CG buffers (sm_ctx.h pad_alloc:
-    own size, >= 1 / 2 GiB, the contiguous flag, own-size physical memory at a
-    2 GiB-aligned address, one contiguous pool packed or in 2 GiB slots) change where the fields live,
-    never the arithmetic: the same solve is bitwise identical under each, at a
-    shape whose fields are 256 MiB (4096 x 2048, the smallest that takes the
-    rule). DESIGN §2 gives why the default is what it is."""
+    own size, or >= 2 GiB each with the contiguous flag) change where the
+    fields live, never the arithmetic: the same solve is bitwise identical
+    under each, at a shape whose fields are 256 MiB (4096 x 2048, the smallest
+    that takes the rule). DESIGN §2 gives why the default is what it is."""
     import schwingermodel_amd as sm
     ref = None
-    for mode in (1, 0, 2, 3, 4, 5, 6, 7, 8):
+    for mode in (0, 5):
         it, x = solve(sm, 4096, 2048, 0.2374, 0.3, {"pad_alloc": mode})
         if ref is None:
             ref = (it, x)
@@ -144,13 +143,14 @@ def test_placement_modes_bitwise():
 
 
 def test_placement_probe_report():
-    """Context creation times candidate placements of the streamed CG
-    buffers and keeps the fastest (sm_capi.cpp placement_probe): at a shape
-    that takes the rule (4096 x 2048, 256 MiB fields) the report lists the
-    sets timed (the default 8, fewer only if the device ran short of free
-    memory), a kept set among them with the smallest time, and a solve on
-    the kept set equals the no-probe solve bitwise. Below the rule's size
-    nothing is probed."""
+    """Context creation searches the placement of the CG pass's streamed
+    buffers one buffer at a time (sm_capi.cpp placement_probe): at a shape
+    that takes the rule (4096 x 2048, 256 MiB fields) the report gives the
+    pass time of the initial placement and after each of the four buffers'
+    searches (never slower than before it: a candidate is kept only if
+    faster), and a solve on the probed placement equals the no-probe solve
+    bitwise. Below the rule's size, or with the probe off through the public
+    switch, nothing is probed."""
     import schwingermodel_amd as sm
 
     def report(L):
@@ -164,13 +164,22 @@ def test_placement_probe_report():
         n, k, us = report(L)
     finally:
         L.close()
-    assert 1 <= n <= 8 and 0 <= k < n, (n, k)
-    assert all(u > 0 for u in us) and us[k] == min(us), us
+    assert n == 5 and 0 <= k < 16, (n, k)
+    assert all(u > 0 for u in us) and all(b <= a for a, b in zip(us, us[1:])), us
     L = sm.Lattice(512, 512)
     try:
         assert report(L)[0] == 0
     finally:
         L.close()
+    sm.check(sm.lib.sm_set_placement_probe(0))
+    try:
+        L = sm.Lattice(4096, 2048)
+        try:
+            assert report(L)[0] == 0
+        finally:
+            L.close()
+    finally:
+        sm.check(sm.lib.sm_set_placement_probe(3))
     a = solve(sm, 4096, 2048, 0.2374, 0.3, {})
-    b = solve(sm, 4096, 2048, 0.2374, 0.3, {"place_probe": 1})
+    b = solve(sm, 4096, 2048, 0.2374, 0.3, {"place_probe": 0})
     assert a[0] == b[0] and np.array_equal(a[1].view(np.uint64), b[1].view(np.uint64))

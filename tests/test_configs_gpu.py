@@ -8,15 +8,20 @@
   residual |phi - D D^dag x| / |phi| < 1e-10, in the iteration count (+-1 %) of
   the stored-Ad two-direction pass and -- at 4096^2 -- of the six-kernel
   reference sequence (the reference's per-element arithmetic), with solutions
-  that agree to 1e-10. At 4096^2 D and D^dag are also bitwise against the
+  that agree to 1e-12 (config 3) / 2.2e-12 (config 5: the reference's own
+  spread between two MPI decompositions, where only the dots' order differs). At 4096^2 D and D^dag are also bitwise against the
   threaded oracle.
 * config 4 (4096^2 over 8 t-shards, Wt = 512) and config 5 over 8 t-shards
   (8192 x 1024 each): the shards run on this one GPU over the host-staged
   transport (RCCL refuses two ranks on one GPU); against one shard: D, D^dag and
   force bitwise, CG in the same iteration count (+-1 %), x to 1e-12 (config 4)
-  / 1e-10 (config 5), true residual < 1e-10.
+  / 2.2e-12 (config 5), true residual < 1e-10; config 5's sharded x is also
+  held against the unmodified reference's own solve of the same inputs
+  (tests/golden/l8192x8192_b2_m-0p19.npz): iterations +-1 %, sampled x and the
+  sum of squares within the reference's own decomposition spread.
 """
 import ctypes
+import json
 
 import numpy as np
 import pytest
@@ -39,11 +44,11 @@ def _solve(sm, L, S, psi, m0, mode):
     return x, res.converged, res.iterations, rel
 
 
-@pytest.mark.parametrize("N,sigma,m0,modes", [
-    (4096, 0.2374, -0.06, (5, 4, 0)),   # config 3 (+ the six-kernel reference sequence)
-    (8192, 0.4242, -0.19, (5, 4)),      # config 5 on one GPU
+@pytest.mark.parametrize("N,sigma,m0,modes,xtol", [
+    (4096, 0.2374, -0.06, (5, 4, 0), 1e-12),   # config 3 (+ the six-kernel reference sequence)
+    (8192, 0.4242, -0.19, (5, 4), 2.2e-12),    # config 5 on one GPU: the reference's own decomposition spread
 ])
-def test_config_single_gpu_cg(oracle, N, sigma, m0, modes):
+def test_config_single_gpu_cg(oracle, N, sigma, m0, modes, xtol):
     import schwingermodel_amd as sm
     from dist_worker import fill_block
     S = N * N
@@ -70,7 +75,7 @@ def test_config_single_gpu_cg(oracle, N, sigma, m0, modes):
         for mode in modes[1:]:
             x, it = sols[mode]
             assert abs(it - it5) <= max(1, it5 // 100), (mode, it, it5)
-            assert np.linalg.norm(x - x5) / np.linalg.norm(x) <= 1e-10, mode
+            assert np.linalg.norm(x - x5) / np.linalg.norm(x) <= xtol, mode
     finally:
         L.close()
 
@@ -78,10 +83,15 @@ def test_config_single_gpu_cg(oracle, N, sigma, m0, modes):
 @pytest.mark.multiproc
 @pytest.mark.parametrize("case,world,xtol", [
     ("big:4096x4096:0.2374:-0.06:full", 8, 1e-12),   # config 4: Wt = 512 per shard
-    ("big:8192x8192:0.4242:-0.19:cg", 8, 1e-10),     # config 5: 8192 x 1024 per shard
+    ("big:8192x8192:0.4242:-0.19:cg", 8, 2.2e-12),   # config 5: 8192 x 1024 per shard
 ])
 def test_config_sharded_vs_one_shard(tmp_path, case, world, xtol):
+    """xtol against the one-shard solve: config 5's is the reference's own
+    spread between two decompositions (2.2e-12, manifest
+    reference_decomposition_spread), the band a different summation order of
+    the dots moves x by after 4556 iterations near m_crit."""
     rep = run_world("big", case, world, tmp_path, timeout=160)
+    print(json.dumps({k: v for k, v in rep.items() if k != "bitwise"}))
     for k, ok in rep["bitwise"].items():
         assert ok is True, (k, rep)
     one_conv, one_it = rep["one_cg"]
@@ -91,3 +101,20 @@ def test_config_sharded_vs_one_shard(tmp_path, case, world, xtol):
     assert conv == 1 and abs(it - one_it) <= max(1, one_it // 100), rep
     assert rep["relres"] < 1e-10, rep
     assert rep["x_rel"] <= xtol, rep
+    fx = rep.get("fixture")
+    if fx is not None:
+        # The sharded solve against the UNMODIFIED reference's own solve of the
+        # same inputs (tests/golden/l8192x8192_b2_m-0p19.npz: 2x4 MPI ranks;
+        # src/conjugate_gradient.cpp:4-66, dots with MPI_Allreduce at
+        # include/variables.h:190). The 8 t-shards are one more decomposition,
+        # so the bars are the reference's own spread between its 2x4 and 4x2
+        # decompositions (1x: x 2.2e-12, sum of squares 4.0e-12), never below
+        # the north star's 1e-12.
+        sp = fx["spread"]
+        x_bar = max([1e-12] + [s["x_rel_to_fixture"] for s in sp])
+        sq_bar = max([2e-12] + [s["sum_x2_rel_to_fixture"] for s in sp if "sum_x2_rel_to_fixture" in s])
+        assert abs(it - fx["cg_iters"]) <= max(1, fx["cg_iters"] // 100), (it, fx)
+        assert fx["x_rel"] <= x_bar, fx
+        assert fx["sumsq_rel"] <= sq_bar, fx
+    elif case.startswith("big:8192"):
+        pytest.fail("config 5 runs against the reference fixture; none matched")
