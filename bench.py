@@ -46,10 +46,10 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_SITE_APPLY = 96  # read psi 32 + U 32, write 32
 # algorithmic HBM bytes per site of one CG iteration, by path
 BYTES_PER_SITE_CG = {"recompute": 160, "twodir": 224, "sixkernel": 576}
-# the recompute-Ad pass reading the links as one-double codes (sm_cg_link_codes,
-# csrc/sm_linkcode.h; sm_cg_link_angles is its round-2 name): U is 16 instead
-# of 32 B/site of every pass
-BYTES_PER_SITE_CG_ANGLES = 144
+# the recompute-Ad pass reading the links as exact codes (sm_cg_link_codes,
+# csrc/sm_linkcode.h: one double + one 16-bit flag word per link;
+# sm_cg_link_angles is its round-2 name): U is 20 instead of 32 B/site
+BYTES_PER_SITE_CG_ANGLES = 148
 CG_PATH_ID = {"recompute": 5, "twodir": 4, "sixkernel": 0}
 
 # BASELINE.json configs on the GPU (1 and 2 are the CPU-plumbing / 1024^2 parity cases)
@@ -86,8 +86,11 @@ def parse(argv=None):
                     help="seconds before a rank that has not finished (e.g. stuck in ncclCommInitRank or a "
                          "mismatched collective) dumps its stacks and exits 124; the spawner then ends the others")
     ap.add_argument("--no-link-angles", action="store_true",
-                    help="recompute-Ad CG reads the complex links (160 B/site) instead of their one-double "
-                         "codes (144; the default from 4M sites per shard)")
+                    help="recompute-Ad CG reads the complex links (160 B/site) instead of their exact "
+                         "codes (148; the default from 4M sites per shard)")
+    ap.add_argument("--evolved-trajectories", type=int, default=50,
+                    help="N = 1: also time the CG on the field after this many pure-gauge leapfrog "
+                         "trajectories (the HMC's link update; 0 skips)")
     return ap.parse_args(argv)
 
 
@@ -440,6 +443,32 @@ def time_cg_steps(rt, sh, m0, cg_path, warmup, steps, link_angles_off=False, beg
     return max(wall, c0.elapsed_time(c1) / 1e3), cg_bytes_per_site(sh, cg_path)
 
 
+def time_evolved(args, rt, sh, cfg, m0):
+    """The CG rate on the bench field after `--evolved-trajectories`
+    leapfrog trajectories (sm_quenched_trajectory: HMC::Leapfrog with the gauge
+    force, 10 MD steps each, so |U| drifts off 1 by the rounding of
+    U <- U exp(i eps P), src/hmc.cpp:70-100). Reports whether the CG pass
+    still reads the exact link codes (sm_linkcode.h) and the rate it runs at.
+    Not part of the headline timing."""
+    sm = sh.sm
+    ntraj = args.evolved_trajectories
+    prm = sm.HMCParams(m0=m0, beta=5.0, tau=1.0, md_steps=10, cg_tol=1e-10, cg_max_iter=10000, seed=2024,
+                       even_odd=0)
+    t = time.perf_counter()
+    for k in range(ntraj):
+        sm.check(sm.lib.sm_quenched_trajectory(sh.L.ctx, ctypes.byref(prm), k))
+    t_md = time.perf_counter() - t
+    err, bad = ctypes.c_double(-1.0), ctypes.c_long(-1)
+    sm.check(sm.lib.sm_link_code_check(sh.L.ctx, None, ctypes.byref(err), ctypes.byref(bad)))
+    t_cg, bps = time_cg_steps(rt, sh, m0, args.cg_path, args.warmup, args.steps, args.no_link_angles)
+    return {"field": f"config-3 field after {ntraj} pure-gauge leapfrog trajectories (beta 5, 10 MD steps, "
+                     "sm_quenched_trajectory)",
+            "md_seconds": round(t_md, 3), "links_not_encodable": bad.value, "largest_decode_error": err.value,
+            "link_codes_in_use": bps == BYTES_PER_SITE_CG_ANGLES, "bytes_per_site": bps,
+            "value": round(args.steps / t_cg, 3), "ms_per_step": round(1e3 * t_cg / args.steps, 4),
+            "unit": "CG iterations/s"}
+
+
 def true_relres(sh, m0):
     """||phi - D D^dag x|| / ||phi|| over all shards (sm_dot_dev is global)."""
     import numpy as np
@@ -489,6 +518,7 @@ def run_config34(args, rt, cfg_id):
     apply_s = apply_time()
     t_cg, apply_s = max_over_ranks(rt, [t_cg, apply_s])
     V = sh.V
+    evolved = time_evolved(args, rt, sh, cfg, m0) if world == 1 and args.evolved_trajectories > 0 else None
     sh.close()
     weak = None
     if not args.no_weak:
@@ -542,6 +572,7 @@ def run_config34(args, rt, cfg_id):
                          "traffic_bytes_per_site": round(tr[2] / V, 2) if tr and len(tr) > 2 and tr[2] else None,
                          "reference_sequence_bytes_per_site": 576},
         "weak": weak,
+        "hmc_evolved_field": evolved,
         "placement_probe": placement,
     })
     print(json.dumps(line), flush=True)

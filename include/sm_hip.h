@@ -140,18 +140,20 @@ int sm_tune_cg(sm_ctx *ctx, int fused, int xchunk);
  * (1, 2 or 4; each wave owns 56 t-columns) and rows marched per block.
  * Values <= 0 keep the current setting. */
 int sm_tune_cg_geometry(sm_ctx *ctx, int waves_per_block, int xchunk);
-/* Compact links in the recompute-Ad CG pass (fused = 5, on by default): the
- * pass reads each link as ONE double, its smaller component with two flag
- * bits (16 instead of 32 B/site; 144 instead of 160 B/site per iteration),
- * and rebuilds the other component as +-sqrt(1 - v^2) in registers
- * (schwingermodel_amd/csrc/sm_linkcode.h). The codes are rebuilt at the first
- * solve after U changes, by a kernel that also decodes every code with the
- * pass's own decoder; they are used only if EVERY link comes back within
- * 2^-51 (4.4e-16) per component of the stored link (fresh exp(i theta)
- * links, as the reference's, src/gauge_conf.cpp:23-29, all do), else the
- * pass reads the complex links. D, D^dag and the force always use the
- * stored links bitwise. sm_cg_link_angles is the round-2 name of the same
- * call (the code was then the link's angle). */
+/* Compact links in the recompute-Ad CG pass (fused = 5, on by default from
+ * 4M sites per shard): the pass reads each link as its smaller component v
+ * (one double, exact) plus a 16-bit flag word -- which component v is, the
+ * sign of the other, and the other's offset in ulps from sqrt(1 - v^2) -- and
+ * rebuilds the link BITWISE in registers (schwingermodel_amd/csrc/
+ * sm_linkcode.h): 20 instead of 32 B/site of links, 148 instead of 160 B/site
+ * per iteration, and the same iterates as the complex-link pass. The codes are
+ * rebuilt at the first solve after U changes, by a kernel that also decodes
+ * every code with the pass's own decoder; they are used only if EVERY link
+ * comes back bitwise (it does unless a link is off the unit circle by more
+ * than ~1e-12 in |U|^2, far beyond the drift of the reference's leapfrog,
+ * src/hmc.cpp:70-100), else the pass reads the complex links. D, D^dag and
+ * the force always read the stored links. sm_cg_link_angles is the round-2
+ * name of the same call (the code was then the link's angle). */
 int sm_cg_link_codes(sm_ctx *ctx, int on, int *in_use);
 /* Round-2 name of sm_cg_link_codes; same behaviour, kept for old callers.
  * on: 1 / 0 enable / disable, < 0 keep; *in_use (may be NULL): 1 if the last
@@ -164,8 +166,9 @@ int sm_cg_link_angles(sm_ctx *ctx, int on, int *in_use);
 /* Diagnostic (tests): encode every link of the context's current U and decode
  * it again ON THE DEVICE with the CG pass's own functions. Writes the rebuilt
  * links to U_out_dev (device, the layout of sm_upload_gauge_dev; may be NULL),
- * the largest per-component |rebuilt - stored| to *max_err and the count of
- * links beyond 2^-51 to *n_bad (this shard only). Synchronous. */
+ * the largest per-component |rebuilt - stored| to *max_err (0 when every link
+ * comes back bitwise) and the count of links NOT rebuilt bitwise to *n_bad
+ * (this shard only). Synchronous. */
 int sm_link_code_check(sm_ctx *ctx, double *U_out_dev, double *max_err, long *n_bad);
 /* Streaming-bandwidth ceiling on the ctx stream (measured roofline reference):
  * out = a + b (two_reads = 1: the stencil's 2-read/1-write byte mix) or
@@ -324,6 +327,15 @@ typedef struct {
     int cg_failures;
 } sm_hmc_result;
 int sm_hmc_trajectory(sm_ctx *ctx, const sm_hmc_params *p, uint64_t traj, sm_hmc_result *out);
+
+/* One pure-gauge (quenched) molecular-dynamics trajectory on the device:
+ * HMC::Leapfrog (src/hmc.cpp:63-101, with its loop bound) driven by
+ * HMC::Force_G alone (:31-40, p->beta), momenta drawn for `traj` as in
+ * sm_hmc_trajectory; the evolved U is kept (no Metropolis step). No CG runs,
+ * so it evolves large fields cheaply through the leapfrog's own link update
+ * U <- U exp(i eps P), whose rounding moves |U| off 1 the way an HMC does
+ * (bench.py times the CG on such a field). p->m0, cg_* and even_odd unused. */
+int sm_quenched_trajectory(sm_ctx *ctx, const sm_hmc_params *p, uint64_t traj);
 
 /* HMC::HMC_algorithm (src/hmc.cpp:181-213): optional hot start
  * (GaugeConf::initialization, drawn on the device), Ntherm thermalisation

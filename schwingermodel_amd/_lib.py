@@ -114,6 +114,7 @@ def _load():
         "sm_hamiltonian": ([vp, ctypes.POINTER(HMCParams), vp, vp, vp, vp, ctypes.POINTER(HamiltonianTerms)], ci),
         "sm_hamiltonian_dev": ([vp, ctypes.POINTER(HMCParams), vp, vp, ctypes.POINTER(HamiltonianTerms)], ci),
         "sm_hmc_trajectory": ([vp, ctypes.POINTER(HMCParams), u64, ctypes.POINTER(HMCResult)], ci),
+        "sm_quenched_trajectory": ([vp, ctypes.POINTER(HMCParams), u64], ci),
         "sm_hmc_run": ([vp, ctypes.POINTER(HMCParams), ci, u64, ci, ci, ci, ctypes.c_char_p,
                         ctypes.POINTER(HMCSummary), vp, vp], ci),
         "sm_jackknife_error": ([vp, ci, ci], cd),

@@ -352,9 +352,12 @@ int exchange_ghost_U(sm_ctx *c) {
 // and so is its staleness (a wish change on one rank marks only that rank's
 // codes stale). So every solve on t-shards first all-reduces the count of
 // stale shards; when it is not 0, EVERY shard rebuilds and joins ONE
-// all-reduce of (links off the unit circle, shards not asking for codes), and
+// all-reduce of (links not encodable bitwise, shards not asking for codes), and
 // the codes are used only when both sums are 0. Every rank thus issues the
 // same collectives in the same order, whichever rank changed its wish.
+// Bytes of the codes of n links: n doubles (v) followed by n flag words.
+static size_t link_code_bytes(long n) { return (sizeof(double) + sizeof(uint16_t)) * (size_t)n; }
+
 int ensure_link_angles(sm_ctx *c) {
     if (c->cg_fused != 5 || c->racfg.fold < 2 || !cg_ra_ok(c)) return SM_OK;
     if (c->sharded()) {
@@ -368,11 +371,10 @@ int ensure_link_angles(sm_ctx *c) {
         return SM_OK;
     }
     if (c->link_angles) {
-        if (!c->Uang) HIP_TRY(stream_malloc(c, (void **)&c->Uang, sizeof(double) * 2 * (size_t)c->g.V));
-        if (c->sharded() && !c->Uang_face)
-            HIP_TRY(hipMalloc(&c->Uang_face, sizeof(double) * 16 * (size_t)c->g.Nx));
+        if (!c->Uang) HIP_TRY(stream_malloc(c, (void **)&c->Uang, link_code_bytes(2 * c->g.V)));
+        if (c->sharded() && !c->Uang_face) HIP_TRY(hipMalloc(&c->Uang_face, link_code_bytes(16 * (long)c->g.Nx)));
         const int nb = launch_link_codes(c->stream, 2 * c->g.V, c->U, c->Uang, c->partials);
-        launch_sum_partials(c->stream, nb, c->partials, c->sums);  // (links beyond SM_LINKCODE_TOL, 0)
+        launch_sum_partials(c->stream, nb, c->partials, c->sums);  // (links not rebuilt bitwise, 0)
     } else {
         c->h_sums[1] = make_double2(0.0, 1.0);                      // (0, this shard declines)
         HIP_TRY(hipMemcpyAsync(c->sums, c->h_sums + 1, sizeof(double2), hipMemcpyHostToDevice, c->stream));
@@ -613,7 +615,7 @@ static int placement_probe(sm_ctx *c, size_t fb) {
     if (M < 1 || c->hosted || c->pad_alloc == 0 || fb < (size_t(c->place_min_mib) << 20) || c->cg_fused != 5 ||
         c->racfg.fold < 2)
         return SM_OK;
-    const size_t ub = sizeof(double) * 2 * (size_t)c->g.V;
+    const size_t ub = link_code_bytes(2 * c->g.V);
     // the link codes are the pass's fifth stream: allocated here so the probe
     // times the real pass (their placement does not move the state)
     if (!c->Uang) HIP_TRY(stream_malloc(c, (void **)&c->Uang, ub));

@@ -13,8 +13,9 @@
 // same stencil code on the same operands, so it is bitwise the value pass j-1
 // used for its dots. A pass reads d_{j-1}, d_{j-2}, U (96 B/site) and writes
 // d_j (32), plus x on half the rows (32 on average): 160 B/site against 224
-// for mode 4 and 576 for the reference's sequence; 144 with
-// the links read as one-double codes (UC). Each x row takes its two updates together
+// for mode 4 and 576 for the reference's sequence; 148 with
+// the links read as exact codes (UC: one double and a 16-bit flag word per
+// link, sm_linkcode.h). Each x row takes its two updates together
 // every other pass, the even rows on even passes and the odd rows on odd
 // ones, so every pass moves the same bytes (with all of x on even passes the
 // odd pass was VALU-bound and the even one HBM-bound). The price of the
@@ -78,7 +79,8 @@ struct RAArgs {
     double mass;
     const double2 *prev;  // RED: pass j-1's partials
     long pass;
-    const double *Ua, *fUa;  // UC: link codes of U_t, U_x (plane stride V, sm_linkcode.h) and their 4-deep faces
+    const double *Ua, *fUa;  // UC: link codes v of U_t, U_x (plane stride V, sm_linkcode.h) and their 4-deep faces
+    const uint16_t *Uf, *fUf;  // UC: the codes' flag words (same layout; stored right after the codes)
     int xpar;                // XP: this pass updates x on the rows of parity xpar (= pass & 1)
     int pbase;               // partial slots: tile pbase + (t-block - tb0) * XB + x-chunk
     double2 *fsend;          // SH: != null -> the edge blocks also write d_j's 4-deep send faces
@@ -94,12 +96,18 @@ struct RAArgs {
     int flip, alt;
 };
 
-// U(1) link from its one-double code (UC; sm_linkcode.h: the smaller
-// component as stored, the other one by a square root, within 3 ulp) in place
-// of a 16-B load.
-__device__ __forceinline__ double2 u_of(double code) {
+// A link as the UC pass loads it: the code v and its flag word (sm_linkcode.h).
+struct LinkCode {
+    double v;
+    uint16_t f;
+};
+
+// U(1) link from its code (UC; sm_linkcode.h: the smaller component as
+// stored, the other one by a square root corrected by the flag word's ulp
+// offset -- bitwise the stored link) in place of a 16-B load.
+__device__ __forceinline__ double2 u_of(LinkCode code) {
     double c, s;
-    sm_link_decode(code, &c, &s);
+    sm_link_decode(code.v, code.f, &c, &s);
     return make_double2(c, s);
 }
 
@@ -248,11 +256,14 @@ __device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x
     const double mass = a.mass;
     const RSrc<double2> S1 = rsrc<SH>(a.d1, a.f1, c, a);
     const RSrc<double2> S2 = rsrc<SH>(a.d2, a.f2, c, a);
-    using LU = std::conditional_t<UC != 0, double, double2>;  // a link as loaded: code or complex
-    const RSrc<LU> SU = [&] {
+    using LU = std::conditional_t<UC != 0, LinkCode, double2>;  // a link as loaded: code or complex
+    using LV = std::conditional_t<UC != 0, double, double2>;    // its first (or only) stream
+    const RSrc<LV> SU = [&] {
         if constexpr (UC != 0) return rsrc<SH>(a.Ua, a.fUa, c, a);
         else return rsrc<SH>(a.U, a.fU, c, a);
     }();
+    // UC: the flag words, same strides as the codes (rsrc of the same column)
+    const uint16_t *SF = UC != 0 ? rsrc<SH>(a.Uf, a.fUf, c, a).p : nullptr;
     const int cx = c < 0 ? 0 : (c >= Wt ? Wt - 1 : c);
     auto wrap = [Nx](int x) { int w = x % Nx; return w < 0 ? w + Nx : w; };
     // REV marches the chunk from its last row to its first: virtual row v
@@ -270,10 +281,14 @@ __device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x
     };
     auto ldu = [&](int xr, LU &ut, LU &ux) {
         const int X = phys(min(xr, xe + 2));
-        const LU *p = SU.p + (long)wrap(X) * SU.xs;
-        ut = p[0];
-        if (REV) ux = SU.p[(long)wrap(X - 1) * SU.xs + SU.ps];
-        else ux = p[SU.ps];
+        const long ot = (long)wrap(X) * SU.xs, ox = (REV ? (long)wrap(X - 1) * SU.xs : ot) + SU.ps;
+        if constexpr (UC != 0) {
+            ut = LinkCode{SU.p[ot], SF[ot]};
+            ux = LinkCode{SU.p[ox], SF[ox]};
+        } else {
+            ut = SU.p[ot];
+            ux = SU.p[ox];
+        }
     };
     auto cvu = [](LU v) -> double2 {
         if constexpr (UC != 0) return u_of(v);
@@ -626,6 +641,8 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
     a.pass = pass;
     a.Ua = Uang;
     a.fUa = fUang;
+    a.Uf = Uang ? reinterpret_cast<const uint16_t *>(Uang + 2 * g.V) : nullptr;  // flag words after the codes
+    a.fUf = fUang ? reinterpret_cast<const uint16_t *>(fUang + 16 * (long)g.Nx) : nullptr;
     a.fsend = fsend;
     a.pbase = pbase;
     a.tick = tick;
@@ -691,18 +708,23 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
 }
 
 // Link codes for the UC passes (sm_linkcode.h) for each of the n links (both
-// planes), and per block the count of links whose code does not decode to
-// within SM_LINKCODE_TOL of the stored link in both components (the pass's
-// own decoder, so the bound holds for every link the pass rebuilds; one such
-// link and the field keeps the complex-link passes, sm_capi.cpp).
+// planes): codes v into Ua[0, n), flag words into the n uint16 after them, and
+// per block the count of links that are NOT encodable bitwise -- each code is
+// decoded again with the pass's own decoder and compared with the stored bits
+// (one such link and the field keeps the complex-link passes, sm_capi.cpp).
 __global__ void __launch_bounds__(256) link_code_kernel(long n, const double2 *U, double *Ua, double2 *part) {
     __shared__ double2 sh[4];
+    uint16_t *Uf = reinterpret_cast<uint16_t *>(Ua + n);
     double bad = 0.0;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
         const double2 u = U[i];
-        const double e = sm_link_encode(u.x, u.y);
-        Ua[i] = e;
-        if (!sm_link_code_ok(u.x, u.y, e)) bad += 1.0;  // NaN links too
+        double v, c2, s2;
+        uint16_t f;
+        const int ok = sm_link_encode(u.x, u.y, &v, &f);
+        sm_link_decode(v, f, &c2, &s2);
+        Ua[i] = v;
+        Uf[i] = f;
+        if (!ok || sm_lc_bits(c2) != sm_lc_bits(u.x) || sm_lc_bits(s2) != sm_lc_bits(u.y)) bad += 1.0;
     }
     const double2 b = block_sum(make_double2(bad, 0.0), sh);
     if (threadIdx.x == 0) part[blockIdx.x] = b;
@@ -714,6 +736,8 @@ int launch_link_codes(hipStream_t s, long n, const double2 *U, double *Ua, doubl
     return nb;
 }
 
+// Diagnostic: encode and decode every link on the device; the rebuilt links
+// (nullable out), per block (links not rebuilt bitwise, largest |difference|).
 __global__ void __launch_bounds__(256) link_code_check_kernel(long n, const double2 *U, double2 *out,
                                                              double2 *part) {
     __shared__ double2 sh[4];
@@ -721,12 +745,13 @@ __global__ void __launch_bounds__(256) link_code_check_kernel(long n, const doub
     double bad = 0.0, mx = 0.0;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
         const double2 u = U[i];
-        const double e = sm_link_encode(u.x, u.y);
-        double c2, s2;
-        sm_link_decode(e, &c2, &s2);
+        double v, c2, s2;
+        uint16_t f;
+        const int ok = sm_link_encode(u.x, u.y, &v, &f);
+        sm_link_decode(v, f, &c2, &s2);
         if (out) out[i] = make_double2(c2, s2);
         const double err = fmax(fabs(c2 - u.x), fabs(s2 - u.y));
-        if (!sm_link_code_ok(u.x, u.y, e)) bad += 1.0;
+        if (!ok || sm_lc_bits(c2) != sm_lc_bits(u.x) || sm_lc_bits(s2) != sm_lc_bits(u.y)) bad += 1.0;
         mx = err > mx || err != err ? err : mx;
     }
     shm[threadIdx.x] = mx;
@@ -745,9 +770,16 @@ int launch_link_code_check(hipStream_t s, long n, const double2 *U, double2 *out
     return nb;
 }
 
+// Codes of the n ghost links of a t-shard face (codes, then flag words).
 __global__ void __launch_bounds__(256) codes_of_kernel(long n, const double2 *U, double *Ua) {
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-        Ua[i] = sm_link_encode(U[i].x, U[i].y);
+    uint16_t *Uf = reinterpret_cast<uint16_t *>(Ua + n);
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        double v;
+        uint16_t f;
+        sm_link_encode(U[i].x, U[i].y, &v, &f);
+        Ua[i] = v;
+        Uf[i] = f;
+    }
 }
 
 void launch_codes_of(hipStream_t s, long n, const double2 *U, double *Ua) {

@@ -72,9 +72,11 @@ struct sm_ctx {
     int cg_flush_nparts = 0;        // its partial count (the one-pass or the recompute-Ad grid)
     int cg_ra_red_max_blocks = 512; // recompute-Ad pass: redundant scalars up to this many blocks (one shard)
     // recompute-Ad pass with compact links (sm_cgra.hip UC): U enters the CG as
-    // one double per link (sm_linkcode.h, 16 B/site), rebuilt in registers.
+    // one double + one 16-bit flag word per link (sm_linkcode.h, 20 B/site),
+    // rebuilt bitwise in registers.
     // Built at the first solve after U changes (uang_state 0); state 1 = in
-    // use, 2 = some link is off the unit circle, so the complex links are used.
+    // use, 2 = some link is not encodable (far off the unit circle, NaN), so
+    // the complex links are used.
     int link_angles = 1;
     int uang_state = 0;
     // Placement of the buffers the CG pass streams (stream_malloc): 5 = an

@@ -149,15 +149,15 @@ constexpr int kMaxTickGroups = 1024;
 // (partial slot of a tile: pbase + (t-block - tb0) * XB + x-chunk; fsend (t-shards):
 // the blocks owning columns 0..3 / Wt-4..Wt-1 also write d_j's 4-deep send
 // faces, lo at fsend and hi at fsend + 8 Nx, as launch_pack_faces_k would)
-// Link codes of U for the passes above (Uang: 16 instead of 32 B/site of
-// links, sm_linkcode.h): writes the one-double code of n links and, per block,
-// the count of links whose code does not rebuild them to within
-// SM_LINKCODE_TOL (sm_linkcode.h) to partials;
-// returns the block count.
+// Link codes of U for the passes above (Uang: 20 instead of 32 B/site of
+// links, sm_linkcode.h): writes the codes v of n links to Ua[0, n) and their
+// flag words to the n uint16 right after them, and per block the count of
+// links the pass's decoder does NOT rebuild bitwise to partials; returns the
+// block count.
 int launch_link_codes(hipStream_t s, long n, const double2 *U, double *Ua, double2 *partials);
-void launch_codes_of(hipStream_t s, long n, const double2 *U, double *Ua);  // faces: codes only
+void launch_codes_of(hipStream_t s, long n, const double2 *U, double *Ua);  // faces: codes + flags only
 // Diagnostic: encode + decode each of n links (the pass's functions) into
-// out (may be null); per block (count beyond SM_LINKCODE_TOL, largest
+// out (may be null); per block (count not rebuilt bitwise, largest
 // per-component error) to partials; returns the block count.
 int launch_link_code_check(hipStream_t s, long n, const double2 *U, double2 *out, double2 *partials);
 // Recompute-Ad CG: after the last pass add alpha_{k-1} d_{k-1} to the rows

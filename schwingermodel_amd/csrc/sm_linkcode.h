@@ -1,39 +1,45 @@
-// sm_linkcode.h -- one double per U(1) link for the compact-link CG pass
-// (sm_cgra.hip, UC): 8 instead of 16 B per link, decoded with one square root.
+// sm_linkcode.h -- exact compact U(1) links for the recompute-Ad CG pass
+// (sm_cgra.hip, UC): 10 instead of 16 B per link, decoded with one square
+// root, and BITWISE the stored link.
 //
-// A unit link U = (c, s) is stored as its smaller component v (s if |s| <= |c|,
-// else c) with two flags in the two lowest mantissa bits: bit 1 = v is the
-// cosine, bit 0 = the other component is negative. The decoder takes v as
-// stored and rebuilds the other one as +-sqrt(1 - v^2), formed as
-// sqrt(fma(-v, v, 1)). Because |v| <= 1/sqrt(2), 1 - v^2 >= 1/2 and the
-// square root's sensitivity to v is |v| / sqrt(1 - v^2) <= 1. For a link ON
-// the unit circle the rebuilt link is within 3 ulp (3.5e-16 absolute) per
-// component (the flags move v by <= 2 ulp, the fma and the square root round
-// once each; tests/test_linkcode_host.py). A link OFF the circle by
-// delta = | |U|^2 - 1 | comes back with its larger component moved by a further
-// ~delta / (2 |w|) <= 0.71 delta, because the decoder puts it back on the circle.
+// A link U = (c, s) is stored as
+//   v  (double): its smaller component (s if |s| <= |c|, else c), exactly as
+//      stored, all 64 bits;
+//   f  (uint16): bit 0 = the other component w is negative, bit 1 = v is the
+//      cosine, bits 2..15 = a signed 14-bit count k of ulps between |w| and the
+//      decoder's root r = sqrt(1 - v^2) (formed as sqrt(fma(-v, v, 1))).
+// The decoder rebuilds |w| as the double whose bit pattern is bits(r) + k
+// (positive doubles are ordered like their bit patterns, so this counts ulps
+// across a binade boundary too, e.g. |w| = 1.0 against r = 1 - 2^-53), then
+// sets its sign from bit 0. Encoder and decoder evaluate r with the SAME
+// function, so every encodable link decodes to its stored bits exactly. A
+// link is encodable iff both components are finite and |k| <= 8191: for a
+// unit link k is 0..3 (r is within 1 ulp of the true root and |w| within a few
+// ulps of it); a link pushed off the unit circle by delta = | |U|^2 - 1 |
+// has |k| ~ delta / (2 |w| 2^-53), so 8191 covers delta up to ~1e-12. The
+// reference's leapfrog multiplies U by exp(i eps P) every MD step
+// (src/hmc.cpp:70-100) without re-unitarising, so |U| takes a random walk of
+// ~0.55 sqrt(steps) ulps (a numpy model of the update: 379 ulps at most after
+// 20000 steps of 200 000 links); it reaches the 14-bit range only after ~10^7
+// steps. Round 4's codes kept v's two flag bits in its mantissa and accepted a
+// link within 2^-51 of its stored components, so the first ~20 trajectories
+// of an HMC pushed fields out of range (the pass then read complex links) and
+// the pass's operator differed from D D^dag by a few ulps.
 //
-// So the guarantee is enforced link by link instead of assumed: the device
-// kernel that builds the codes (sm_cgra.hip link_code_kernel) decodes every
-// code with this same function and counts the links whose rebuilt components
-// differ from the stored ones by more than SM_LINKCODE_TOL = 2^-51 (4.4e-16,
-// 4 ulp of a component in [1/2, 1)). One such link anywhere and the field keeps
-// the complex-link passes (sm_capi.cpp ensure_link_angles). Fresh exp(i theta)
-// links (src/gauge_conf.cpp:23-29, the generator here) all pass: the config-3
-// field generated on the device comes back within 2^-51 exactly (its links sit
-// a few ulp off the circle; tests/test_gpu_parity.py). Links pushed off the
-// circle by more than ~1.6e-15 in |U|^2 never pass (their larger component
-// moves by >= delta / 2 - 3.5e-16), which is where many leapfrog updates
-// (U <- U exp(i eps P), rounded each time) eventually take a field.
+// Device layout (sm_capi.cpp ensure_link_angles): one allocation holds the
+// codes v of both planes (2V doubles: U_t plane, then U_x plane) followed by
+// the flags f (2V uint16, same order); the t-shard ghost faces likewise
+// (16 Nx doubles, then 16 Nx uint16).
 // Plain C as well, so tests/test_linkcode_host.py runs the same code on the
-// host (with a perturbed reciprocal-square-root seed to model v_rsq_f64);
-// tests/test_gpu_parity.py checks the device's own decode.
+// host (with a perturbed reciprocal-square-root seed to model v_rsq_f64; the
+// host pair is exact for the host's own root, as the device pair is for the
+// device's); tests/test_gpu_parity.py checks the device's own round trip.
 #pragma once
 
 #include <stdint.h>
 #include <string.h>
 
-#define SM_LINKCODE_TOL 0x1p-51  // per component, absolute: the acceptance bound above
+#define SM_LINKCODE_KMAX 8191  // largest |k| a flag word holds (14-bit signed)
 
 #ifdef __HIPCC__
 #define SM_LINKCODE_FN __host__ __device__ __forceinline__
@@ -53,24 +59,12 @@ SM_LINKCODE_FN double sm_lc_double(uint64_t b) {
     return v;
 }
 
-SM_LINKCODE_FN double sm_link_encode(double c, double s) {
-    const int cosv = __builtin_fabs(s) > __builtin_fabs(c);  // store the cosine (the sine is the larger)
-    const double v = cosv ? c : s, w = cosv ? s : c;
-    const uint64_t f = ((uint64_t)cosv << 1) | (uint64_t)(__builtin_signbit(w) != 0);
-    const uint64_t b = sm_lc_bits(v);
-    // nearest bit pattern whose low two bits are f: |change| <= 2 in the
-    // magnitude bits (sign-magnitude, so it moves v by <= 2 ulp)
-    const uint64_t d = (f - b) & 3u;
-    const uint64_t mag = b & 0x7fffffffffffffffull;
-    const uint64_t e = (d == 3 && mag != 0) ? b - 1 : b + d;
-    return sm_lc_double(e);
-}
-
-// sqrt(a) for a in [1/2, 1] (no scaling, no special cases): the hardware
+// sqrt(a) for a in ~[1/2, 1] (no scaling, no special cases): the hardware
 // reciprocal square root (~2^-23 relative) on the device, 1 / sqrt on the host,
 // then one Goldschmidt step (error ~2^-46) and one Newton correction of the
 // root (~2^-92 before rounding): within 1 ulp, ~8 operations against ~18 for
-// the general correctly rounded square root.
+// the general correctly rounded square root. Exactness of the codes does not
+// depend on this accuracy (the offset k absorbs it), only their range does.
 SM_LINKCODE_FN double sm_lc_sqrt_half1(double a) {
 #ifdef __HIP_DEVICE_COMPILE__
     const double y = __builtin_amdgcn_rsq(a);
@@ -88,20 +82,37 @@ SM_LINKCODE_FN double sm_lc_sqrt_half1(double a) {
     return __builtin_fma(d, h, g);
 }
 
-SM_LINKCODE_FN void sm_link_decode(double e, double *c_out, double *s_out) {
-    const uint64_t b = sm_lc_bits(e);
-    const double r = sm_lc_sqrt_half1(__builtin_fma(-e, e, 1.0));
-    const double w = (b & 1u) ? -r : r;
-    const int cosv = (int)((b >> 1) & 1u);
-    *c_out = cosv ? e : w;
-    *s_out = cosv ? w : e;
+// The decoder's root for code v.
+SM_LINKCODE_FN double sm_lc_root(double v) { return sm_lc_sqrt_half1(__builtin_fma(-v, v, 1.0)); }
+
+// Code (v, f) of link (c, s); returns 1 iff the link is encodable (then the
+// decoder gives back c and s bitwise), else 0 with f = 0.
+SM_LINKCODE_FN int sm_link_encode(double c, double s, double *v_out, uint16_t *f_out) {
+    const int cosv = __builtin_fabs(s) > __builtin_fabs(c);  // store the cosine (the sine is the larger)
+    const double v = cosv ? c : s, w = cosv ? s : c;
+    *v_out = v;
+    *f_out = 0;
+    if (!(c - c == 0.0 && s - s == 0.0)) return 0;  // NaN / Inf
+    const int64_t k = (int64_t)sm_lc_bits(__builtin_fabs(w)) - (int64_t)sm_lc_bits(sm_lc_root(v));
+    if (k < -SM_LINKCODE_KMAX || k > SM_LINKCODE_KMAX) return 0;
+    *f_out = (uint16_t)(((uint32_t)(int32_t)k << 2) | ((uint32_t)cosv << 1) | (uint32_t)(__builtin_signbit(w) != 0));
+    return 1;
 }
 
-// 1 iff the code e of link (c, s) decodes to within SM_LINKCODE_TOL of it in
-// both components (0 for NaN / Inf links).
-SM_LINKCODE_FN int sm_link_code_ok(double c, double s, double e) {
-    double c2, s2;
-    sm_link_decode(e, &c2, &s2);
-    const double err = __builtin_fmax(__builtin_fabs(c2 - c), __builtin_fabs(s2 - s));
-    return err <= SM_LINKCODE_TOL && c - c == 0.0 && s - s == 0.0;
+SM_LINKCODE_FN void sm_link_decode(double v, uint16_t f, double *c_out, double *s_out) {
+    const int64_t k = (int64_t)((int16_t)f >> 2);  // arithmetic shift: the signed offset
+    const uint64_t wb = (uint64_t)((int64_t)sm_lc_bits(sm_lc_root(v)) + k) | ((uint64_t)(f & 1u) << 63);
+    const double w = sm_lc_double(wb);
+    const int cosv = (int)((f >> 1) & 1u);
+    *c_out = cosv ? v : w;
+    *s_out = cosv ? w : v;
+}
+
+// 1 iff link (c, s) is encodable and its code decodes to it bitwise.
+SM_LINKCODE_FN int sm_link_code_ok(double c, double s) {
+    double v, c2, s2;
+    uint16_t f;
+    if (!sm_link_encode(c, s, &v, &f)) return 0;
+    sm_link_decode(v, f, &c2, &s2);
+    return sm_lc_bits(c2) == sm_lc_bits(c) && sm_lc_bits(s2) == sm_lc_bits(s);
 }

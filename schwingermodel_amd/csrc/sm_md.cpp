@@ -254,6 +254,33 @@ int sm_hamiltonian(sm_ctx *c, const sm_hmc_params *p, const double *phi0, const 
     return sm_hamiltonian_dev(c, p, (const double *)phi, c->Pmd, out);
 }
 
+int sm_quenched_trajectory(sm_ctx *c, const sm_hmc_params *p, uint64_t traj) {
+    TRY(check_ready(c));
+    TRY(check_params(p));
+    HIP_TRY(hipSetDevice(c->device));
+    TRY(ensure_md(c));
+    // HMC::Leapfrog (src/hmc.cpp:63-101, its loop bound included) with
+    // HMC::Force_G alone (:31-40): the fermion force is dropped, so no CG runs
+    launch_draw_momenta(c->stream, c->g, sm_traj_seed(p->seed, traj), c->Pmd);  // RandomPI
+    const double eps = p->tau / (p->md_steps * 1.0);
+    const size_t rb = sizeof(double) * 2 * (size_t)c->g.V;
+    auto force = [&]() -> int {
+        HIP_TRY(hipMemsetAsync(c->Fmd, 0, rb, c->stream));
+        launch_staple_force(c->stream, c->g, c->kshards(), c->U, ufaces(c), p->beta, c->Fmd, nullptr);
+        HIP_TRY(hipGetLastError());
+        return SM_OK;
+    };
+    TRY(md_step(c, c->Pmd, eps, 0, 0.5 * eps));
+    TRY(force());
+    for (int step = 1; step < p->md_steps - 1; step++) {
+        TRY(md_step(c, c->Pmd, eps, 1, eps));
+        TRY(force());
+    }
+    TRY(md_step(c, c->Pmd, eps, 1, 0.5 * eps));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SM_OK;
+}
+
 int sm_hmc_trajectory(sm_ctx *c, const sm_hmc_params *p, uint64_t traj, sm_hmc_result *out) {
     TRY(check_ready(c));
     TRY(check_params(p));
