@@ -46,10 +46,11 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_SITE_APPLY = 96  # read psi 32 + U 32, write 32
 # algorithmic HBM bytes per site of one CG iteration, by path
 BYTES_PER_SITE_CG = {"recompute": 160, "twodir": 224, "sixkernel": 576}
-# the recompute-Ad pass reading the links as exact codes (sm_cg_link_codes,
-# csrc/sm_linkcode.h: one double + one 16-bit flag word per link;
-# sm_cg_link_angles is its round-2 name): U is 20 instead of 32 B/site
-BYTES_PER_SITE_CG_ANGLES = 148
+# the recompute-Ad pass streams 128 B/site besides the links; it reads the
+# links as exact codes (sm_cg_link_codes, csrc/sm_linkcode.h): 17 B/site with
+# both links' flag nibbles packed in one byte (fresh fields), 20 with 16-bit
+# flag words, 32 as complex links (sm_cg_link_bytes reports which)
+BYTES_PER_SITE_CG_NOLINKS = 128
 CG_PATH_ID = {"recompute": 5, "twodir": 4, "sixkernel": 0}
 
 # BASELINE.json configs on the GPU (1 and 2 are the CPU-plumbing / 1024^2 parity cases)
@@ -87,7 +88,7 @@ def parse(argv=None):
                          "mismatched collective) dumps its stacks and exits 124; the spawner then ends the others")
     ap.add_argument("--no-link-angles", action="store_true",
                     help="recompute-Ad CG reads the complex links (160 B/site) instead of their exact "
-                         "codes (148; the default from 4M sites per shard)")
+                         "codes (145 or 148; the default from 4M sites per shard)")
     ap.add_argument("--evolved-trajectories", type=int, default=50,
                     help="N = 1: also time the CG on the field after this many pure-gauge leapfrog "
                          "trajectories (the HMC's link update; 0 skips)")
@@ -401,9 +402,11 @@ def placement_report(sh):
 def cg_bytes_per_site(sh, cg_path):
     """Algorithmic bytes per site of the CG iteration the last solve ran."""
     sm = sh.sm
-    u = ctypes.c_int(0)
-    sm.check(sm.lib.sm_cg_link_angles(sh.L.ctx, -1, ctypes.byref(u)))
-    return BYTES_PER_SITE_CG_ANGLES if (cg_path == "recompute" and u.value) else BYTES_PER_SITE_CG[cg_path]
+    if cg_path != "recompute":
+        return BYTES_PER_SITE_CG[cg_path]
+    b = ctypes.c_int(0)
+    sm.check(sm.lib.sm_cg_link_bytes(sh.L.ctx, ctypes.byref(b)))
+    return BYTES_PER_SITE_CG_NOLINKS + b.value
 
 
 def begin_cg(sh, m0, cg_path, link_angles_off=False):
@@ -464,7 +467,7 @@ def time_evolved(args, rt, sh, cfg, m0):
     return {"field": f"config-3 field after {ntraj} pure-gauge leapfrog trajectories (beta 5, 10 MD steps, "
                      "sm_quenched_trajectory)",
             "md_seconds": round(t_md, 3), "links_not_encodable": bad.value, "largest_decode_error": err.value,
-            "link_codes_in_use": bps == BYTES_PER_SITE_CG_ANGLES, "bytes_per_site": bps,
+            "link_codes_in_use": bps < BYTES_PER_SITE_CG["recompute"], "bytes_per_site": bps,
             "value": round(args.steps / t_cg, 3), "ms_per_step": round(1e3 * t_cg / args.steps, 4),
             "unit": "CG iterations/s"}
 
@@ -563,7 +566,7 @@ def run_config34(args, rt, cfg_id):
         "cpu_baseline": cpu,
         # the CG iteration's own streaming rate (informational; the graded
         # roofline is the Dirac apply's): algorithmic bytes / time per step
-        "cg_iteration": {"path": args.cg_path, "link_angles": cg_bps == BYTES_PER_SITE_CG_ANGLES,
+        "cg_iteration": {"path": args.cg_path, "link_codes": cg_bps < BYTES_PER_SITE_CG["recompute"],
                          "bytes_per_site": cg_bps,
                          "achieved_GBps_per_gpu": round(cg_bps * V * it_per_s / 1e9, 1),
                          "frac_of_peak": round(cg_bps * V * it_per_s / 1e9 / HBM_PEAK_GBPS, 4),
@@ -615,7 +618,7 @@ def run_config5(args, rt):
         "iterations": res.iterations, "converged": res.converged,
         "cg_residual_rel": res.residual / res.phi_norm if res.phi_norm else None,
         "true_relres": rel,
-        "cg_iteration": {"path": args.cg_path, "link_angles": cg_bps == BYTES_PER_SITE_CG_ANGLES,
+        "cg_iteration": {"path": args.cg_path, "link_codes": cg_bps < BYTES_PER_SITE_CG["recompute"],
                          "bytes_per_site": cg_bps,
                          "achieved_GBps_per_gpu": round(cg_bps * V * res.iterations / dt / 1e9, 1)},
         "placement_probe": placement,

@@ -163,6 +163,12 @@ int sm_cg_link_codes(sm_ctx *ctx, int on, int *in_use);
  * rank); if it is not 0 every shard rebuilds and the codes are used only if
  * every shard asks for them (one more all-reduce, which every shard joins). */
 int sm_cg_link_angles(sm_ctx *ctx, int on, int *in_use);
+/* Bytes of link data per site the recompute-Ad CG pass read in the last
+ * solve: 32 (complex links), 20 (codes with 16-bit flag words) or 17 (codes
+ * with the flag nibbles of both links packed into one byte, the form every
+ * field takes whose ulp offsets all lie in [-2, 1], e.g. fresh exp(i theta)
+ * fields). A pass streams 128 B/site besides. */
+int sm_cg_link_bytes(const sm_ctx *ctx, int *bytes_per_site);
 /* Diagnostic (tests): encode every link of the context's current U and decode
  * it again ON THE DEVICE with the CG pass's own functions. Writes the rebuilt
  * links to U_out_dev (device, the layout of sm_upload_gauge_dev; may be NULL),

@@ -99,6 +99,7 @@ def _load():
         "sm_cg_link_codes": ([vp, ci, ctypes.POINTER(ci)], ci),
         "sm_cg_link_angles": ([vp, ci, ctypes.POINTER(ci)], ci),
         "sm_link_code_check": ([vp, vp, ctypes.POINTER(cd), ctypes.POINTER(ctypes.c_long)], ci),
+        "sm_cg_link_bytes": ([vp, ctypes.POINTER(ci)], ci),
         "sm_tune_cg_geometry": ([vp, ci, ci], ci),
         # gauge field / molecular dynamics / HMC
         "sm_download_gauge": ([vp, vp, vp], ci),

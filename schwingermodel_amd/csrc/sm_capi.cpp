@@ -355,8 +355,9 @@ int exchange_ghost_U(sm_ctx *c) {
 // all-reduce of (links not encodable bitwise, shards not asking for codes), and
 // the codes are used only when both sums are 0. Every rank thus issues the
 // same collectives in the same order, whichever rank changed its wish.
-// Bytes of the codes of n links: n doubles (v) followed by n flag words.
-static size_t link_code_bytes(long n) { return (sizeof(double) + sizeof(uint16_t)) * (size_t)n; }
+// Bytes of the codes of n links (sm_linkcode.h): n doubles (v), n flag words,
+// then the packed form's flag bytes (one per site = per two links).
+static size_t link_code_bytes(long n) { return (sizeof(double) + sizeof(uint16_t)) * (size_t)n + (size_t)(n + 1) / 2; }
 
 int ensure_link_angles(sm_ctx *c) {
     if (c->cg_fused != 5 || c->racfg.fold < 2 || !cg_ra_ok(c)) return SM_OK;
@@ -370,20 +371,31 @@ int ensure_link_angles(sm_ctx *c) {
     } else if (c->uang_state != 0 || !c->link_angles) {
         return SM_OK;
     }
+    // sums[0] = (links not rebuilt bitwise, links whose flag word needs 16
+    // bits), sums[1] = (shards declining the codes, 0), all-reduced together
     if (c->link_angles) {
         if (!c->Uang) HIP_TRY(stream_malloc(c, (void **)&c->Uang, link_code_bytes(2 * c->g.V)));
         if (c->sharded() && !c->Uang_face) HIP_TRY(hipMalloc(&c->Uang_face, link_code_bytes(16 * (long)c->g.Nx)));
         const int nb = launch_link_codes(c->stream, 2 * c->g.V, c->U, c->Uang, c->partials);
-        launch_sum_partials(c->stream, nb, c->partials, c->sums);  // (links not rebuilt bitwise, 0)
+        launch_sum_partials(c->stream, nb, c->partials, c->sums);
+        HIP_TRY(hipMemsetAsync(c->sums + 1, 0, sizeof(double2), c->stream));
     } else {
-        c->h_sums[1] = make_double2(0.0, 1.0);                      // (0, this shard declines)
-        HIP_TRY(hipMemcpyAsync(c->sums, c->h_sums + 1, sizeof(double2), hipMemcpyHostToDevice, c->stream));
+        c->h_sums[1] = make_double2(0.0, 0.0);
+        c->h_sums[2] = make_double2(1.0, 0.0);  // this shard declines
+        HIP_TRY(hipMemcpyAsync(c->sums, c->h_sums + 1, 2 * sizeof(double2), hipMemcpyHostToDevice, c->stream));
     }
-    TRY(allreduce_dev(c, (double *)c->sums, 2));
-    HIP_TRY(hipMemcpyAsync(c->h_sums, c->sums, sizeof(double2), hipMemcpyDeviceToHost, c->stream));
+    TRY(allreduce_dev(c, (double *)c->sums, 4));
+    HIP_TRY(hipMemcpyAsync(c->h_sums, c->sums, 2 * sizeof(double2), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    c->uang_state = c->h_sums[0].x == 0.0 && c->h_sums[0].y == 0.0 ? 1 : 2;
-    if (c->uang_state == 1 && c->sharded()) launch_codes_of(c->stream, 16 * (long)c->g.Nx, face4_recv_U(c), c->Uang_face);
+    c->uang_state = c->h_sums[0].x == 0.0 && c->h_sums[1].x == 0.0 ? 1 : 2;
+    // the packed flags (one byte per site) when every flag word fits a nibble
+    // on every shard, else the 16-bit flag words
+    c->link_fmt = c->h_sums[0].y == 0.0 ? 2 : 1;
+    if (c->uang_state == 1 && c->link_fmt == 2) launch_link_nibbles(c->stream, c->g.V, c->Uang);
+    if (c->uang_state == 1 && c->sharded()) {
+        launch_codes_of(c->stream, 16 * (long)c->g.Nx, face4_recv_U(c), c->Uang_face);
+        if (c->link_fmt == 2) launch_face_nibbles(c->stream, c->g.Nx, c->Uang_face);
+    }
     HIP_TRY(hipGetLastError());
     return SM_OK;
 }
@@ -657,7 +669,7 @@ static int placement_probe(sm_ctx *c, size_t fb) {
                 launch_cg_ra(c->own_stream, g, c->racfg, 1, d[(j + 2) % 3], d[(j + 1) % 3], d[j % 3], (double2 *)f[3],
                              nullptr, nullptr, nullptr, nullptr, 1.94, j, c->sc, c->partials, 0, c->racfg.TBk,
                              nullptr, c->Uang, nullptr, nullptr, 0, tail ? c->tick : nullptr, nparts, c->gsum,
-                             nullptr);
+                             nullptr, 0, 2);  // the packed flags: what fresh fields take
             float ms = 0.f;
             if (hipEventRecord(ev[1], c->own_stream) != hipSuccess || hipEventSynchronize(ev[1]) != hipSuccess ||
                 hipEventElapsedTime(&ms, ev[0], ev[1]) != hipSuccess || hipGetLastError() != hipSuccess)
@@ -970,6 +982,13 @@ int sm_tune_cg_geometry(sm_ctx *c, int waves_per_block, int xchunk) {
 
 int sm_cg_link_angles(sm_ctx *c, int on, int *in_use) { return sm_cg_link_codes(c, on, in_use); }
 
+int sm_cg_link_bytes(const sm_ctx *c, int *bytes_per_site) {
+    if (!c || !bytes_per_site) return fail(SM_ERR_ARG, "null argument");
+    const bool codes = c->link_angles && c->cg_fused == 5 && c->uang_state == 1;
+    *bytes_per_site = !codes ? 32 : (c->link_fmt == 2 ? 17 : 20);
+    return SM_OK;
+}
+
 int sm_link_code_check(sm_ctx *c, double *U_out, double *max_err, long *n_bad) {
     TRY(check_ready(c));
     if (!max_err || !n_bad) return fail(SM_ERR_ARG, "null argument");
@@ -1250,7 +1269,7 @@ static int cg_ra_pass(sm_ctx *c) {
         const bool tail = !red && c->cg_tail && fc.fold >= 2 && (nparts + 63) / 64 <= kMaxTickGroups;
         launch_cg_ra(c->stream, c->g, fc, 1, d1, d2, dn, c->cg_x, c->U, nullptr, nullptr, nullptr, c->cg_mass, j,
                      c->sc, part, 0, fc.TBk, prev, ua, nullptr, nullptr, 0, tail ? c->tick : nullptr, nparts, c->gsum,
-                     nullptr);
+                     nullptr, 0, c->link_fmt);
         if (red) {
             c->cg_flush_pass = j;
             c->cg_flush_nparts = nparts;
@@ -1300,7 +1319,7 @@ static int cg_ra_pass(sm_ctx *c) {
     auto pass = [&](const CGFusedCfg &cf, int tb0, int tbn, hipStream_t st, int pbase, double2 *fsend) {
         launch_cg_ra(st, c->g, cf, c->kshards(), d1, d2, dn, c->cg_x, c->U, f1, f2, face4_recv_U(c), c->cg_mass, j,
                      c->sc, c->partials, tb0, tbn, nullptr, ua, c->Uang_face, fsend, pbase, tail ? c->tick : nullptr,
-                     nparts_pass, c->gsum, sums, red ? 1 : 0);
+                     nparts_pass, c->gsum, sums, red ? 1 : 0, c->link_fmt);
     };
     HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));

@@ -80,7 +80,9 @@ struct RAArgs {
     const double2 *prev;  // RED: pass j-1's partials
     long pass;
     const double *Ua, *fUa;  // UC: link codes v of U_t, U_x (plane stride V, sm_linkcode.h) and their 4-deep faces
-    const uint16_t *Uf, *fUf;  // UC: the codes' flag words (same layout; stored right after the codes)
+    const uint16_t *Uf, *fUf;  // UC 1: the codes' flag words (same layout; stored right after the codes)
+    const uint8_t *Ub, *fUb;   // UC 2: one byte per site, the U_t (low) and U_x (high) flag nibbles
+                               // (after the flag words; faces [col][x])
     int xpar;                // XP: this pass updates x on the rows of parity xpar (= pass & 1)
     int pbase;               // partial slots: tile pbase + (t-block - tb0) * XB + x-chunk
     double2 *fsend;          // SH: != null -> the edge blocks also write d_j's 4-deep send faces
@@ -96,18 +98,23 @@ struct RAArgs {
     int flip, alt;
 };
 
-// A link as the UC pass loads it: the code v and its flag word (sm_linkcode.h).
+// A link as the UC pass loads it: the code v and its flag word (UC 1), or the
+// site's flag byte of two nibbles (UC 2), as loaded (converted only when the
+// link is decoded, so the load stays a prefetch).
 struct LinkCode {
     double v;
-    uint16_t f;
+    uint32_t f;
 };
 
 // U(1) link from its code (UC; sm_linkcode.h: the smaller component as
 // stored, the other one by a square root corrected by the flag word's ulp
-// offset -- bitwise the stored link) in place of a 16-B load.
-__device__ __forceinline__ double2 u_of(LinkCode code) {
+// offset -- bitwise the stored link) in place of a 16-B load. UC 2: the
+// nibble at bit `shift` of the flag byte.
+template <int UC>
+__device__ __forceinline__ double2 u_of(LinkCode code, int shift) {
     double c, s;
-    sm_link_decode(code.v, code.f, &c, &s);
+    const uint16_t f = UC == 2 ? sm_lc_flags_of_nibble(code.f >> shift) : (uint16_t)code.f;
+    sm_link_decode(code.v, f, &c, &s);
     return make_double2(c, s);
 }
 
@@ -262,8 +269,26 @@ __device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x
         if constexpr (UC != 0) return rsrc<SH>(a.Ua, a.fUa, c, a);
         else return rsrc<SH>(a.U, a.fU, c, a);
     }();
-    // UC: the flag words, same strides as the codes (rsrc of the same column)
-    const uint16_t *SF = UC != 0 ? rsrc<SH>(a.Uf, a.fUf, c, a).p : nullptr;
+    // UC 1: the flag words, same strides as the codes (rsrc of the same column)
+    const uint16_t *SF = UC == 1 ? rsrc<SH>(a.Uf, a.fUf, c, a).p : nullptr;
+    // UC 2: the flag bytes of this column, one per site (in-domain rows Wt
+    // apart; a received face's [col][x] rows 1 apart)
+    long bxs = a.Wt;
+    const uint8_t *SB = nullptr;
+    if constexpr (UC == 2) {
+        if (!SH) {
+            int cw = c % a.Wt;
+            if (cw < 0) cw += a.Wt;
+            SB = a.Ub + cw;
+        } else if (c >= 0 && c < a.Wt) {
+            SB = a.Ub + c;
+        } else {
+            int fc = c < 0 ? c + RH : c - a.Wt + RH;
+            fc = fc < 0 ? 0 : (fc > 2 * RH - 1 ? 2 * RH - 1 : fc);
+            SB = a.fUb + (long)fc * a.Nx;
+            bxs = 1;
+        }
+    }
     const int cx = c < 0 ? 0 : (c >= Wt ? Wt - 1 : c);
     auto wrap = [Nx](int x) { int w = x % Nx; return w < 0 ? w + Nx : w; };
     // REV marches the chunk from its last row to its first: virtual row v
@@ -282,7 +307,11 @@ __device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x
     auto ldu = [&](int xr, LU &ut, LU &ux) {
         const int X = phys(min(xr, xe + 2));
         const long ot = (long)wrap(X) * SU.xs, ox = (REV ? (long)wrap(X - 1) * SU.xs : ot) + SU.ps;
-        if constexpr (UC != 0) {
+        if constexpr (UC == 2) {
+            const uint8_t bt = SB[(long)wrap(X) * bxs];
+            ut = LinkCode{SU.p[ot], bt};
+            ux = LinkCode{SU.p[ox], REV ? SB[(long)wrap(X - 1) * bxs] : bt};
+        } else if constexpr (UC == 1) {
             ut = LinkCode{SU.p[ot], SF[ot]};
             ux = LinkCode{SU.p[ox], SF[ox]};
         } else {
@@ -290,18 +319,18 @@ __device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x
             ux = SU.p[ox];
         }
     };
-    auto cvu = [](LU v) -> double2 {
-        if constexpr (UC != 0) return u_of(v);
+    auto cvu = [](LU v, int shift) -> double2 {  // shift: the U_t (0) or U_x (4) nibble of UC 2
+        if constexpr (UC != 0) return u_of<UC>(v, shift);
         else return v;
     };
     // FOLD 2 takes pre-scaled links (ra_site): U_t by -sr0/2, U_x by -1/2
     const double kt = FOLD == 2 ? -0.5 * sr0 : 1.0, kx = FOLD == 2 ? -0.5 : 1.0;
     auto cvt = [&](LU v) -> double2 {
-        const double2 u = cvu(v);
+        const double2 u = cvu(v, 0);
         return FOLD == 2 ? make_double2(u.x * kt, u.y * kt) : u;
     };
     auto cvx = [&](LU v) -> double2 {
-        const double2 u = cvu(v);
+        const double2 u = cvu(v, 4);
         return FOLD == 2 ? make_double2(u.x * kx, u.y * kx) : u;
     };
     auto ld2 = [&](int xr, Sp &q, Sp &xv) {
@@ -624,7 +653,7 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
                   const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
                   int tb0, int tbn, const double2 *prev_partials, const double *Uang, const double *fUang,
                   double2 *fsend, int pbase, unsigned *tick, int ntiles, double2 *gsum, double2 *out3,
-                  int red_sums) {
+                  int red_sums, int link_fmt) {
     if (tbn <= 0) return;
     RAArgs a;
     a.d1 = d1; a.d2 = d2; a.dn = dn; a.x = x; a.U = U;
@@ -641,8 +670,11 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
     a.pass = pass;
     a.Ua = Uang;
     a.fUa = fUang;
-    a.Uf = Uang ? reinterpret_cast<const uint16_t *>(Uang + 2 * g.V) : nullptr;  // flag words after the codes
+    // flag words right after the codes, flag bytes right after the flag words
+    a.Uf = Uang ? reinterpret_cast<const uint16_t *>(Uang + 2 * g.V) : nullptr;
     a.fUf = fUang ? reinterpret_cast<const uint16_t *>(fUang + 16 * (long)g.Nx) : nullptr;
+    a.Ub = Uang ? reinterpret_cast<const uint8_t *>(a.Uf + 2 * g.V) : nullptr;
+    a.fUb = fUang ? reinterpret_cast<const uint8_t *>(a.fUf + 16 * (long)g.Nx) : nullptr;
     a.fsend = fsend;
     a.pbase = pbase;
     a.tick = tick;
@@ -659,16 +691,18 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
     a.xpar = (int)(pass & 1);
     // one kernel per (shards, x pass, fold, scalar mode, link form, tail) combination
     const int f = c.fold >= 2 ? 2 : (c.fold ? 1 : 0);
-    const int uc = Uang && f == 2;  // link codes: with the fused multiply-add fold only
+    const int uc = Uang && f == 2 ? (link_fmt == 2 ? 2 : 1) : 0;  // link codes: with the fused multiply-add fold only
     const int tk = tick != nullptr && f == 2;
     if (prev_partials && nshard == 1 && f == 2 && tb0 == 0 && tbn == c.TBk) {
-        if (uc) ra_go<0, 1, 1, 2>(xp, 0, grid, block, lds, s, a);
+        if (uc == 2) ra_go<0, 1, 2, 2>(xp, 0, grid, block, lds, s, a);
+        else if (uc) ra_go<0, 1, 1, 2>(xp, 0, grid, block, lds, s, a);
         else ra_go<0, 1, 0, 2>(xp, 0, grid, block, lds, s, a);
         return;
     }
     const bool sh = nshard > 1;
     if (red_sums && sh && f == 2 && tk) {  // t-shards: scalars from pass j-1's all-reduced sums (sc->sumr)
-        if (uc) ra_go<1, 2, 1, 2>(xp, tk, grid, block, lds, s, a);
+        if (uc == 2) ra_go<1, 2, 2, 2>(xp, tk, grid, block, lds, s, a);
+        else if (uc) ra_go<1, 2, 1, 2>(xp, tk, grid, block, lds, s, a);
         else ra_go<1, 2, 0, 2>(xp, tk, grid, block, lds, s, a);
         return;
     }
@@ -691,7 +725,10 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
         a.alt = 1;
     }
     if (f == 2) {
-        if (uc) {
+        if (uc == 2) {
+            if (sh) ra_go<1, 0, 2, 2>(xp, tk, grid, block, lds, s, a);
+            else ra_go<0, 0, 2, 2>(xp, tk, grid, block, lds, s, a, rev);
+        } else if (uc) {
             if (sh) ra_go<1, 0, 1, 2>(xp, tk, grid, block, lds, s, a);
             else ra_go<0, 0, 1, 2>(xp, tk, grid, block, lds, s, a, rev);
         } else {
@@ -715,7 +752,7 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
 __global__ void __launch_bounds__(256) link_code_kernel(long n, const double2 *U, double *Ua, double2 *part) {
     __shared__ double2 sh[4];
     uint16_t *Uf = reinterpret_cast<uint16_t *>(Ua + n);
-    double bad = 0.0;
+    double bad = 0.0, wide = 0.0;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
         const double2 u = U[i];
         double v, c2, s2;
@@ -725,8 +762,9 @@ __global__ void __launch_bounds__(256) link_code_kernel(long n, const double2 *U
         Ua[i] = v;
         Uf[i] = f;
         if (!ok || sm_lc_bits(c2) != sm_lc_bits(u.x) || sm_lc_bits(s2) != sm_lc_bits(u.y)) bad += 1.0;
+        if (sm_lc_nibble(f) == 0xff) wide += 1.0;  // needs the 16-bit flag word
     }
-    const double2 b = block_sum(make_double2(bad, 0.0), sh);
+    const double2 b = block_sum(make_double2(bad, wide), sh);
     if (threadIdx.x == 0) part[blockIdx.x] = b;
 }
 
@@ -768,6 +806,33 @@ int launch_link_code_check(hipStream_t s, long n, const double2 *U, double2 *out
     const int nb = reduce_blocks(n);
     hipLaunchKernelGGL(link_code_check_kernel, dim3(nb), dim3(256), 0, s, n, U, out, partials);
     return nb;
+}
+
+// Flag bytes of the packed form (sm_linkcode.h sm_lc_nibble): byte i of Ub =
+// the nibbles of flag words i (low) and i + ps (high), for i < m. Main field:
+// m = V, ps = V (U_t, U_x planes); faces [col][plane][x]: called per column.
+__global__ void __launch_bounds__(256) link_nibbles_kernel(long m, long ps, long rows, long rs, const uint16_t *Uf,
+                                                           uint8_t *Ub, long bs) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < m * rows; i += (long)gridDim.x * blockDim.x) {
+        const long r = i / m, k = i - r * m;
+        const uint16_t *f = Uf + r * rs;
+        Ub[r * bs + k] = (uint8_t)(sm_lc_nibble(f[k]) | (sm_lc_nibble(f[k + ps]) << 4));
+    }
+}
+
+void launch_link_nibbles(hipStream_t s, long V, const double *Ua) {
+    const uint16_t *Uf = reinterpret_cast<const uint16_t *>(Ua + 2 * V);
+    uint8_t *Ub = const_cast<uint8_t *>(reinterpret_cast<const uint8_t *>(Uf + 2 * V));
+    hipLaunchKernelGGL(link_nibbles_kernel, dim3(reduce_blocks(V)), dim3(256), 0, s, V, V, 1L, 0L, Uf, Ub, 0L);
+}
+
+void launch_face_nibbles(hipStream_t s, int Nx, const double *fUa) {
+    // 8 columns of [plane][x] flag words -> 8 columns of [x] bytes
+    const long n = 16L * Nx;
+    const uint16_t *Uf = reinterpret_cast<const uint16_t *>(fUa + n);
+    uint8_t *Ub = const_cast<uint8_t *>(reinterpret_cast<const uint8_t *>(Uf + n));
+    hipLaunchKernelGGL(link_nibbles_kernel, dim3((unsigned)((8L * Nx + 255) / 256)), dim3(256), 0, s, (long)Nx,
+                       (long)Nx, 8L, 2L * Nx, Uf, Ub, (long)Nx);
 }
 
 // Codes of the n ghost links of a t-shard face (codes, then flag words).

@@ -79,6 +79,7 @@ struct sm_ctx {
     // the complex links are used.
     int link_angles = 1;
     int uang_state = 0;
+    int link_fmt = 1;               // codes in use: 2 = flag nibbles, one byte per site; 1 = 16-bit flag words
     // Placement of the buffers the CG pass streams (stream_malloc): 5 = an
     // allocation of >= 2 GiB each with hipDeviceMallocContiguous (the
     // default; plain allocation of that size when the driver has no

@@ -141,7 +141,7 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
                   int tb0, int tbn, const double2 *prev_partials = nullptr, const double *Uang = nullptr,
                   const double *fUang = nullptr, double2 *fsend = nullptr, int pbase = 0,
                   unsigned *tick = nullptr, int ntiles = 0, double2 *gsum = nullptr, double2 *out3 = nullptr,
-                  int red_sums = 0);
+                  int red_sums = 0, int link_fmt = 1);
 // (tick != null: ticketed tail over the ntiles tiles of every launch of the
 // pass -- the last block forms the scalars in sc, or writes the shard's three
 // sums to out3; tick holds 1 + ceil(ntiles / 64) zeroed counters, gsum 3 per group)
@@ -156,6 +156,12 @@ constexpr int kMaxTickGroups = 1024;
 // block count.
 int launch_link_codes(hipStream_t s, long n, const double2 *U, double *Ua, double2 *partials);
 void launch_codes_of(hipStream_t s, long n, const double2 *U, double *Ua);  // faces: codes + flags only
+// Packed link flags (launch_cg_ra link_fmt 2): one byte per site holding the
+// U_t and U_x flag nibbles, written after the flag words of the V-site code
+// block / of the 4-deep face block (sm_linkcode.h sm_lc_nibble; only for
+// fields whose every flag word fits a nibble)
+void launch_link_nibbles(hipStream_t s, long V, const double *Ua);
+void launch_face_nibbles(hipStream_t s, int Nx, const double *fUa);
 // Diagnostic: encode + decode each of n links (the pass's functions) into
 // out (may be null); per block (count not rebuilt bitwise, largest
 // per-component error) to partials; returns the block count.

@@ -27,9 +27,12 @@
 // the pass's operator differed from D D^dag by a few ulps.
 //
 // Device layout (sm_capi.cpp ensure_link_angles): one allocation holds the
-// codes v of both planes (2V doubles: U_t plane, then U_x plane) followed by
-// the flags f (2V uint16, same order); the t-shard ghost faces likewise
-// (16 Nx doubles, then 16 Nx uint16).
+// codes v of both planes (2V doubles: U_t plane, then U_x plane), the flags f
+// (2V uint16, same order) and the packed form's flag bytes (V bytes, below);
+// the t-shard ghost faces likewise (16 Nx doubles, 16 Nx uint16, 8 Nx bytes).
+// The pass reads v and either the flag words (20 B/site of links) or, when
+// every offset of the field lies in [-2, 1] -- fresh exp(i theta) fields --
+// the flag bytes (17 B/site).
 // Plain C as well, so tests/test_linkcode_host.py runs the same code on the
 // host (with a perturbed reciprocal-square-root seed to model v_rsq_f64; the
 // host pair is exact for the host's own root, as the device pair is for the
@@ -106,6 +109,22 @@ SM_LINKCODE_FN void sm_link_decode(double v, uint16_t f, double *c_out, double *
     const int cosv = (int)((f >> 1) & 1u);
     *c_out = cosv ? v : w;
     *s_out = cosv ? w : v;
+}
+
+// Packed form for fields whose every offset k lies in [-2, 1] (fresh
+// exp(i theta) fields: |k| <= 1 measured): a link's flag word as a nibble
+// (bit 0 sign of w, bit 1 v is the cosine, bits 2..3 k as 2-bit two's
+// complement), the U_t nibble and the U_x nibble of a site in ONE byte --
+// 17 instead of 20 B/site of links. sm_lc_nibble returns 0xff for a flag word
+// that does not fit.
+SM_LINKCODE_FN uint8_t sm_lc_nibble(uint16_t f) {
+    const int k = (int16_t)f >> 2;
+    return (k < -2 || k > 1) ? (uint8_t)0xff : (uint8_t)((f & 3u) | (((unsigned)k & 3u) << 2));
+}
+
+SM_LINKCODE_FN uint16_t sm_lc_flags_of_nibble(unsigned nib) {
+    const int k = (int)((nib >> 2) & 3u) - (int)((nib >> 1) & 4u);  // sign-extend the 2-bit k
+    return (uint16_t)((nib & 3u) | ((uint32_t)(int32_t)k << 2));
 }
 
 // 1 iff link (c, s) is encodable and its code decodes to it bitwise.

@@ -424,7 +424,10 @@ def test_link_codes_device_decode_matches_stored_links(sm):
     far = U.copy()
     far.mu0[123] *= 1.0 + 1e-9
     try:
-        for field, nbad in ((U, 0), (drift, 0), (near, 0), (far, 1)):
+        # link bytes per site the pass reads: packed flag nibbles (fresh field,
+        # every ulp offset in [-2, 1]), 16-bit flag words (offsets beyond), or
+        # the complex links (a link not encodable)
+        for field, nbad, lbytes in ((U, 0, 17), (drift, 0, 20), (near, 0, 20), (far, 1, 32)):
             host = np.concatenate([field.mu0, field.mu1])
             dU = hip.upload(host)
             dout = hip.upload(np.zeros(2 * S, dtype=np.complex128))
@@ -445,8 +448,52 @@ def test_link_codes_device_decode_matches_stored_links(sm):
                 xs[on] = (flat(x), u.value)
             assert xs[1][1] == (1 if bad == 0 else 0), (bad, xs[1][1])
             assert bits_equal(xs[1][0], xs[0][0])
+            sm.check(sm.lib.sm_cg_link_codes(L.ctx, 1, None))
+            x = sm.spinor(S)
+            assert sm.conjugate_gradient(field, psi, x, -0.1) == 1
+            b = ctypes.c_int(-1)
+            sm.check(sm.lib.sm_cg_link_bytes(L.ctx, ctypes.byref(b)))
+            assert b.value == lbytes, (b.value, lbytes)
     finally:
         sm.check(sm.lib.sm_cg_link_codes(L.ctx, 1, None))
+
+
+@pytest.mark.parametrize("drift", [False, True], ids=["packed_flags", "flag_words"])
+def test_link_codes_tshard_path_bitwise(sm, drift):
+    """The t-shard form of the code pass (faces of codes and flags through
+    the RCCL loopback context, sm_create_loopback) in both flag formats: a
+    fresh field (flag nibbles, 17 B/site of links) and one with every link a
+    few ulp off the circle (16-bit flag words, 20 B/site). Codes on and off
+    give bitwise the same x, and the same x as the one-shard context."""
+    Nx, Nt = 64, 512
+    S = Nx * Nt
+    P = lambda a: a.ctypes.data  # noqa: E731
+    U, psi = sm.spinor(S), sm.spinor(S)
+    sm.lib.sm_fill_gauge(4321, 0.3246, Nt, 0, Nx, 0, Nt, P(U.mu0), P(U.mu1))
+    sm.lib.sm_fill_spinor(13, Nt, 0, Nx, 0, Nt, P(psi.mu0), P(psi.mu1))
+    if drift:
+        f = 1.0 + np.random.default_rng(3).integers(-6, 7, 2 * S) * 2.0 ** -53
+        U.mu0 *= f[:S]
+        U.mu1 *= f[S:]
+    out = {}
+    for loop in (True, False):
+        L = sm.init(Nx, Nt, loopback=loop)  # the context the reference-shaped calls use
+        try:
+            sm.check(sm.lib.sm_tune_cg(L.ctx, 5, 0))
+            for on in (1, 0):
+                sm.check(sm.lib.sm_cg_link_codes(L.ctx, on, None))
+                x = sm.spinor(S)
+                assert sm.conjugate_gradient(U, psi, x, -0.05) == 1
+                b = ctypes.c_int(-1)
+                sm.check(sm.lib.sm_cg_link_bytes(L.ctx, ctypes.byref(b)))
+                out[(loop, on)] = (flat(x), b.value)
+        finally:
+            L.close()
+    assert out[(True, 1)][1] == out[(False, 1)][1] == (20 if drift else 17), out
+    assert out[(True, 0)][1] == 32
+    assert bits_equal(out[(True, 1)][0], out[(True, 0)][0])
+    assert bits_equal(out[(False, 1)][0], out[(False, 0)][0])
+    assert np.linalg.norm(out[(True, 1)][0] - out[(False, 1)][0]) / np.linalg.norm(out[(False, 1)][0]) <= 1e-12
 
 
 def test_link_codes_after_hmc_trajectories(sm):

@@ -17,7 +17,9 @@ bitwise; the device's own round trip is checked on the device
     20000 steps of the leapfrog's link update U <- U exp(i y) (src/hmc.cpp:70,
     rounded every step, never re-unitarised): encodable and rebuilt bitwise;
   * links off the circle by 1e-9 (|k| far beyond 8191), NaN and Inf: not
-    encodable (the pass then reads the complex links).
+    encodable (the pass then reads the complex links);
+  * the packed form's flag nibble (k in [-2, 1]) round-trips every flag word
+    it accepts and refuses every other.
 """
 import os
 import subprocess
@@ -85,7 +87,16 @@ int main(void) {
     uint16_t f;
     far_ok += sm_link_encode(0.0 / 0.0, 0.5, &v, &f) + sm_link_encode(0.5, INFINITY, &v, &f);
     far_ok += sm_link_code_ok(0.0 / 0.0, 0.5) + sm_link_code_ok(2.0, 2.0);
-    printf("%ld %ld %ld %ld %ld %ld\n", unit_kmax, unit_rejected, drift_rejected, inexact, kmax, far_ok);
+    /* the packed flags: every nibble round-trips, offsets outside [-2, 1] do not pack */
+    long nib_bad = 0;
+    for (int k = -8191; k <= 8191; ++k)
+        for (unsigned lo = 0; lo < 4; ++lo) {
+            const uint16_t f = (uint16_t)(((uint32_t)(int32_t)k << 2) | lo);
+            const uint8_t nb = sm_lc_nibble(f);
+            if (k >= -2 && k <= 1) nib_bad += nb > 15 || sm_lc_flags_of_nibble(nb) != f;
+            else nib_bad += nb != 0xff;
+        }
+    printf("%ld %ld %ld %ld %ld %ld %ld\n", unit_kmax, unit_rejected, drift_rejected, inexact, kmax, far_ok, nib_bad);
     return 0;
 }
 """
@@ -102,10 +113,11 @@ def test_link_code_round_trip(tmp_path, perturb):
         cmd.insert(1, f"-DSM_LC_HOST_SEED_PERTURB={perturb}")
     subprocess.run(cmd, check=True)
     out = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
-    unit_kmax, unit_rejected, drift_rejected, inexact, kmax, far_ok = out
+    unit_kmax, unit_rejected, drift_rejected, inexact, kmax, far_ok, nib_bad = out
     print(f"unit links |k| <= {unit_kmax}; largest |k| over all encodable links {kmax}")
     assert unit_rejected == 0 and unit_kmax <= 3, out
     assert drift_rejected == 0, out          # 20000 leapfrog updates stay in the 14-bit range
     assert inexact == 0, out                 # every encodable link is rebuilt bitwise
     assert kmax <= 8191, out
     assert far_ok == 0, out                  # 1e-9 off the circle, NaN, Inf: never encodable
+    assert nib_bad == 0, out                 # flag nibbles: exact for k in [-2, 1], refused otherwise
