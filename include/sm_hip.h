@@ -157,11 +157,11 @@ int sm_tune_cg_geometry(sm_ctx *ctx, int waves_per_block, int xchunk);
 int sm_cg_link_codes(sm_ctx *ctx, int on, int *in_use);
 /* Round-2 name of sm_cg_link_codes; same behaviour, kept for old callers.
  * on: 1 / 0 enable / disable, < 0 keep; *in_use (may be NULL): 1 if the last
- * sm_cg_begin / sm_cg set the codes up for the active path. On t-shards the
- * choice is collective at the next solve: every solve all-reduces the count
- * of shards whose codes are stale (a new U, or a changed wish on any one
- * rank); if it is not 0 every shard rebuilds and the codes are used only if
- * every shard asks for them (one more all-reduce, which every shard joins). */
+ * sm_cg_begin / sm_cg set the codes up for the active path. The choice is
+ * each context's own, also on t-shards: the codes are exact, so shards that
+ * choose differently still compute bitwise the same iterates with the same
+ * collectives (each shard checks its own links and the ghost links it
+ * receives). */
 int sm_cg_link_angles(sm_ctx *ctx, int on, int *in_use);
 /* Bytes of link data per site the recompute-Ad CG pass read in the last
  * solve: 32 (complex links), 20 (codes with 16-bit flag words) or 17 (codes

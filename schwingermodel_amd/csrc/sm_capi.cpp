@@ -345,56 +345,41 @@ int exchange_ghost_U(sm_ctx *c) {
 }
 
 
-// Link codes for the recompute-Ad pass (cg_ra_kernel UC, sm_linkcode.h), rebuilt at the
-// first solve after U changed. On t-shards the decision is collective: the
-// path conditions below are rank-uniform (shape rules, the same test options
-// everywhere), but the link_angles wish is per context (sm_cg_link_angles),
-// and so is its staleness (a wish change on one rank marks only that rank's
-// codes stale). So every solve on t-shards first all-reduces the count of
-// stale shards; when it is not 0, EVERY shard rebuilds and joins ONE
-// all-reduce of (links not encodable bitwise, shards not asking for codes), and
-// the codes are used only when both sums are 0. Every rank thus issues the
-// same collectives in the same order, whichever rank changed its wish.
 // Bytes of the codes of n links (sm_linkcode.h): n doubles (v), n flag words,
 // then the packed form's flag bytes (one per site = per two links).
 static size_t link_code_bytes(long n) { return (sizeof(double) + sizeof(uint16_t)) * (size_t)n + (size_t)(n + 1) / 2; }
 
+// Link codes for the recompute-Ad pass (cg_ra_kernel UC, sm_linkcode.h), rebuilt at the
+// first solve after U changed (every change comes through exchange_ghost_U)
+// or after the wish changed (sm_cg_link_codes). The codes rebuild every link
+// BITWISE, so a pass reading them is the same arithmetic as one reading the
+// complex links, and the choice needs no agreement between shards: each shard
+// decides for itself from ITS links and the ghost links it received (the
+// 4-deep face its pass reads), and shards deciding differently still compute
+// the same iterates with the same collectives. The decision is a local host
+// read (the counts of links not encodable and of flag words too wide for the
+// packed form), no collective, and it runs only on a rebuild: a solve on an
+// unchanged U and wish costs nothing here (round 4 all-reduced a
+// stale count at every t-shard solve).
 int ensure_link_angles(sm_ctx *c) {
     if (c->cg_fused != 5 || c->racfg.fold < 2 || !cg_ra_ok(c)) return SM_OK;
-    if (c->sharded()) {
-        c->h_sums[1] = make_double2(c->uang_state == 0 ? 1.0 : 0.0, 0.0);  // (this shard is stale, 0)
-        HIP_TRY(hipMemcpyAsync(c->sums, c->h_sums + 1, sizeof(double2), hipMemcpyHostToDevice, c->stream));
-        TRY(allreduce_dev(c, (double *)c->sums, 2));
-        HIP_TRY(hipMemcpyAsync(c->h_sums, c->sums, sizeof(double2), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        if (c->h_sums[0].x == 0.0) return SM_OK;  // rank-uniform: no shard is stale
-    } else if (c->uang_state != 0 || !c->link_angles) {
-        return SM_OK;
-    }
-    // sums[0] = (links not rebuilt bitwise, links whose flag word needs 16
-    // bits), sums[1] = (shards declining the codes, 0), all-reduced together
-    if (c->link_angles) {
-        if (!c->Uang) HIP_TRY(stream_malloc(c, (void **)&c->Uang, link_code_bytes(2 * c->g.V)));
-        if (c->sharded() && !c->Uang_face) HIP_TRY(hipMalloc(&c->Uang_face, link_code_bytes(16 * (long)c->g.Nx)));
-        const int nb = launch_link_codes(c->stream, 2 * c->g.V, c->U, c->Uang, c->partials);
-        launch_sum_partials(c->stream, nb, c->partials, c->sums);
-        HIP_TRY(hipMemsetAsync(c->sums + 1, 0, sizeof(double2), c->stream));
-    } else {
-        c->h_sums[1] = make_double2(0.0, 0.0);
-        c->h_sums[2] = make_double2(1.0, 0.0);  // this shard declines
-        HIP_TRY(hipMemcpyAsync(c->sums, c->h_sums + 1, 2 * sizeof(double2), hipMemcpyHostToDevice, c->stream));
-    }
-    TRY(allreduce_dev(c, (double *)c->sums, 4));
-    HIP_TRY(hipMemcpyAsync(c->h_sums, c->sums, 2 * sizeof(double2), hipMemcpyDeviceToHost, c->stream));
+    if (c->uang_state != 0 || !c->link_angles) return SM_OK;
+    if (!c->Uang) HIP_TRY(stream_malloc(c, (void **)&c->Uang, link_code_bytes(2 * c->g.V)));
+    if (c->sharded() && !c->Uang_face) HIP_TRY(hipMalloc(&c->Uang_face, link_code_bytes(16 * (long)c->g.Nx)));
+    // per block (links not rebuilt bitwise, links whose flag word needs 16 bits)
+    int nb = launch_link_codes(c->stream, 2 * c->g.V, c->U, c->Uang, c->partials);
+    if (c->sharded())
+        nb += launch_link_codes(c->stream, 16 * (long)c->g.Nx, face4_recv_U(c), c->Uang_face, c->partials + nb);
+    launch_sum_partials(c->stream, nb, c->partials, c->sums);
+    HIP_TRY(hipMemcpyAsync(c->h_sums, c->sums, sizeof(double2), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    c->uang_state = c->h_sums[0].x == 0.0 && c->h_sums[1].x == 0.0 ? 1 : 2;
-    // the packed flags (one byte per site) when every flag word fits a nibble
-    // on every shard, else the 16-bit flag words
+    c->uang_state = c->h_sums[0].x == 0.0 ? 1 : 2;
+    // the packed flags (one byte per site) when every flag word fits a nibble,
+    // else the 16-bit flag words
     c->link_fmt = c->h_sums[0].y == 0.0 ? 2 : 1;
-    if (c->uang_state == 1 && c->link_fmt == 2) launch_link_nibbles(c->stream, c->g.V, c->Uang);
-    if (c->uang_state == 1 && c->sharded()) {
-        launch_codes_of(c->stream, 16 * (long)c->g.Nx, face4_recv_U(c), c->Uang_face);
-        if (c->link_fmt == 2) launch_face_nibbles(c->stream, c->g.Nx, c->Uang_face);
+    if (c->uang_state == 1 && c->link_fmt == 2) {
+        launch_link_nibbles(c->stream, c->g.V, c->Uang);
+        if (c->sharded()) launch_face_nibbles(c->stream, c->g.Nx, c->Uang_face);
     }
     HIP_TRY(hipGetLastError());
     return SM_OK;
@@ -515,6 +500,12 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //   edge_xchunk=N       t-shards: rows per edge block (0: the interior's)
 //   ra_red_max_blocks=N one shard: redundant scalars up to N blocks
 //   fold=0|1|2          recompute-Ad pass arithmetic (2: fused multiply-adds)
+//   apply_split=0|1     t-shard Dirac apply: interior / edge launches around
+//                       the faces on the comm stream (1; default from Wt 2048)
+//                       or faces first, then one launch (0)
+//   ra_remap=0|1        recompute-Ad pass tile order (1: each XCD takes a
+//                       contiguous range of x-adjacent chunks, the default;
+//                       0: round-robin dispatch order)
 //   rev=0|1|2           recompute-Ad pass march schedule (0 all forward; 1 odd
 //                       passes backward; 2, the default, x-adjacent chunks in
 //                       opposite directions and odd passes flipped)
@@ -564,6 +555,11 @@ static int apply_test_opts(sm_ctx *c) {
             c->racfg.fold = iv;
         } else if (k == "rev") {
             c->racfg.rev_odd = iv;
+        } else if (k == "apply_split") {
+            c->apply_split = iv ? 1 : 0;
+        } else if (k == "ra_remap") {
+            if (iv < 0 || iv > 1) return fail(SM_ERR_ARG, "SM_TEST_OPTS: ra_remap must be 0 or 1");
+            c->racfg.remap = iv;
 
         } else if (k == "probe_min_mib") {
             if (iv < 1) return fail(SM_ERR_ARG, "SM_TEST_OPTS: probe_min_mib must be >= 1");
@@ -1011,7 +1007,7 @@ int sm_cg_link_codes(sm_ctx *c, int on, int *in_use) {
     if (!c) return fail(SM_ERR_ARG, "null context");
     if (on >= 0 && (on ? 1 : 0) != c->link_angles) {
         c->link_angles = on ? 1 : 0;
-        c->uang_state = 0;  // decided again (collectively on t-shards) at the next solve
+        c->uang_state = 0;  // decided again (by this shard) at the next solve
     }
     if (in_use) *in_use = c->link_angles && c->cg_fused == 5 && c->uang_state == 1 ? 1 : 0;
     return SM_OK;

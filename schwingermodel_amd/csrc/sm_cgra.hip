@@ -835,22 +835,6 @@ void launch_face_nibbles(hipStream_t s, int Nx, const double *fUa) {
                        (long)Nx, 8L, 2L * Nx, Uf, Ub, (long)Nx);
 }
 
-// Codes of the n ghost links of a t-shard face (codes, then flag words).
-__global__ void __launch_bounds__(256) codes_of_kernel(long n, const double2 *U, double *Ua) {
-    uint16_t *Uf = reinterpret_cast<uint16_t *>(Ua + n);
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-        double v;
-        uint16_t f;
-        sm_link_encode(U[i].x, U[i].y, &v, &f);
-        Ua[i] = v;
-        Uf[i] = f;
-    }
-}
-
-void launch_codes_of(hipStream_t s, long n, const double2 *U, double *Ua) {
-    hipLaunchKernelGGL(codes_of_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, U, Ua);
-}
-
 // After the last pass J = k of the recompute-Ad CG, the rows of parity
 // != (k & 1) still lack alpha_{k-1} d_{k-1} (their last update was pass k-1).
 // A stopping evaluation keeps alpha = alpha_{k-1}; a non-final one has moved it

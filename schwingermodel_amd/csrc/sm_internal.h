@@ -155,7 +155,6 @@ constexpr int kMaxTickGroups = 1024;
 // links the pass's decoder does NOT rebuild bitwise to partials; returns the
 // block count.
 int launch_link_codes(hipStream_t s, long n, const double2 *U, double *Ua, double2 *partials);
-void launch_codes_of(hipStream_t s, long n, const double2 *U, double *Ua);  // faces: codes + flags only
 // Packed link flags (launch_cg_ra link_fmt 2): one byte per site holding the
 // U_t and U_x flag nibbles, written after the flag words of the V-site code
 // block / of the 4-deep face block (sm_linkcode.h sm_lc_nibble; only for

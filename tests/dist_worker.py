@@ -328,15 +328,23 @@ def run_eocg(name, result_path, dist, rank, world):
     dist.destroy_process_group()
 
 
+def bits_sha(*arrays):
+    import hashlib
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).view(np.uint8))
+    return h.hexdigest()
+
+
 def run_angles(name, result_path, dist, rank, world):
-    """mode "angles": the link-angle choice of the recompute-Ad CG is
-    collective on t-shards. name = gen:<Nx>x<Nt>:<sigma>:<m0>:<wish>
-    where wish is one 0/1 digit per rank for sm_cg_link_angles. Each rank
-    solves twice (the second solve re-decides after U is re-uploaded) and
-    reports (converged, iterations, in_use) per solve; nothing may hang.
-    With a sixth field (gen:...:<wish>:<wish2>) the ranks set
-    wish2 between the solves and do NOT re-upload U, so only the ranks whose
-    wish changed have stale codes at the second solve."""
+    """mode "angles": each shard's own link-code choice in the recompute-Ad
+    CG. name = gen:<Nx>x<Nt>:<sigma>:<m0>:<wish> where wish is one 0/1 digit
+    per rank for sm_cg_link_angles. Each rank solves twice (the second solve
+    re-decides after U is re-uploaded), then once more with the codes off, and
+    reports (converged, iterations, in_use, SHA-256 of x) per solve; nothing
+    may hang. With a sixth field (gen:...:<wish>:<wish2>) the ranks set wish2
+    between the solves and do NOT re-upload U, so only the ranks whose wish
+    changed rebuild at the second solve."""
     import schwingermodel_amd as sm
     from schwingermodel_amd import dist as smd
     parts = name.split(":")
@@ -366,7 +374,14 @@ def run_angles(name, result_path, dist, rank, world):
         sm.check(sm.lib.sm_cg(ctx, P_(p[0]), P_(p[1]), P_(x0), P_(x1), m0, 1e-10, 10000, ctypes.byref(res)))
         used = ctypes.c_int(-1)
         sm.check(sm.lib.sm_cg_link_angles(ctx, -1, ctypes.byref(used)))
-        out.append([int(res.converged), int(res.iterations), int(used.value)])
+        out.append([int(res.converged), int(res.iterations), int(used.value), bits_sha(x0, x1)])
+    # the same solve with every shard on the complex links: the reference
+    # point of the bitwise comparison (the codes are exact)
+    sm.check(sm.lib.sm_cg_link_angles(ctx, 0, None))
+    x0, x1 = np.empty(Nx * Wt.value, complex), np.empty(Nx * Wt.value, complex)
+    res = sm.CGResult()
+    sm.check(sm.lib.sm_cg(ctx, P_(p[0]), P_(p[1]), P_(x0), P_(x1), m0, 1e-10, 10000, ctypes.byref(res)))
+    out.append([int(res.converged), int(res.iterations), 0, bits_sha(x0, x1)])
     sm.lib.sm_destroy(ctx)
     gathered = [None] * world
     dist.all_gather_object(gathered, out)
