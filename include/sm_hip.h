@@ -362,6 +362,9 @@ typedef struct {
     long trajectories;      /* all updates run                            */
     long cg_iterations;
     int cg_failures;
+    int cg_link_bytes;      /* link bytes per site the CG pass read in the last
+                               solve (sm_cg_link_bytes: 32 complex links, 20
+                               codes + flag words, 17 codes + packed flags) */
 } sm_hmc_summary;
 int sm_hmc_run(sm_ctx *ctx, const sm_hmc_params *p, int hot_start, uint64_t first_traj, int Ntherm, int Nmeas,
                int Nsteps, const char *save_prefix, sm_hmc_summary *out, double *sp_series, double *gs_series);

@@ -35,7 +35,8 @@ class HamiltonianTerms(ctypes.Structure):
 class HMCSummary(ctypes.Structure):
     _fields_ = [("Ep", ctypes.c_double), ("dEp", ctypes.c_double), ("gS", ctypes.c_double),
                 ("dgS", ctypes.c_double), ("acceptance", ctypes.c_double), ("accepted", ctypes.c_long),
-                ("trajectories", ctypes.c_long), ("cg_iterations", ctypes.c_long), ("cg_failures", ctypes.c_int)]
+                ("trajectories", ctypes.c_long), ("cg_iterations", ctypes.c_long), ("cg_failures", ctypes.c_int),
+                ("cg_link_bytes", ctypes.c_int)]
 
 
 class HMCResult(ctypes.Structure):

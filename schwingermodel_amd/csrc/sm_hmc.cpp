@@ -146,6 +146,7 @@ int sm_hmc_run(sm_ctx *c, const sm_hmc_params *p, int hot_start, uint64_t first_
     out->trajectories = ntraj;
     out->cg_iterations = cg_it;
     out->cg_failures = cg_fail;
+    TRY(sm_cg_link_bytes(c, &out->cg_link_bytes));  // the link form the solves ended on, reported
     if (sp_series)
         for (int i = 0; i < Nmeas; i++) sp_series[i] = sp[i];
     if (gs_series)

@@ -207,7 +207,8 @@ int main(int argc, char **argv) {
         std::cout << "Acceptance rate: " << acc_stdout << std::endl;
         std::cout << "Execution time = " << end - begin << " s" << std::endl;
         std::cout << "CG iterations = " << s.cg_iterations << ", CG failures = " << s.cg_failures
-                  << ", trajectories = " << s.trajectories << std::endl;
+                  << ", trajectories = " << s.trajectories << ", CG link bytes/site = " << s.cg_link_bytes
+                  << std::endl;
         std::cout << "-------------------------------" << std::endl;
         Datfile.open(NameData.str(), std::ios::app);
         Datfile << "#Ep                           #dEp\n";

@@ -661,36 +661,36 @@ void launch_pack_faces(hipStream_t s, const Geometry &g, const double2 *field, d
 // reference's own (src/dirac_operator.cpp:31-43, 255-267; force :493-506).
 // Face packs: one thread per row x, strided loads (a row apart), so they are
 // latency-bound; 64-thread blocks spread the Nx threads over 4x as many CUs.
-__global__ void pack_faces_proj_kernel(int Nx, int Wt, long V, const double2 *f, const double2 *U, int kind,
-                                       double2 *lo, double2 *hi) {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= Nx) return;
-    const long a = (long)x * Wt, b = (long)x * Wt + Wt - 1;
-    const double2 a0 = f[a], a1 = f[a + V], b0 = f[b], b1 = f[b + V];
+// One thread per (x, side): side 0 forms the lo face from column 0, side 1 the
+// hi face from column Wt-1 (with its link). The loads are one site per row,
+// Wt sites apart, so the kernel is latency-bound: 2 Nx threads in 256-wide
+// blocks put every load in flight at once (round 4's one thread per x, in
+// 64-wide blocks: 6 us at Nx = 4096 on the RCCL loopback timeline).
+__global__ void __launch_bounds__(256) pack_faces_proj_kernel(int Nx, int Wt, long V, const double2 *f,
+                                                              const double2 *U, int kind, double2 *lo,
+                                                              double2 *hi) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 2 * Nx) return;
+    const int x = i >> 1, side = i & 1;
+    const long n = (long)x * Wt + (side ? Wt - 1 : 0);
+    const double2 p0 = f[n], p1 = f[n + V];
+    if (!side) {
+        // lo: D sends p0 - p1 down; D^dag and the force's left field p0 + p1,
+        // its right field p0 - p1
+        lo[x] = (kind == FACE_DDAG || kind == FACE_FORCE_L) ? cadd(p0, p1) : csub(p0, p1);
+        return;
+    }
     switch (kind) {
-        case FACE_D:
-            lo[x] = csub(a0, a1);
-            hi[x] = cmul(cconj(U[b]), cadd(b0, b1));
-            break;
-        case FACE_DDAG:
-            lo[x] = cadd(a0, a1);
-            hi[x] = cmul(cconj(U[b]), csub(b0, b1));
-            break;
-        case FACE_FORCE_L:  // the force reads only its t+1 neighbours (hi faces)
-            lo[x] = cadd(a0, a1);
-            hi[x] = make_double2(0.0, 0.0);
-            break;
-        default:            // FACE_FORCE_R
-            lo[x] = csub(a0, a1);
-            hi[x] = make_double2(0.0, 0.0);
-            break;
+        case FACE_D: hi[x] = cmul(cconj(U[n]), cadd(p0, p1)); break;
+        case FACE_DDAG: hi[x] = cmul(cconj(U[n]), csub(p0, p1)); break;
+        default: hi[x] = make_double2(0.0, 0.0); break;  // the force reads only t+1 neighbours: the lo face sent down
     }
 }
 
 void launch_pack_faces_proj(hipStream_t s, const Geometry &g, const double2 *field, const double2 *U, int kind,
                             double2 *lo_face, double2 *hi_face) {
-    hipLaunchKernelGGL(pack_faces_proj_kernel, dim3((g.Nx + 63) / 64), dim3(64), 0, s, g.Nx, g.Wt, g.V, field, U,
-                       kind, lo_face, hi_face);
+    hipLaunchKernelGGL(pack_faces_proj_kernel, dim3((2 * g.Nx + 255) / 256), dim3(256), 0, s, g.Nx, g.Wt, g.V, field,
+                       U, kind, lo_face, hi_face);
 }
 
 }  // namespace sm

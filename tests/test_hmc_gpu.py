@@ -76,6 +76,7 @@ def test_hmc_run_matches_reference_statistics(sm, ref):
                                ptr(sp), ptr(gs)))
     L.close()
     assert s.cg_failures == 0
+    assert s.cg_link_bytes == 32  # 64^2: the stored-Ad CG pass, complex links (codes from 4M sites per shard)
     assert s.trajectories == ref["Ntherm"] + n + ref["Nsteps"] * (n - 1)
     # summary = the reference's statistics over the measured series
     assert s.Ep == seq_mean(sp) / V
@@ -107,6 +108,7 @@ def test_sm_hmc_program(tmp_path, sm):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     ep = float(re.search(r"Ep = (\S+) dEp", r.stdout).group(1))
     assert "Acceptance rate:" in r.stdout and "Execution time" in r.stdout
+    assert re.search(r"CG link bytes/site = (32|20|17)\b", r.stdout), r.stdout[-500:]  # the link form is reported
     sim = tmp_path / f"2D_U1_{N}x{N}_m00.10000000000000001_SimData.txt"
     assert sim.exists(), os.listdir(tmp_path)
     assert "#Ep" in sim.read_text()

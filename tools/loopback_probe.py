@@ -19,6 +19,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
@@ -51,6 +52,7 @@ def main():
         x = torch.empty_like(phi)
         ctxs = {"one": sm.Lattice(Nx, Nt), "loopback": sm.Lattice(Nx, Nt, loopback=True)}
         times = {k: [] for k in ctxs}
+        host = {k: [] for k in ctxs}  # host seconds to ENQUEUE the timed iterations (host-bound if ~ the GPU time)
         for L in ctxs.values():
             sm.check(sm.lib.sm_set_stream(L.ctx, ctypes.c_void_p(s.cuda_stream)))
             sm.check(sm.lib.sm_upload_gauge_dev(L.ctx, vp(dU)))
@@ -62,7 +64,9 @@ def main():
                 sm.check(sm.lib.sm_cg_begin(L.ctx, vp(phi), vp(x), a.m0, 0.0))
                 sm.check(sm.lib.sm_cg_iterate(L.ctx, a.warmup))
                 e0.record(s)
+                th = time.perf_counter()
                 sm.check(sm.lib.sm_cg_iterate(L.ctx, a.iters))
+                host[k].append((time.perf_counter() - th) * 1e3 / a.iters)
                 e1.record(s)
                 e1.synchronize()
                 times[k].append(e0.elapsed_time(e1) / a.iters)
@@ -86,6 +90,7 @@ def main():
         for k, L in ctxs.items():
             print(json.dumps({"shape": shape, "context": k, "ms_per_iter": round(statistics.median(times[k]), 4),
                               "min": round(min(times[k]), 4), "iters": a.iters,
+                              "host_enqueue_ms_per_iter": round(statistics.median(host[k]), 4),
                               "apply_us": round(statistics.median(ap[k]), 2)}), flush=True)
             L.close()
         del dU, phi, x
