@@ -503,10 +503,9 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //   apply_split=0|1     t-shard Dirac apply: interior / edge launches around
 //                       the faces on the comm stream (1; default from Wt 2048)
 //                       or faces first, then one launch (0)
-//   ra_remap=0|1|2      recompute-Ad pass tile order (1: each XCD takes a
+//   ra_remap=0|1        recompute-Ad pass tile order (1: each XCD takes a
 //                       contiguous range of x-adjacent chunks, t-adjacent
-//                       tiles consecutive; 2: the same range t-block-major;
-//                       0: round-robin dispatch order)
+//                       tiles consecutive; 0: round-robin dispatch order)
 //   rev=0|1|2           recompute-Ad pass march schedule (0 all forward; 1 odd
 //                       passes backward; 2, the default, x-adjacent chunks in
 //                       opposite directions and odd passes flipped)
@@ -559,7 +558,7 @@ static int apply_test_opts(sm_ctx *c) {
         } else if (k == "apply_split") {
             c->apply_split = iv ? 1 : 0;
         } else if (k == "ra_remap") {
-            if (iv < 0 || iv > 2) return fail(SM_ERR_ARG, "SM_TEST_OPTS: ra_remap must be 0, 1 or 2");
+            if (iv < 0 || iv > 1) return fail(SM_ERR_ARG, "SM_TEST_OPTS: ra_remap must be 0 or 1");
             c->racfg.remap = iv;
 
         } else if (k == "probe_min_mib") {

@@ -512,15 +512,11 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
         if (a.remap) {  // each XCD takes a contiguous range of tiles: its own x-chunks (L2 reuse of halo rows)
             const int q = n >> 3, rr = n & 7, xcd = w & 7;
             const int len = xcd < rr ? q + 1 : q;
-            int i = a.flip ? len - 1 - (w >> 3) : (w >> 3);  // flip: the XCD's tiles in reverse order
-            // remap 2, where every XCD owns whole x-chunks: its tiles in
-            // t-block-major order, so the tiles resident together span all of
-            // its chunks (every x-adjacent pair starts together) instead of
-            // ~3 whole chunks per round (remap 1: t-adjacent tiles consecutive)
-            if (a.remap == 2 && rr == 0 && q % a.tbn == 0) {
-                const int nch = q / a.tbn;
-                i = (i % nch) * a.tbn + i / nch;
-            }
+            // t-adjacent tiles consecutive. (Round 5: taking the range
+            // t-block-major instead, so every x-adjacent pair of the XCD's
+            // chunks starts together, changed the read bytes by 0.1 % and was
+            // slower, profiles/r05_i_remap2.jsonl.)
+            const int i = a.flip ? len - 1 - (w >> 3) : (w >> 3);  // flip: the XCD's tiles in reverse order
             w = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + i;
         } else if (a.flip) {
             w = n - 1 - w;
