@@ -391,7 +391,7 @@ def placement_report(sh):
     the initial placement of its streamed buffers and after the search of each
     buffer (x, d1, d0, d2), and which buffers were re-placed."""
     sm = sh.sm
-    us = (ctypes.c_double * 8)()
+    us = (ctypes.c_double * 16)()
     n, chosen = ctypes.c_int(0), ctypes.c_int(0)
     sm.check(sm.lib.sm_placement_report(sh.L.ctx, us, ctypes.byref(n), ctypes.byref(chosen)))
     names = ("x", "d1", "d0", "d2")

@@ -193,11 +193,12 @@ const char *sm_build_id(void);
  * at a time (x, then the three direction buffers), trying up to
  * `candidates` fresh allocations of that buffer and keeping the fastest
  * (schwingermodel_amd/csrc/sm_capi.cpp placement_probe; not on host-staged
- * contexts, where shard processes share one GPU). *n = timings (0: no probe,
- * else 5), us_per_pass[0] (may be NULL; room for 8) = median microseconds
- * per pass of the initial placement, us_per_pass[i] = after the search of
- * buffer i; *chosen = bit mask of the buffers that moved (bit 0 x, 1..3 the
- * direction buffers). */
+ * contexts, where shard processes share one GPU); a sweep over the four
+ * buffers that improved the pass by > 1 % is followed by another (at most 3).
+ * *n = timings (0: no probe, else 1 + 4 per sweep), us_per_pass[0] (may be
+ * NULL; room for 16) = median microseconds per pass of the initial placement,
+ * us_per_pass[i] = after the search of the i-th buffer searched; *chosen = bit
+ * mask of the buffers that moved (bit 0 x, 1..3 the direction buffers). */
 int sm_placement_report(const sm_ctx *ctx, double *us_per_pass, int *n, int *chosen);
 /* Candidates per buffer of the placement probe for contexts created after
  * this call (process-wide; default 3, 0 disables the probe, at most 8).

@@ -604,8 +604,10 @@ static int apply_test_opts(sm_ctx *c) {
 // up to place_probe fresh allocations of that buffer (held while it is
 // searched, so the allocator cannot hand the same memory back), takes the
 // fastest candidate if it beats the current set by more than 1 %, and frees
-// the rest before the next buffer. 24 contexts on one box reached 430-439 us
-// from starts of 437-505 this way (r05_b_descent.jsonl). Transient memory:
+// the rest before the next buffer; a sweep that improved the pass by > 1 % is
+// followed by another (at most 3). One sweep reached 430-439 us in 24 of 24
+// trials on one box (r05_b_descent.jsonl) but stayed at 456-460 in 2 of 12 on
+// another, where each of those had still moved (r05_l_probe_sweeps.jsonl). Transient memory:
 // place_probe allocations of one buffer (3 x 2 GiB at 4096^2), and only while
 // 16 GiB stay free besides them; a candidate that cannot be allocated ends
 // that buffer's search (not the context). Only where the rule applies (fields
@@ -680,8 +682,17 @@ static int placement_probe(sm_ctx *c, size_t fb) {
     int rc = time_set(cur, &now);
     c->place_us[c->place_n++] = now;
     const size_t bytes = stream_alloc_bytes(fb);
-    for (int step = 0; step < 4 && rc == SM_OK; ++step) {
-        const int b = (int[]){3, 1, 0, 2}[step];  // x, d1, d0, d2
+    // sweeps over the four buffers, another one while the last improved the
+    // pass by > 1 % (at most kSweeps): a sweep that ends still slow has usually
+    // moved, and the next one starts from there (profiles/r05_l_probe_sweeps.jsonl)
+    constexpr int kSweeps = 3;
+    double sweep_start = now;
+    for (int step = 0; step < 4 * kSweeps && rc == SM_OK; ++step) {
+        if (step > 0 && step % 4 == 0) {
+            if (!(now < 0.99 * sweep_start)) break;
+            sweep_start = now;
+        }
+        const int b = (int[]){3, 1, 0, 2}[step % 4];  // x, d1, d0, d2
         std::vector<void *> cand;
         int keep = -1;
         double best = now;
@@ -709,7 +720,7 @@ static int placement_probe(sm_ctx *c, size_t fb) {
             cur[b] = cand[keep];
             c->fields[kSlot[b]] = (double2 *)cur[b];
             now = best;
-            c->place_chosen |= 1 << step;
+            c->place_chosen |= 1 << (step % 4);
         }
         for (void *p : cand)
             if (p != cur[b]) stream_free(c, p);

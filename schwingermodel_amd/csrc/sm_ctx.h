@@ -93,7 +93,7 @@ struct sm_ctx {
     int place_probe = 3;
     long place_min_mib = 256;       // smallest field (MiB) that is probed; test option probe_min_mib=N
     int place_n = 0, place_chosen = 0;
-    double place_us[8] = {};
+    double place_us[16] = {};       // the initial set, then one per buffer searched (up to 3 sweeps of 4)
     double *Uang = nullptr;         // 2V link codes (plane mu0 then mu1)
     double *Uang_face = nullptr;    // t-shards: codes of the 4-deep ghost links (16 Nx)
     hipStream_t own_stream = nullptr, stream = nullptr;

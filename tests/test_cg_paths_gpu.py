@@ -146,15 +146,15 @@ def test_placement_probe_report():
     """Context creation searches the placement of the CG pass's streamed
     buffers one buffer at a time (sm_capi.cpp placement_probe): at a shape
     that takes the rule (4096 x 2048, 256 MiB fields) the report gives the
-    pass time of the initial placement and after each of the four buffers'
-    searches (never slower than before it: a candidate is kept only if
+    pass time of the initial placement and after each buffer's search, in
+    sweeps of four (never slower than before it: a candidate is kept only if
     faster), and a solve on the probed placement equals the no-probe solve
     bitwise. Below the rule's size, or with the probe off through the public
     switch, nothing is probed."""
     import schwingermodel_amd as sm
 
     def report(L):
-        us = (ctypes.c_double * 8)()
+        us = (ctypes.c_double * 16)()
         n, k = ctypes.c_int(-1), ctypes.c_int(-2)
         sm.check(sm.lib.sm_placement_report(L.ctx, us, ctypes.byref(n), ctypes.byref(k)))
         return n.value, k.value, list(us)[:max(0, n.value)]
@@ -164,7 +164,7 @@ def test_placement_probe_report():
         n, k, us = report(L)
     finally:
         L.close()
-    assert n == 5 and 0 <= k < 16, (n, k)
+    assert n in (5, 9, 13) and 0 <= k < 16, (n, k)  # the initial set + 4 per sweep
     assert all(u > 0 for u in us) and all(b <= a for a, b in zip(us, us[1:])), us
     L = sm.Lattice(512, 512)
     try:
