@@ -497,7 +497,7 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //   tail=0              scalar kernel instead of the ticketed tail
 //   red_shards=0        t-shards: scalar kernel after the all-reduce
 //   face_pipe=0         t-shards: no pipelined d_j faces
-//   edge_xchunk=N       t-shards: rows per edge block (0: the interior's)
+//   edge_xchunk=N       t-shards: rows per edge block (0: the interior's; -1: rule)
 //   ra_red_max_blocks=N one shard: redundant scalars up to N blocks
 //   fold=0|1|2          recompute-Ad pass arithmetic (2: fused multiply-adds)
 //   apply_split=0|1     t-shard Dirac apply: interior / edge launches around
@@ -769,6 +769,8 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     HIP_TRY(hipSetDevice(device));
     sm_ctx *c = new sm_ctx();
     c->device = device;
+    if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->n_cu <= 0)
+        c->n_cu = 256;
     c->loop = loop;
     c->nshard = nshard;
     c->shard = shard;
@@ -1307,10 +1309,24 @@ static int cg_ra_pass(sm_ctx *c) {
     // them on the comm stream, under the interior launch and the scalar step;
     // the edge launch marches short chunks so it ends long before the interior
     // one (its blocks otherwise run as long as the whole pass, AFTER the faces).
+    // Edge rows per block: 16, or 32 where only the longer chunks let the
+    // edge tiles join the interior ones in one residency round (the pass holds
+    // 2 waves per SIMD, -Rpass-analysis=kernel-resource-usage: 8 one-wave
+    // blocks per CU). RCCL loopback, ms per
+    // iteration, 16 / 32 / 24 rows (profiles/r05_q_edge_chunk_long.jsonl):
+    // 4096x1024 (1751 interior tiles + 512 / 256 / 342 edge ones against 2048
+    // slots) 0.159 / 0.150 / 0.173; 4096x512 (all fit) 0.085 / 0.093 / 0.088;
+    // 4096x2048 (the interior alone overflows) 0.257 / 0.261-0.271 / 0.260.
     CGFusedCfg ec = fc;
     const bool pipe = split && c->cg_face_pipe && ra_edge_owns_faces(c, fc, tb_lo, tb_hi);
-    if (pipe && c->cg_edge_xchunk > 0 && c->cg_edge_xchunk < fc.xchunk) {
-        ec.xchunk = c->cg_edge_xchunk;
+    int exc = c->cg_edge_xchunk;
+    if (exc < 0) {
+        const long slots = (long)c->n_cu * 8 / fc.wpb, inner = (long)nint * fc.XB;
+        auto tiles = [&](int r) { return inner + (long)nedge * ((c->g.Nx + r - 1) / r); };
+        exc = tiles(16) > slots && tiles(32) <= slots ? 32 : 16;
+    }
+    if (pipe && exc > 0 && exc < fc.xchunk) {
+        ec.xchunk = exc;
         ec.XB = (c->g.Nx + ec.xchunk - 1) / ec.xchunk;
         if (3L * (nint * fc.XB + nedge * ec.XB) > 2L * kMaxPartials) ec = fc;
     }

@@ -107,7 +107,8 @@ struct sm_ctx {
     // whose d_{j-1} faces are already in flight); edge launch rows per block
     int cg_face_pipe = 1;
     int apply_split = 1;            // t-shard Dirac apply: interior / edge launches around the faces (0: faces first)
-    int cg_edge_xchunk = 16;
+    int cg_edge_xchunk = -1;        // -1: by the residency rule (launch_cg_ra_pass)
+    int n_cu = 256;                 // compute units of the device (residency of a launch)
     long cg_faces_for = -1;
     // recompute-Ad pass: ticketed tail (the pass's last block sums the partials
     // by groups of 64 and forms the scalars / the shard's sums), no scalar kernel
