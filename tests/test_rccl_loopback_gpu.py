@@ -175,3 +175,41 @@ def test_loopback_cg_after_nan_solve(sm):
         L.close()
     assert its["loop"][0] == its["one"][0] == 1 and its["loop"][1] == its["one"][1], (its["loop"][:2], its["one"][:2])
     assert np.linalg.norm(its["loop"][2] - its["one"][2]) / np.linalg.norm(its["one"][2]) <= 1e-13
+
+
+@pytest.mark.parametrize("split", [0, 1])
+@pytest.mark.parametrize("shape,sigma", [((32, 48), 0.41), ((96, 1024), 0.3246), ((64, 4096), 0.2374),
+                                         ((8, 2), 0.5), ((24, 3), 0.5)],
+                         ids=["32x48", "96x1024", "64x4096", "8x2", "24x3"])
+def test_loopback_apply_modes_bitwise(sm, shape, sigma, split):
+    """Both t-shard Dirac apply schedules (faces first; interior / edge
+    t-blocks around the faces -- sm_capi.cpp apply) give D, D^dag, D D^dag
+    bitwise equal to the one-shard context, on shapes down to two and three
+    t-columns."""
+    from conftest import opts_env
+    Nx, Nt = shape
+    S = Nx * Nt
+    U, psi, chi, _ = fields(sm, Nx, Nt, sigma)
+    h = lambda a: (ptr(a[:2 * S]), ptr(a[2 * S:]))  # noqa: E731
+
+    def ops(L):
+        sm.check(sm.lib.sm_upload_gauge(L.ctx, *h(U)))
+        out = []
+        for dag, src in ((0, psi), (1, chi)):
+            o = np.empty(4 * S)
+            sm.check(sm.lib.sm_dirac(L.ctx, *h(src), *h(o), -0.07, dag))
+            out.append(o)
+        o = np.empty(4 * S)
+        sm.check(sm.lib.sm_ddag(L.ctx, *h(psi), *h(o), -0.07))
+        out.append(o)
+        return out
+
+    one = sm.Lattice(Nx, Nt)
+    ref = ops(one)
+    one.close()
+    with opts_env(apply_split=split):
+        loop = sm.Lattice(Nx, Nt, loopback=True)
+    got = ops(loop)
+    loop.close()
+    for k, (g, r) in enumerate(zip(got, ref)):
+        assert bits_equal(g, r), (split, k)

@@ -151,6 +151,19 @@ r() {
   done
 }
 
+# s: the t-shard apply without its edge columns (apply_split=2) -- bitwise tests, then the
+#    loopback's apply time per schedule, twice
+s() {
+  local L="python -u tools/loopback_probe.py --shapes 4096x512,4096x1024,4096x2048 --iters 100 --rounds 2 --applies 20"
+  timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_rccl_loopback_gpu.py \
+    -k apply_modes > gpurun_out/r05s_tests.log 2>&1 || return 1
+  for i in 1 2; do
+    for m in 0 1 2; do
+      SM_TEST_OPTS=apply_split=$m timeout -k 10 300 $L > gpurun_out/r05s_split${m}_$i.log 2>&1 || return 1
+    done
+  done
+}
+
 # gate: the full GPU gate in natural order, then smoke (tag $2)
 gate() {
   local T=${1:-cur}
