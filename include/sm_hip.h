@@ -192,7 +192,7 @@ const char *sm_build_id(void);
  * its streamed buffers relative to each other, so creation searches one buffer
  * at a time (x, then the three direction buffers), trying up to
  * `candidates` fresh allocations of that buffer and keeping the fastest
- * (schwingermodel_amd/csrc/sm_capi.cpp placement_probe; not on host-staged
+ * (schwingermodel_amd/csrc/sm_place.cpp placement_probe; not on host-staged
  * contexts, where shard processes share one GPU); a sweep over the four
  * buffers that improved the pass by > 1 % is followed by another (at most 3).
  * *n = timings (0: no probe, else 1 + 4 per sweep), us_per_pass[0] (may be

@@ -86,7 +86,7 @@ struct sm_ctx {
     // contiguous memory), 0 = own size (A/B). Test option pad_alloc=N; DESIGN
     // §2 and profiles/r04_e_alloc_trials.jsonl give the measurements.
     int pad_alloc = 5;
-    // Placement probe at creation (sm_capi.cpp placement_probe): candidates
+    // Placement probe at creation (sm_place.cpp placement_probe): candidates
     // per streamed buffer (0 = no probe; sm_set_placement_probe, test option
     // place_probe=N), the pass time of the initial set and after each
     // buffer's search (us per pass), and which buffers moved (bit mask).
@@ -229,6 +229,14 @@ double2 *face2_recv(sm_ctx *c, int which);  // 0: d, 1: r, 2: U, 3: Ad
 double2 *face4_recv_U(sm_ctx *c);           // 4-deep ghost links (recompute-Ad CG)
 bool cg_ra_ok(const sm_ctx *c);             // the recompute-Ad pass fits this shard (Wt >= 4 when sharded)
 int exchange_ghost_U(sm_ctx *c);
+
+// Streamed CG buffers and the placement probe (sm_place.cpp)
+size_t stream_alloc_bytes(size_t bytes, size_t floor_bytes = size_t(2) << 30);
+hipError_t stream_malloc(sm_ctx *c, void **p, size_t bytes);
+void stream_free(sm_ctx *c, void *p);
+size_t link_code_bytes(long n);           // codes of n links (sm_linkcode.h), flag words and flag bytes
+int placement_probe(sm_ctx *c, size_t fb);
+int placement_probe_default();            // candidates per buffer for new contexts
 
 // even-odd preconditioned pseudofermion action (sm_eo.cpp); phi / chi in the
 // full layout, only their even sites used
