@@ -79,7 +79,14 @@ def main():
     dslash = [k for k in kernels if "dslash_kernel" in k and "<0, 0>" in k]
     # the CG pass behind bench.py's value: one shard, x rows, fused multiply-
     # adds, in-kernel scalars off, link angles, ticketed tail (sm_cgra.hip)
-    cgk = [k for k in kernels if "cg_ra_kernel<0, 1, 2, 0, 1, 1" in k]  # any march-schedule suffix
+    # (link codes: UC 2 packed flag bytes, 145 B/site; UC 1 flag words, 148; any march-schedule suffix)
+    cg_bytes = {2: 145, 1: 148}
+    cgk, cg_uc = [], None
+    for uc in (2, 1):
+        cgk = [k for k in kernels if f"cg_ra_kernel<0, 1, 2, 0, {uc}, 1" in k]
+        if cgk:
+            cg_uc = uc
+            break
     out = {"Nx": a.nx, "Nt": a.nt, "build_id": a.build_id,
            "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes",
            "correction": "reads = 2 x FETCH_SIZE KiB (gfx950), writes = WRITE_SIZE KiB",
@@ -87,7 +94,7 @@ def main():
            "dslash_kernel": dslash[0] if dslash else None,
            "hbm_bytes_per_launch": kernels[dslash[0]]["hbm_bytes"] if dslash else None,
            "cg_pass_kernel": cgk[0] if cgk else None,
-           "cg_pass_algorithmic_bytes_per_launch": 144 * sites,
+           "cg_pass_algorithmic_bytes_per_launch": cg_bytes[cg_uc] * sites if cgk else None,
            "cg_pass_hbm_bytes_per_launch": kernels[cgk[0]]["hbm_bytes"] if cgk else None,
            "kernels": kernels}
     with open(os.path.join(pdir, f"{tag}_dslash_pmc.json"), "w") as f:
