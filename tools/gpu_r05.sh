@@ -164,6 +164,19 @@ s() {
   done
 }
 
+# u: where the CG pass's extra reads come from -- L2 counters and timing per launch geometry
+#    (waves per block, rows per block) at 4096^2 with the link codes
+u() {
+  rm -rf gpurun_out/r05u_*
+  for g in 1,64 1,128 1,32 2,64 4,64 2,32; do
+    timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum --output-format csv \
+      -d gpurun_out/r05u_pmc_${g/,/_} -o run -- python3 tools/tune_shapes.py 4096x4096:$g,1 --iters 30 --rounds 1 \
+      > gpurun_out/r05u_pmc_${g/,/_}.log 2>&1 || return 1
+  done
+  timeout -k 10 300 python3 -u tools/tune_shapes.py 4096x4096:1,64,1 4096x4096:1,128,1 4096x4096:1,32,1 \
+    4096x4096:2,64,1 4096x4096:4,64,1 4096x4096:2,32,1 --iters 100 --rounds 3 > gpurun_out/r05u_time.log 2>&1
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step
 #      gap, FETCH / WRITE passes, the loopback, and the placement probe over 10 contexts
 fin() {
