@@ -177,6 +177,16 @@ u() {
     4096x4096:2,64,1 4096x4096:4,64,1 4096x4096:2,32,1 --iters 100 --rounds 3 > gpurun_out/r05u_time.log 2>&1
 }
 
+# w: read request sizes (32 / 64 / 128 B) of the CG pass and the apply
+w() {
+  rm -rf gpurun_out/r05w_*
+  local P="python3 bench.py --steps 10 --warmup 2 --applies 4 --no-cpu-baseline --no-weak --evolved-trajectories 0"
+  timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum \
+    --output-format csv -d gpurun_out/r05w_sizes -o run -- $P > gpurun_out/r05w_sizes.log 2>&1 &&
+  timeout -s KILL 120 rocprofv3 --pmc TCC_REQ_sum TCC_READ_sum TCC_STREAMING_REQ_sum TCC_BUBBLE_sum \
+    --output-format csv -d gpurun_out/r05w_req -o run -- $P > gpurun_out/r05w_req.log 2>&1
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step
 #      gap, FETCH / WRITE passes, the loopback, and the placement probe over 10 contexts
 fin() {
