@@ -187,6 +187,19 @@ w() {
     --output-format csv -d gpurun_out/r05w_req -o run -- $P > gpurun_out/r05w_req.log 2>&1
 }
 
+# x: read requests of the CG pass when the halo lanes of the named streams load owned columns
+#    (counter-only variants, tools/exp_halo_build.py; wrong values, traffic only)
+x() {
+  rm -rf gpurun_out/r05x_*
+  local T="python3 tools/tune_shapes.py 4096x4096:1,64,1 --iters 30 --rounds 1"
+  for v in base d1 d2 uc x all; do
+    local lib=""
+    [ $v != base ] && lib=$PWD/tools/exp/libsm_hip_$v.so
+    SM_LIB_PATH=$lib timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_READ_sum \
+      --output-format csv -d gpurun_out/r05x_$v -o run -- $T > gpurun_out/r05x_$v.log 2>&1 || return 1
+  done
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step
 #      gap, FETCH / WRITE passes, the loopback, and the placement probe over 10 contexts
 fin() {
