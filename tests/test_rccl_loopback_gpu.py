@@ -213,3 +213,37 @@ def test_loopback_apply_modes_bitwise(sm, shape, sigma, split):
     loop.close()
     for k, (g, r) in enumerate(zip(got, ref)):
         assert bits_equal(g, r), (split, k)
+
+
+@pytest.mark.parametrize("shape", [(4096, 1024), (4096, 512)], ids=["4096x1024_edge32", "4096x512_edge16"])
+def test_loopback_cg_edge_rows_rule(sm, shape):
+    """The t-shard CG pass's edge launch marches 32-row chunks where only those
+    let its tiles join the interior ones in one residency round (4096 x 1024)
+    and 16 elsewhere (sm_capi.cpp cg_ra_pass): the loopback solve equals the
+    one-shard solve (iterations within one, x to 1e-12) either way, and forcing the
+    other chunk length (test option edge_xchunk) changes only the partial
+    sums' partition."""
+    from conftest import opts_env
+    Nx, Nt = shape
+    S = Nx * Nt
+    U, psi, _, _ = fields(sm, Nx, Nt, 0.2374)
+    h = lambda a: (ptr(a[:2 * S]), ptr(a[2 * S:]))  # noqa: E731
+    out = {}
+    other = 16 if Nt == 1024 else 32
+    for name, kw, opts in (("one", {}, {}), ("loop", {"loopback": True}, {}),
+                           ("loop_other", {"loopback": True}, {"edge_xchunk": other})):
+        with opts_env(**opts):
+            L = sm.Lattice(Nx, Nt, **kw)
+        sm.check(sm.lib.sm_upload_gauge(L.ctx, *h(U)))
+        sm.check(sm.lib.sm_tune_cg(L.ctx, 5, 0))
+        x = np.empty(4 * S)
+        res = sm.CGResult()
+        sm.check(sm.lib.sm_cg(L.ctx, *h(psi), *h(x), -0.06, 1e-10, 20000, ctypes.byref(res)))
+        out[name] = (res.converged, res.iterations, x)
+        L.close()
+    c0, it0, x0 = out["one"]
+    assert c0 == 1
+    for k in ("loop", "loop_other"):
+        c, it, x = out[k]
+        assert c == 1 and abs(it - it0) <= 1, (k, it, it0)
+        assert np.linalg.norm(x - x0) / np.linalg.norm(x0) <= 1e-12, k
