@@ -200,6 +200,18 @@ x() {
   done
 }
 
+# z: A/B of the product library against tools/ab_libs/libsm_hip_base.so (the previous build), ABAB x4,
+#    the driver's bench at 200 steps without the extras; then the CG parity subset on the product
+z() {
+  local B="python3 bench.py --steps 200 --warmup 20 --applies 20 --no-cpu-baseline --no-weak --evolved-trajectories 0"
+  for i in 1 2 3 4; do
+    SM_LIB_PATH=$PWD/tools/ab_libs/libsm_hip_base.so SM_LIB_AB=1 timeout -k 10 200 $B > gpurun_out/r05z_base_$i.log 2>&1 &&
+    timeout -k 10 200 $B > gpurun_out/r05z_new_$i.log 2>&1 || return 1
+  done
+  timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_cg_paths_gpu.py \
+    -k "cg" > gpurun_out/r05z_tests.log 2>&1
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step
 #      gap, FETCH / WRITE passes, the loopback, and the placement probe over 10 contexts
 fin() {
