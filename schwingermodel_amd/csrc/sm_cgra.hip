@@ -289,7 +289,11 @@ __device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x
             bxs = 1;
         }
     }
-    const int cx = c < 0 ? 0 : (c >= Wt ? Wt - 1 : c);
+    // x is read and written by the owned lanes only: the halo lanes load their
+    // wave's nearest owned column (no partial line outside the owned ones;
+    // 106.6 against 108.0 read B/site, profiles/r05_x_halo_variants_counters.jsonl)
+    const int co = min(max(c, g * RW), g * RW + RW - 1);
+    const int cx = co < 0 ? 0 : (co >= Wt ? Wt - 1 : co);
     auto wrap = [Nx](int x) { int w = x % Nx; return w < 0 ? w + Nx : w; };
     // REV marches the chunk from its last row to its first: virtual row v
     // (the march order, x0 - 6 .. xe - 1 as forward) is physical row
