@@ -212,6 +212,25 @@ z() {
     -k "cg" > gpurun_out/r05z_tests.log 2>&1
 }
 
+# ab: the apply with odd x-chunks marching backward -- bitwise tests, apply time A/B (apply_alt=0 / 1, x4),
+#     L2 read counters per variant
+ab() {
+  rm -rf gpurun_out/r05ab_*
+  timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_parity.py \
+    tests/test_gpu_large.py -k "march_directions or operators_bitwise or oracle_parity or large_lattice" \
+    > gpurun_out/r05ab_tests.log 2>&1 || return 1
+  local B="python3 bench.py --steps 20 --warmup 5 --applies 200 --no-cpu-baseline --no-weak --evolved-trajectories 0"
+  for i in 1 2 3 4; do
+    SM_TEST_OPTS=apply_alt=0 timeout -k 10 200 $B > gpurun_out/r05ab_fwd_$i.log 2>&1 &&
+    timeout -k 10 200 $B > gpurun_out/r05ab_alt_$i.log 2>&1 || return 1
+  done
+  local P="python3 bench.py --steps 4 --warmup 2 --applies 10 --no-cpu-baseline --no-weak --evolved-trajectories 0"
+  SM_TEST_OPTS=apply_alt=0 timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum --output-format csv \
+    -d gpurun_out/r05ab_pmc_fwd -o run -- $P > gpurun_out/r05ab_pmc_fwd.log 2>&1 &&
+  timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum --output-format csv \
+    -d gpurun_out/r05ab_pmc_alt -o run -- $P > gpurun_out/r05ab_pmc_alt.log 2>&1
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step
 #      gap, FETCH / WRITE passes, the loopback, and the placement probe over 10 contexts
 fin() {
