@@ -231,6 +231,15 @@ ab() {
     -d gpurun_out/r05ab_pmc_alt -o run -- $P > gpurun_out/r05ab_pmc_alt.log 2>&1
 }
 
+# ac: apply variants 1 (all forward) and 3 (odd x-chunks backward) interleaved in ONE process on the same
+#     buffers, 32 / 64-row chunks, D and D^dag, twice
+ac() {
+  for d in 0 1 0 1; do
+    timeout -k 10 300 python3 -u tools/tune_dslash.py --bt 256 --xchunk 32,64 --remap 1 --variant 1,3 --rounds 15 \
+      --applies 50 --dagger $d >> gpurun_out/r05ac_d$d.jsonl 2>&1 || return 1
+  done
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step
 #      gap, FETCH / WRITE passes, the loopback, and the placement probe over 10 contexts
 fin() {
