@@ -121,9 +121,7 @@ int sm_synchronize(sm_ctx *ctx);
 /* Launch-geometry knobs of the stencil kernels (tuning / A-B benchmarks):
  * bt = t-columns per block (64, 128, 256), xchunk = rows marched per block,
  * xcd_remap = 1 maps the tiles one XCD receives to x-adjacent tiles,
- * variant selects the stencil code variant (0 one-row lookahead, 1 two-row
- * lookahead, 2 the same capped at 3 waves/SIMD, 3 variant 1 with the odd
- * x-chunks of plain applies marching backward). Values <= 0 (< 0 for xcd_remap
+ * variant selects the stencil code variant. Values <= 0 (< 0 for xcd_remap
  * and variant) keep the current setting. */
 int sm_tune(sm_ctx *ctx, int bt, int xchunk, int xcd_remap, int variant);
 /* CG path: fused = 5 (the default from 256^2 sites per shard up) is the

@@ -410,8 +410,6 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //                       sm_set_placement_probe sets the default)
 //   probe_min_mib=N     smallest field (MiB) whose context runs the probe
 //   link_angles=0|1     recompute-Ad pass reads the links as one-double codes
-//   apply_alt=0|1       Dirac apply: odd x-chunks march backward (1: code
-//                       variant 3) or every chunk forward (0: variant 1)
 //   bt=64|128|256       Dirac apply t-columns per block
 //   eo_fused=0, eo_cg_td=0, eo_cg_folded=1   even-odd operator / CG forms
 //   debug_cg=1          CG host loops print their status (stderr)
@@ -468,8 +466,6 @@ static int apply_test_opts(sm_ctx *c) {
             c->pad_alloc = iv;
         } else if (k == "link_angles") {
             c->link_angles = iv ? 1 : 0;
-        } else if (k == "apply_alt") {
-            c->cfg.variant = iv ? 3 : 1;
         } else if (k == "bt") {
             if (iv != 64 && iv != 128 && iv != 256) return fail(SM_ERR_ARG, "SM_TEST_OPTS: bt must be 64, 128 or 256");
             c->cfg.bt = iv;

@@ -31,7 +31,6 @@ struct DArgs {
     int Nx, Wt, t0, Ntg, xchunk;
     int TB, XB, xcd_remap;   // tile grid (t-blocks x x-chunks), 1-D launch
     int tb0, tbn, part0;     // this launch covers t-blocks [tb0, tb0+tbn) mod TB; partials by tile
-    int alt;                 // plain one-shard applies: odd x-chunks march backward
     double mass;
 };
 
@@ -209,54 +208,6 @@ __device__ __forceinline__ void dslash_body(const DArgs &a) {
                 uxm = cur.ux;
                 cur = nxt;
             }
-        } else if (EPI == EPI_NONE && !PROJ && a.alt && (xc & 1)) {
-        // Backward march (odd x-chunks, plain applies): x = xend-1 .. xbeg.
-        // Row x takes psi(x+1) from the row marched last and psi(x-1), U_x(x-1)
-        // from the row marched next -- the forward march's operands, so the
-        // values are bitwise the same. An x-chunk and its neighbours then
-        // reach their shared halo rows at the same time (even chunks end at
-        // the boundary the next odd chunk ends at, and start where the one
-        // before it starts), so the second read of a halo row is an L2 hit.
-        // The row marched next is loaded whole, the halo row xbeg-1 included
-        // (its t-neighbours and links are the neighbour chunk's, read there
-        // at the same time); past it the prefetch clamps (cache hits).
-        auto rowb = [&](int r) {
-            r = r < xbeg - 1 ? xbeg - 1 : r;
-            return r < 0 ? r + Nx : r;
-        };
-        const long nh = (long)wrap(xend) * Wt + t;
-        double2 pxp0 = a.in[nh], pxp1 = a.in[nh + V];  // psi(x+1) of the row being computed
-        Row R0, R1, R2;
-        load_row(a, L, xend - 1, xend - 1, t, R0);
-        {
-            const int r = rowb(xend - 2);
-            load_row(a, L, r, r, t, R1);
-        }
-        int x = xend - 1;
-        auto step = [&](Row &cur, const Row &nx1, Row &nx2) {
-            const long n = (long)x * Wt + t;
-            {
-                const int r = rowb(x - 2);
-                load_row(a, L, r, r, t, nx2);
-            }
-            Row P;
-            P.c0 = pxp0;
-            P.c1 = pxp1;
-            double2 s0, s1;
-            dslash_site<DAG, PROJ>(a, sr0, sl0, elo, ehi, cur, P, nx1.c0, nx1.c1, nx1.ux, s0, s1);
-            st_nt(a.out + n, s0);
-            st_nt(a.out + n + V, s1);
-            pxp0 = cur.c0;
-            pxp1 = cur.c1;
-        };
-        for (;;) {
-            step(R0, R1, R2);
-            if (--x < xbeg) break;
-            step(R1, R2, R0);
-            if (--x < xbeg) break;
-            step(R2, R0, R1);
-            if (--x < xbeg) break;
-        }
         } else {
         // Three row registers used round-robin (manual 3-way unroll): the
         // rotation is a renaming, so no register copy waits on an in-flight load.
@@ -303,8 +254,7 @@ __device__ __forceinline__ void dslash_body(const DArgs &a) {
 
 // Variants (LaunchCfg::variant): 0 = one-row lookahead; 1 = two-row
 // lookahead, registers unconstrained (2 waves/SIMD); 2 = two-row lookahead
-// capped at 168 VGPRs (3 waves/SIMD); 3 = variant 1 with the odd x-chunks of
-// plain applies marching backward (DArgs::alt).
+// capped at 168 VGPRs (3 waves/SIMD).
 template <int DAG, int EPI>
 __global__ void __launch_bounds__(256) dslash_kernel_v0(DArgs a) { dslash_body<DAG, EPI, 1>(a); }
 template <int DAG, int EPI>
@@ -369,7 +319,6 @@ void launch_dslash(hipStream_t s, const Geometry &g, const LaunchCfg &c, int dag
     a.TB = (g.Wt + c.bt - 1) / c.bt;
     a.XB = (g.Nx + c.xchunk - 1) / c.xchunk;
     a.xcd_remap = c.xcd_remap;
-    a.alt = c.variant == 3 ? 1 : 0;
     a.mass = mass;
     if (tbn < 0) {
         tb0 = 0;
@@ -393,7 +342,7 @@ void launch_dslash(hipStream_t s, const Geometry &g, const LaunchCfg &c, int dag
         }                                                                               \
     } while (0)
     if (f.proj) SM_LAUNCH(dslash_kernel_proj);
-    else if (c.variant == 1 || c.variant == 3) SM_LAUNCH(dslash_kernel_v1);
+    else if (c.variant == 1) SM_LAUNCH(dslash_kernel_v1);
     else if (c.variant == 2) SM_LAUNCH(dslash_kernel_v2);
     else SM_LAUNCH(dslash_kernel_v0);
 #undef SM_LAUNCH

@@ -277,41 +277,6 @@ def test_oracle_parity_random_sizes(sm, oracle):
             assert bits_equal(flat(out), flat(ref)), (Nx, Nt, dag)
 
 
-@pytest.mark.parametrize("Nx,Nt", [(7, 5), (33, 70), (256, 512), (1000, 1024), (4096, 64)])
-def test_apply_march_directions_bitwise(sm, oracle, Nx, Nt):
-    """The Dirac apply marches odd x-chunks backward (test option apply_alt,
-    sm_kernels.hip dslash_body): D, D^dag and D D^dag are bitwise the all-forward
-    apply's and the oracle's, on shapes with one-row chunks, ragged last chunks
-    and single t-blocks."""
-    S = Nx * Nt
-    U, psi = sm.spinor(S), sm.spinor(S)
-    sm.lib.sm_fill_gauge(31, 0.41, Nt, 0, Nx, 0, Nt, ptr(U.mu0), ptr(U.mu1))
-    sm.lib.sm_fill_spinor(32, Nt, 0, Nx, 0, Nt, ptr(psi.mu0), ptr(psi.mu1))
-    h = lambda a: (ptr(a.mu0), ptr(a.mu1))  # noqa: E731
-    outs = {}
-    for alt in (0, 1):
-        with opts_env(apply_alt=alt):
-            L = sm.Lattice(Nx, Nt)
-        sm.check(sm.lib.sm_upload_gauge(L.ctx, *h(U)))
-        res = []
-        for dag in (0, 1):
-            o = sm.spinor(S)
-            sm.check(sm.lib.sm_dirac(L.ctx, *h(psi), *h(o), -0.07, dag))
-            res.append(flat(o))
-        o = sm.spinor(S)
-        sm.check(sm.lib.sm_ddag(L.ctx, *h(psi), *h(o), -0.07))
-        res.append(flat(o))
-        outs[alt] = res
-        L.close()
-    for k in range(3):
-        assert bits_equal(outs[0][k], outs[1][k]), k
-    for dag in (0, 1):
-        ref = sm.spinor(S)
-        oracle.oracle_dirac_mt(Nx, Nt, ptr(U.mu0), ptr(U.mu1), ptr(psi.mu0), ptr(psi.mu1),
-                               ptr(ref.mu0), ptr(ref.mu1), -0.07, dag, 8)
-        assert bits_equal(outs[1][dag], flat(ref)), dag
-
-
 @pytest.mark.parametrize("Nx,Nt", [(1024, 1024), (4096, 4096)])
 def test_large_lattice_properties(sm, oracle, Nx, Nt):
     """Full-size checks: bitwise vs the threaded oracle on the same inputs
