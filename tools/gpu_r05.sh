@@ -240,6 +240,13 @@ ac() {
   done
 }
 
+# ad: the N > 1 bench path rehearsed on one GPU with host-staged halos (4 and 8 ranks: spawn, barrier,
+#     max over ranks, one JSON line)
+ad() {
+  timeout -k 10 400 python3 bench.py --gpus 4 --transport hosted --steps 20 --warmup 5 > gpurun_out/r05ad_bench4.log 2>&1 &&
+  timeout -k 10 500 python3 bench.py --gpus 8 --transport hosted --steps 20 --warmup 5 > gpurun_out/r05ad_bench8.log 2>&1
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step
 #      gap, FETCH / WRITE passes, the loopback, and the placement probe over 10 contexts
 fin() {
