@@ -247,6 +247,15 @@ ad() {
   timeout -k 10 500 python3 bench.py --gpus 8 --transport hosted --steps 20 --warmup 5 > gpurun_out/r05ad_bench8.log 2>&1
 }
 
+# ae: 4096 x 512 shards (config 4 over 8 GPUs, the weak slab): rows per block, one-wave blocks, codes on
+ae() {
+  timeout -k 10 300 python3 -u tools/tune_shapes.py 4096x512:1,48,1 4096x512:1,40,1 4096x512:1,32,1 4096x512:1,24,1 \
+    4096x512:1,21,1 4096x512:1,20,1 4096x512:1,16,1 4096x512:1,64,1 4096x512:1,48,0 --iters 200 --rounds 5 \
+    > gpurun_out/r05ae_4096x512.log 2>&1 &&
+  timeout -k 10 300 python3 -u tools/tune_shapes.py 4096x1024:1,40,1 4096x1024:1,32,1 4096x1024:1,21,1 4096x1024:1,64,1 \
+    4096x2048:1,32,1 4096x2048:1,40,1 4096x2048:1,64,1 --iters 100 --rounds 5 >> gpurun_out/r05ae_4096x512.log 2>&1
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step
 #      gap, FETCH / WRITE passes, the loopback, and the placement probe over 10 contexts
 fin() {
