@@ -256,6 +256,18 @@ ae() {
     4096x2048:1,32,1 4096x2048:1,40,1 4096x2048:1,64,1 --iters 100 --rounds 5 >> gpurun_out/r05ae_4096x512.log 2>&1
 }
 
+# af: 4096 x 512 rows per block (one dispatch round: 21) in the plain shard and through the loopback
+af() {
+  timeout -k 10 300 python3 -u tools/tune_shapes.py 4096x512:1,48,0 4096x512:1,21,0 4096x512:1,24,0 4096x512:1,22,0 \
+    4096x512:1,25,0 4096x512:1,21,1 --iters 200 --rounds 5 > gpurun_out/r05af_shapes.log 2>&1 || return 1
+  for i in 1 2; do
+    for g in 1,48 1,21 1,24; do
+      timeout -k 10 200 python -u tools/loopback_probe.py --shapes 4096x512 --iters 200 --rounds 3 --applies 5 --geom $g \
+        >> gpurun_out/r05af_loopback.log 2>&1 || return 1
+    done
+  done
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step
 #      gap, FETCH / WRITE passes, the loopback, and the placement probe over 10 contexts
 fin() {

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--applies", type=int, default=50)
     ap.add_argument("--m0", type=float, default=-0.06)
     ap.add_argument("--sigma", type=float, default=0.2374)
+    ap.add_argument("--geom", default="", help="waves per block,rows per block of the CG pass (sm_tune_cg_geometry)")
     a = ap.parse_args()
     import torch
     import schwingermodel_amd as sm
@@ -57,6 +58,8 @@ def main():
             sm.check(sm.lib.sm_set_stream(L.ctx, ctypes.c_void_p(s.cuda_stream)))
             sm.check(sm.lib.sm_upload_gauge_dev(L.ctx, vp(dU)))
             sm.check(sm.lib.sm_tune_cg(L.ctx, 5, 0))
+            if a.geom:
+                sm.check(sm.lib.sm_tune_cg_geometry(L.ctx, *(int(v) for v in a.geom.split(","))))
             sm.check(sm.lib.sm_cg_link_angles(L.ctx, -1, None))
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for _ in range(a.rounds):
@@ -88,7 +91,7 @@ def main():
                 e1.synchronize()
                 ap[k].append(e0.elapsed_time(e1) * 1e3 / a.applies)
         for k, L in ctxs.items():
-            print(json.dumps({"shape": shape, "context": k, "ms_per_iter": round(statistics.median(times[k]), 4),
+            print(json.dumps({"shape": shape, "context": k, "geom": a.geom or "default", "ms_per_iter": round(statistics.median(times[k]), 4),
                               "min": round(min(times[k]), 4), "iters": a.iters,
                               "host_enqueue_ms_per_iter": round(statistics.median(host[k]), 4),
                               "apply_us": round(statistics.median(ap[k]), 2)}), flush=True)
