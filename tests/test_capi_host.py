@@ -178,3 +178,32 @@ def test_jackknife_matches_reference():
         d = np.array(c["data"])
         got = sm.lib.sm_jackknife_error(d.ctypes.data, len(d), c["bin"])
         assert got == c["jackknife_error"], (len(d), got, c["jackknife_error"])
+
+
+def test_conf_read_truncated_file_fails(tmp_path):
+    """A conf file shorter than Nx*Nt*2 records fails with SM_ERR_ARG and a
+    message naming the site (sm_conf.cpp). The reference's readBinary does not
+    check its reads (src/gauge_conf.cpp:515-531), so past the end it would keep
+    whatever the variables held; the drop-in refuses instead."""
+    Nx, Nt = 4, 4
+    S = Nx * Nt
+    u = np.arange(4 * S, dtype=np.float64)
+    u0, u1 = planes(u, S)
+    path = str(tmp_path / "short.ctxt")
+    assert lib.sm_conf_write(path.encode(), Nx, Nt, u0.ctypes.data, u1.ctypes.data) == 0
+    with open(path, "r+b") as f:
+        f.truncate(28 * (2 * S - 3))
+    back = np.empty(4 * S)
+    b0, b1 = planes(back, S)
+    assert lib.sm_conf_read(path.encode(), Nx, Nt, b0.ctypes.data, b1.ctypes.data) == 1
+    assert b"truncated" in lib.sm_last_error()
+
+
+def test_placement_probe_setting_is_validated():
+    """sm_set_placement_probe takes 0 (no probe) .. 8 candidates per buffer and
+    rejects anything else without touching the current setting (sm_place.cpp)."""
+    for bad in (-1, 9, 100):
+        assert lib.sm_set_placement_probe(bad) == 1
+        assert b"0..8" in lib.sm_last_error()
+    for ok in (0, 8, 3):  # leaves the default (3) in place
+        assert lib.sm_set_placement_probe(ok) == 0
