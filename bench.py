@@ -389,14 +389,43 @@ def time_applies(rt, sh, m0, n):
 def placement_report(sh):
     """The context's placement probe (sm_placement_report): the CG pass time of
     the initial placement of its streamed buffers and after the search of each
-    buffer (x, d1, d0, d2), and which buffers were re-placed."""
+    buffer (the library names them, sm_placement_buffer_name), and which
+    buffers were re-placed."""
     sm = sh.sm
     us = (ctypes.c_double * 16)()
     n, chosen = ctypes.c_int(0), ctypes.c_int(0)
     sm.check(sm.lib.sm_placement_report(sh.L.ctx, us, ctypes.byref(n), ctypes.byref(chosen)))
-    names = ("x", "d1", "d0", "d2")
-    return {"us_per_pass": [round(us[k], 1) for k in range(n.value)],
-            "moved": [names[i] for i in range(4) if chosen.value >> i & 1]}
+    names = []
+    while (nm := sm.lib.sm_placement_buffer_name(len(names))) is not None:
+        names.append(nm.decode())
+    rep = {"us_per_pass": [round(us[k], 1) for k in range(n.value)],
+           "moved": [names[i] for i in range(len(names)) if chosen.value >> i & 1]}
+    if n.value:
+        rep["probe_kept_us"] = rep["us_per_pass"][-1]
+    return rep
+
+
+def check_rccl_world(transport, world, nmin, nmax):
+    """The RCCL world the communicators themselves report (sm_comm_info:
+    ncclCommCount), min and max over ranks, against the job: under
+    --transport rccl with N > 1 every rank's communicator must hold exactly
+    WORLD_SIZE ranks, or the line would describe a job that did not run.
+    Returns None when it holds, else the reason."""
+    if transport == "rccl" and world > 1 and not nmin == nmax == world:
+        return f"RCCL communicators hold {nmin}..{nmax} ranks, WORLD_SIZE is {world}"
+    return None
+
+
+def comm_world(args, rt, sh):
+    """{"transport", "rccl_ranks": [min, max] over ranks} from sm_comm_info;
+    exits non-zero when RCCL's own count differs from WORLD_SIZE."""
+    transport, n, _ = sh.L.comm_info()
+    mx, neg_mn = max_over_ranks(rt, [float(n), float(-n)])
+    nmin, nmax = int(-neg_mn), int(mx)
+    why = check_rccl_world(args.transport, rt["world"], nmin, nmax)
+    if why:
+        raise SystemExit(f"[bench] {why}: refusing to report this run")
+    return {"transport": transport, "rccl_ranks": [nmin, nmax]}
 
 
 def cg_bytes_per_site(sh, cg_path):
@@ -515,11 +544,16 @@ def run_config34(args, rt, cfg_id):
     m0, world, rank = cfg["m0"], rt["world"], rt["rank"]
     sh = Shard(rt, Nx, Nt, cfg["sigma"])
     placement = placement_report(sh)
+    world_seen = comm_world(args, rt, sh)
     begin_cg(sh, m0, args.cg_path, args.no_link_angles)
     apply_time = time_applies(rt, sh, m0, args.applies)
     t_cg, cg_bps = time_cg_steps(rt, sh, m0, args.cg_path, args.warmup, args.steps, args.no_link_angles, begun=True)
     apply_s = apply_time()
     t_cg, apply_s = max_over_ranks(rt, [t_cg, apply_s])
+    if "probe_kept_us" in placement:
+        # the probe times short bursts; the timed run sustains its own pass time
+        # (both are reported)
+        placement["sustained_us_per_pass"] = round(1e6 * t_cg / args.steps, 1)
     V = sh.V
     evolved = time_evolved(args, rt, sh, cfg, m0) if world == 1 and args.evolved_trajectories > 0 else None
     sh.close()
@@ -577,6 +611,7 @@ def run_config34(args, rt, cfg_id):
         "weak": weak,
         "hmc_evolved_field": evolved,
         "placement_probe": placement,
+        "comm": world_seen,
     })
     print(json.dumps(line), flush=True)
 
@@ -588,6 +623,7 @@ def run_config5(args, rt):
     sm = None
     sh = Shard(rt, Nx, Nt, cfg["sigma"])
     placement = placement_report(sh)
+    world_seen = comm_world(args, rt, sh)
     sm = sh.sm
     sm.check(sm.lib.sm_tune_cg(sh.L.ctx, CG_PATH_ID[args.cg_path], 0))
     sm.check(sm.lib.sm_cg_link_angles(sh.L.ctx, 0 if args.no_link_angles else -1, None))
@@ -622,6 +658,7 @@ def run_config5(args, rt):
                          "bytes_per_site": cg_bps,
                          "achieved_GBps_per_gpu": round(cg_bps * V * res.iterations / dt / 1e9, 1)},
         "placement_probe": placement,
+        "comm": world_seen,
     })
     print(json.dumps(line), flush=True)
     if not res.converged or not rel < 1e-9:

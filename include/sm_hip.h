@@ -112,11 +112,18 @@ int sm_create_loopback(sm_ctx **out, int Nx, int Nt_global, int device, const vo
 int sm_destroy(sm_ctx *ctx);
 /* Launch on a caller stream (a hipStream_t, e.g. torch's current stream);
  * NULL restores the context's own stream. Synchronises the previous stream
- * first: each of a sharded context's two RCCL communicators is driven from
- * one stream at a time (the main one from this stream, the second from the
- * context's private comm stream), so no communicator's operations are ever
- * in flight on two streams. */
+ * first. A sharded context issues every RCCL operation with its one
+ * communicator on ONE stream, in issue order: this stream (the default), so
+ * after the switch they run here; overlapped work on the context's private
+ * comm stream joins it by events. */
 int sm_set_stream(sm_ctx *ctx, void *hip_stream);
+/* The context's communication world, read from the transport itself:
+ * transport 0 = none (one shard), 1 = host-staged (sm_create_hosted),
+ * 2 = RCCL (sm_create with nshard > 1, or sm_create_loopback); *nranks /
+ * *rank = ncclCommCount / ncclCommUserRank of the RCCL communicator, and
+ * 1 / 0 without one (the RCCL world of a host-staged or one-shard context is
+ * this process alone). Any output pointer may be NULL. */
+int sm_comm_info(const sm_ctx *ctx, int *transport, int *nranks, int *rank);
 int sm_synchronize(sm_ctx *ctx);
 /* Launch-geometry knobs of the stencil kernels (tuning / A-B benchmarks):
  * bt = t-columns per block (64, 128, 256), xchunk = rows marched per block,
@@ -163,11 +170,13 @@ int sm_cg_link_codes(sm_ctx *ctx, int on, int *in_use);
  * collectives (each shard checks its own links and the ghost links it
  * receives). */
 int sm_cg_link_angles(sm_ctx *ctx, int on, int *in_use);
-/* Bytes of link data per site the recompute-Ad CG pass read in the last
- * solve: 32 (complex links), 20 (codes with 16-bit flag words) or 17 (codes
- * with the flag nibbles of both links packed into one byte, the form every
- * field takes whose ulp offsets all lie in [-2, 1], e.g. fresh exp(i theta)
- * fields). A pass streams 128 B/site besides. */
+/* Bytes of link data per site the last CG pass launched on this context read,
+ * recorded at its launch: 32 (complex links; every path but the recompute-Ad
+ * pass), 20 (codes with 16-bit flag words) or 17 (codes with the flag
+ * nibbles of both links packed into one byte, the form every field takes
+ * whose ulp offsets all lie in [-2, 1], e.g. fresh exp(i theta) fields); 0
+ * before the first pass. A later gauge upload or Metropolis reject does not
+ * change it. The recompute-Ad pass streams 128 B/site besides. */
 int sm_cg_link_bytes(const sm_ctx *ctx, int *bytes_per_site);
 /* Diagnostic (tests): encode every link of the context's current U and decode
  * it again ON THE DEVICE with the CG pass's own functions. Writes the rebuilt
@@ -198,12 +207,20 @@ const char *sm_build_id(void);
  * *n = timings (0: no probe, else 1 + 4 per sweep), us_per_pass[0] (may be
  * NULL; room for 16) = median microseconds per pass of the initial placement,
  * us_per_pass[i] = after the search of the i-th buffer searched; *chosen = bit
- * mask of the buffers that moved (bit 0 x, 1..3 the direction buffers). */
+ * mask of the buffers that moved, bit i = buffer i of the search order, whose
+ * names sm_placement_buffer_name gives. */
 int sm_placement_report(const sm_ctx *ctx, double *us_per_pass, int *n, int *chosen);
+/* Name of bit i of sm_placement_report's mask ("x", "d1", "d0", "d2"; the
+ * order the probe searches the buffers in), NULL past the last. */
+const char *sm_placement_buffer_name(int i);
 /* Candidates per buffer of the placement probe for contexts created after
  * this call (process-wide; default 3, 0 disables the probe, at most 8).
- * Transient memory while probing: that many allocations of one buffer. */
+ * Transient memory while probing: that many allocations of one buffer.
+ * SM_ERR_ARG for a value out of range, which leaves the setting as it was. */
 int sm_set_placement_probe(int candidates);
+/* The current process-wide setting of sm_set_placement_probe (callers that
+ * change it temporarily restore this value). */
+int sm_get_placement_probe(void);
 
 /* Gauge field (host / device). Must precede every operator call; re-upload
  * whenever the caller changes U (the reference mutates U between calls,

@@ -103,6 +103,15 @@ class Lattice:
         self.ctx = h
         self.last_cg = CGResult()
 
+    TRANSPORTS = {0: "none", 1: "hosted", 2: "rccl"}
+
+    def comm_info(self):
+        """(transport, nranks, rank) as the context's transport reports them
+        (sm_comm_info: ncclCommCount / ncclCommUserRank for RCCL)."""
+        t, n, r = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib.sm_comm_info(self.ctx, ctypes.byref(t), ctypes.byref(n), ctypes.byref(r)))
+        return self.TRANSPORTS[t.value], n.value, r.value
+
     def close(self):
         if self.ctx:
             lib.sm_destroy(self.ctx)

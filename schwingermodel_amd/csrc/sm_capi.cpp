@@ -75,18 +75,67 @@ int down_rank(const sm_ctx *c) { return (c->shard - 1 + c->nshard) % c->nshard; 
 // column goes down (the down-neighbour's t = Wt). The face buffers are
 // [plane][x], 4*Nx doubles.
 
-// One communicator per stream. Co-residency assumption: while a
-// pass's pipelined face exchange runs on comm_side (comm stream), the main
-// stream's all-reduce on comm may be in flight too. RCCL documents that two
-// communicators with blocking kernels in flight at once can deadlock if those
-// kernels cannot be resident together on the GPU. Here each is ONE small
-// kernel (a send/recv pair of <= 1 MiB and a 48-byte all-reduce, one channel's
-// worth of blocks each) next to at most the CG pass's interior launch, whose
-// blocks retire on their own (no spin on other kernels), so both collective
-// kernels always find room as the pass drains; every rank issues them in the
-// same order. The multi-process RCCL run that exercises this is the driver's
-// N > 1 bench; the one-rank loopback tests cover the code path.
-ncclComm_t comm_for(const sm_ctx *c, hipStream_t s) { return s == c->comm_stream ? c->comm_side : c->comm; }
+// One communicator, one stream. Every RCCL operation of
+// a context -- face exchanges, scalar all-reduces, the gauge gather -- is
+// issued on ONE stream with the context's single communicator, in the order
+// the host issues them, which is the same on every rank. That stream runs
+// them one after another, so no two RCCL kernels of a context are ever in
+// flight at once and nothing relies on two communicators' kernels being
+// co-resident (round 5 split a second communicator off for the comm stream
+// and argued that they always were). The stream is the main stream
+// (rccl_main = 1, the default) or the private comm stream (0). An operation
+// requested on another stream joins the RCCL stream by events: that stream
+// -> RCCL stream before the operation (rccl_enter), RCCL stream -> that
+// stream after it (rccl_leave). Each such hop costs ~10 us of queue latency
+// on the critical path (RCCL loopback), so the default keeps the
+// critical chain of a CG pass -- interior launch, all-reduce, next pass --
+// on the main stream with no hop, and the pipelined face exchange joins it
+// behind the interior launch.
+static hipStream_t rccl_stream(const sm_ctx *c) { return c->rccl_main ? c->stream : c->comm_stream; }
+
+static int rccl_enter(sm_ctx *c, hipStream_t s) {
+    const hipStream_t r = rccl_stream(c);
+    if (s == r) return SM_OK;
+    HIP_TRY(hipEventRecord(c->ev_rccl_in, s));
+    HIP_TRY(hipStreamWaitEvent(r, c->ev_rccl_in, 0));
+    return SM_OK;
+}
+
+static int rccl_leave(sm_ctx *c, hipStream_t s) {
+    const hipStream_t r = rccl_stream(c);
+    if (s == r) return SM_OK;
+    HIP_TRY(hipEventRecord(c->ev_rccl_out, r));
+    HIP_TRY(hipStreamWaitEvent(s, c->ev_rccl_out, 0));
+    return SM_OK;
+}
+
+int rccl_p2p_group(sm_ctx *c, hipStream_t s, int n, const double2 *const *send_up, double2 *const *recv_down,
+                   const double2 *const *send_down, double2 *const *recv_up, size_t cnt) {
+    TRY(rccl_enter(c, s));
+    const hipStream_t cs = rccl_stream(c);
+    NCCL_TRY(ncclGroupStart());
+    for (int i = 0; i < n; ++i) {
+        NCCL_TRY(ncclSend(send_up[i], cnt, ncclDouble, up_rank(c), c->comm, cs));
+        NCCL_TRY(ncclRecv(recv_down[i], cnt, ncclDouble, down_rank(c), c->comm, cs));
+        NCCL_TRY(ncclSend(send_down[i], cnt, ncclDouble, down_rank(c), c->comm, cs));
+        NCCL_TRY(ncclRecv(recv_up[i], cnt, ncclDouble, up_rank(c), c->comm, cs));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    return rccl_leave(c, s);
+}
+
+int rccl_gather_to0(sm_ctx *c, hipStream_t s, const double *send, double *recv, size_t cnt) {
+    TRY(rccl_enter(c, s));
+    const hipStream_t cs = rccl_stream(c);
+    NCCL_TRY(ncclGroupStart());
+    if (c->shard == 0) {
+        for (int r = 1; r < c->nshard; r++) NCCL_TRY(ncclRecv(recv + (size_t)r * cnt, cnt, ncclDouble, r, c->comm, cs));
+    } else {
+        NCCL_TRY(ncclSend(send, cnt, ncclDouble, 0, c->comm, cs));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    return rccl_leave(c, s);
+}
 
 int exchange_faces_on(sm_ctx *c, hipStream_t s, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi,
                       size_t cnt) {
@@ -103,14 +152,9 @@ int exchange_faces_on(sm_ctx *c, hipStream_t s, double2 *slo, double2 *shi, doub
         HIP_TRY(hipStreamSynchronize(s));  // staging buffers are reused
         return SM_OK;
     }
-    ncclComm_t cm = comm_for(c, s);
-    NCCL_TRY(ncclGroupStart());
-    NCCL_TRY(ncclSend(shi, cnt, ncclDouble, up_rank(c), cm, s));
-    NCCL_TRY(ncclRecv(rlo, cnt, ncclDouble, down_rank(c), cm, s));
-    NCCL_TRY(ncclSend(slo, cnt, ncclDouble, down_rank(c), cm, s));
-    NCCL_TRY(ncclRecv(rhi, cnt, ncclDouble, up_rank(c), cm, s));
-    NCCL_TRY(ncclGroupEnd());
-    return SM_OK;
+    const double2 *su[1] = {shi}, *sd[1] = {slo};
+    double2 *rd[1] = {rlo}, *ru[1] = {rhi};
+    return rccl_p2p_group(c, s, 1, su, rd, sd, ru, cnt);
 }
 
 int exchange_faces_multi(sm_ctx *c, hipStream_t s, int n, double2 *const *slo, double2 *const *shi,
@@ -120,16 +164,7 @@ int exchange_faces_multi(sm_ctx *c, hipStream_t s, int n, double2 *const *slo, d
         return SM_OK;
     }
     if (cnt > kMaxFaceDoubles * (size_t)c->g.Nx) return fail(SM_ERR_ARG, "face too large (%zu)", cnt);
-    ncclComm_t cm = comm_for(c, s);
-    NCCL_TRY(ncclGroupStart());
-    for (int i = 0; i < n; ++i) {
-        NCCL_TRY(ncclSend(shi[i], cnt, ncclDouble, up_rank(c), cm, s));
-        NCCL_TRY(ncclRecv(rlo[i], cnt, ncclDouble, down_rank(c), cm, s));
-        NCCL_TRY(ncclSend(slo[i], cnt, ncclDouble, down_rank(c), cm, s));
-        NCCL_TRY(ncclRecv(rhi[i], cnt, ncclDouble, up_rank(c), cm, s));
-    }
-    NCCL_TRY(ncclGroupEnd());
-    return SM_OK;
+    return rccl_p2p_group(c, s, n, shi, rlo, slo, rhi, cnt);
 }
 
 int exchange_faces(sm_ctx *c, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi, size_t cnt) {
@@ -148,8 +183,9 @@ int allreduce_dev(sm_ctx *c, double *dev, int n) {
         HIP_TRY(hipStreamSynchronize(c->stream));
         return SM_OK;
     }
-    NCCL_TRY(ncclAllReduce(dev, dev, n, ncclDouble, ncclSum, comm_for(c, c->stream), c->stream));
-    return SM_OK;
+    TRY(rccl_enter(c, c->stream));
+    NCCL_TRY(ncclAllReduce(dev, dev, n, ncclDouble, ncclSum, c->comm, rccl_stream(c)));
+    return rccl_leave(c, c->stream);
 }
 
 // 1-deep t-faces of `field` for the operator `kind` (FaceKind): spin-projected,
@@ -173,7 +209,9 @@ int apply(sm_ctx *c, const double2 *in, double2 *out, double mass, int dagger, c
           double2 *partials, const CGScalars *skip) {
     TFaces f;
     const int TB = (c->g.Wt + c->cfg.bt - 1) / c->cfg.bt;
-    if (!c->sharded() || TB < 3 || !c->apply_split) {
+    // the split schedule overlaps the faces with the interior launch only when
+    // they travel on the comm stream (rccl_main = 0)
+    if (!c->sharded() || TB < 3 || !c->apply_split || c->rccl_main) {
         // one shard, or a narrow t-shard: faces first, then one launch
         TRY(halo(c, in, 0, dagger ? FACE_DDAG : FACE_D, &f));
         launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip);
@@ -250,16 +288,16 @@ int halo2_multi(sm_ctx *c, hipStream_t s, const double2 *const *fields, double2 
                                   faces[f] + (size_t)4 * c->g.Nx, cnt));
         return SM_OK;
     }
-    ncclComm_t cm = comm_for(c, s);
-    NCCL_TRY(ncclGroupStart());
+    const double2 *su[3], *sd[3];
+    double2 *rd[3], *ru[3];
+    if (nf > 3) return fail(SM_ERR_ARG, "halo2_multi: %d fields", nf);
     for (int f = 0; f < nf; ++f) {
-        NCCL_TRY(ncclSend(face2_send(c, f, 1), cnt, ncclDouble, up_rank(c), cm, s));
-        NCCL_TRY(ncclRecv(faces[f], cnt, ncclDouble, down_rank(c), cm, s));
-        NCCL_TRY(ncclSend(face2_send(c, f, 0), cnt, ncclDouble, down_rank(c), cm, s));
-        NCCL_TRY(ncclRecv(faces[f] + (size_t)4 * c->g.Nx, cnt, ncclDouble, up_rank(c), cm, s));
+        su[f] = face2_send(c, f, 1);
+        sd[f] = face2_send(c, f, 0);
+        rd[f] = faces[f];
+        ru[f] = faces[f] + (size_t)4 * c->g.Nx;
     }
-    NCCL_TRY(ncclGroupEnd());
-    return SM_OK;
+    return rccl_p2p_group(c, s, nf, su, rd, sd, ru, cnt);
 }
 
 int halo2(sm_ctx *c, const double2 *field, double2 *face) {
@@ -395,8 +433,10 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //   ra_red_max_blocks=N one shard: redundant scalars up to N blocks
 //   fold=0|1|2          recompute-Ad pass arithmetic (2: fused multiply-adds)
 //   apply_split=0|1     t-shard Dirac apply: interior / edge launches around
-//                       the faces on the comm stream (1; default from Wt 2048)
-//                       or faces first, then one launch (0)
+//                       the faces on the comm stream (1; default from Wt 2048,
+//                       with rccl_main=0 only) or faces first, then one launch (0)
+//   rccl_main=0|1       the stream every RCCL operation is issued on: the main
+//                       stream (1, the default) or the private comm stream (0)
 //   ra_remap=0|1        recompute-Ad pass tile order (1: each XCD takes a
 //                       contiguous range of x-adjacent chunks, t-adjacent
 //                       tiles consecutive; 0: round-robin dispatch order)
@@ -451,6 +491,8 @@ static int apply_test_opts(sm_ctx *c) {
             c->racfg.rev_odd = iv;
         } else if (k == "apply_split") {
             c->apply_split = iv ? 1 : 0;
+        } else if (k == "rccl_main") {
+            c->rccl_main = iv ? 1 : 0;
         } else if (k == "ra_remap") {
             if (iv < 0 || iv > 1) return fail(SM_ERR_ARG, "SM_TEST_OPTS: ra_remap must be 0 or 1");
             c->racfg.remap = iv;
@@ -587,6 +629,8 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     chk(hipMalloc(&c->faces4, sizeof(double2) * 64 * (size_t)Nx));
     chk(hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming));
     chk(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
+    chk(hipEventCreateWithFlags(&c->ev_rccl_in, hipEventDisableTiming));
+    chk(hipEventCreateWithFlags(&c->ev_rccl_out, hipEventDisableTiming));
     chk(hipMalloc(&c->partials, sizeof(double2) * 2 * (size_t)np));
     chk(hipMalloc(&c->sums, sizeof(double2) * 4));
     chk(hipMalloc(&c->Fbuf, sizeof(double) * 2 * (size_t)c->g.V));
@@ -625,16 +669,6 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
             sm_destroy(c);
             return fail(SM_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
         }
-        // the second communicator of the comm stream (comm_for): each
-        // communicator is driven from ONE stream, so its operations run in
-        // issue order without a cross-stream hand-off, and the main stream's
-        // all-reduce never queues behind the comm stream's face exchange
-        r = ncclCommSplit(c->comm, 0, shard, &c->comm_side, nullptr);
-        if (r != ncclSuccess) {
-            c->comm_side = nullptr;
-            sm_destroy(c);
-            return fail(SM_ERR_RCCL, "ncclCommSplit: %s", ncclGetErrorString(r));
-        }
     }
     *out = c;
     return SM_OK;
@@ -661,7 +695,6 @@ int sm_destroy(sm_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);  // e.g. a CG's trailing face exchange
-    if (c->comm_side) ncclCommDestroy(c->comm_side);
     if (c->comm) ncclCommDestroy(c->comm);
     for (double2 *&f : c->fields)
         if (f) {
@@ -680,8 +713,8 @@ int sm_destroy(sm_ctx *c) {
     if (c->h_face) (void)hipHostFree(c->h_face);
     if (c->h_red) (void)hipHostFree(c->h_red);
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
-    if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
-    if (c->ev_halo) (void)hipEventDestroy(c->ev_halo);
+    for (hipEvent_t ev : {c->ev_ready, c->ev_halo, c->ev_rccl_in, c->ev_rccl_out})
+        if (ev) (void)hipEventDestroy(ev);
     if (c->comm_stream && c->own_comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
@@ -717,6 +750,7 @@ int sm_tune_cg_geometry(sm_ctx *c, int waves_per_block, int xchunk) {
     f.XB = (c->g.Nx + f.xchunk - 1) / f.xchunk;
     if (3L * cg_fused_blocks(f) > 2L * kMaxPartials) return fail(SM_ERR_ARG, "too many blocks");
     c->racfg = f;
+    for (int &n : c->cg_shard_blocks_per_cu) n = -1;  // the block size may have changed
     return SM_OK;
 }
 
@@ -724,8 +758,9 @@ int sm_cg_link_angles(sm_ctx *c, int on, int *in_use) { return sm_cg_link_codes(
 
 int sm_cg_link_bytes(const sm_ctx *c, int *bytes_per_site) {
     if (!c || !bytes_per_site) return fail(SM_ERR_ARG, "null argument");
-    const bool codes = c->link_angles && c->cg_fused == 5 && c->uang_state == 1;
-    *bytes_per_site = !codes ? 32 : (c->link_fmt == 2 ? 17 : 20);
+    // recorded by the passes as they were launched: a later gauge
+    // upload, a Metropolis reject or a change of wish does not rewrite it
+    *bytes_per_site = c->cg_link_bytes_last;
     return SM_OK;
 }
 
@@ -782,12 +817,28 @@ int sm_bench_stream(sm_ctx *c, int two_reads, long n, const double *a, const dou
 
 int sm_set_stream(sm_ctx *c, void *s) {
     if (!c) return fail(SM_ERR_ARG, "null context");
-    // the old stream's work (and its communicator's operations) completes
-    // before any is issued on the new one: comm_for keys the main
-    // communicator to whichever stream is current
+    // the old stream's work completes before any is issued on the new one
+    // (with rccl_main the RCCL operations follow it to the new stream, one
+    // stream at a time; else they stay on the comm stream)
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->stream = s ? (hipStream_t)s : c->own_stream;
     if (c->hosted) c->comm_stream = c->stream;  // hosted contexts run on one stream
+    return SM_OK;
+}
+
+int sm_comm_info(const sm_ctx *c, int *transport, int *nranks, int *rank) {
+    if (!c) return fail(SM_ERR_ARG, "null context");
+    int t = 0, n = 1, r = 0;
+    if (c->hosted) {
+        t = 1;
+    } else if (c->comm) {
+        t = 2;
+        NCCL_TRY(ncclCommCount(c->comm, &n));  // what the communicator itself holds, not the creation arguments
+        NCCL_TRY(ncclCommUserRank(c->comm, &r));
+    }
+    if (transport) *transport = t;
+    if (nranks) *nranks = n;
+    if (rank) *rank = r;
     return SM_OK;
 }
 
@@ -1007,9 +1058,10 @@ static int cg_ra_pass(sm_ctx *c) {
         double2 *part = red ? c->partials + (j & 1) * 3 * (size_t)nparts : c->partials;
         const double2 *prev = red ? c->partials + ((j + 1) & 1) * 3 * (size_t)nparts : nullptr;
         const bool tail = !red && c->cg_tail && fc.fold >= 2 && (nparts + 63) / 64 <= kMaxTickGroups;
-        launch_cg_ra(c->stream, c->g, fc, 1, d1, d2, dn, c->cg_x, c->U, nullptr, nullptr, nullptr, c->cg_mass, j,
-                     c->sc, part, 0, fc.TBk, prev, ua, nullptr, nullptr, 0, tail ? c->tick : nullptr, nparts, c->gsum,
-                     nullptr, 0, c->link_fmt);
+        c->cg_link_bytes_last =
+            launch_cg_ra(c->stream, c->g, fc, 1, d1, d2, dn, c->cg_x, c->U, nullptr, nullptr, nullptr, c->cg_mass, j,
+                         c->sc, part, 0, fc.TBk, prev, ua, nullptr, nullptr, 0, tail ? c->tick : nullptr, nparts,
+                         c->gsum, nullptr, 0, c->link_fmt);
         if (red) {
             c->cg_flush_pass = j;
             c->cg_flush_nparts = nparts;
@@ -1041,9 +1093,10 @@ static int cg_ra_pass(sm_ctx *c) {
     // the edge launch marches short chunks so it ends long before the interior
     // one (its blocks otherwise run as long as the whole pass, AFTER the faces).
     // Edge rows per block: 16, or 32 where only the longer chunks let the
-    // edge tiles join the interior ones in one residency round (the pass holds
-    // 2 waves per SIMD, -Rpass-analysis=kernel-resource-usage: 8 one-wave
-    // blocks per CU). RCCL loopback, ms per
+    // edge tiles join the interior ones in one residency round (the resident
+    // blocks per CU come from the runtime's occupancy of the launched kernel,
+    // cg_ra_shard_blocks_per_cu: 8 one-wave blocks at 2 waves per SIMD for
+    // the round-5 kernel). RCCL loopback, ms per
     // iteration, 16 / 32 / 24 rows (profiles/r05_q_edge_chunk_long.jsonl):
     // 4096x1024 (1751 interior tiles + 512 / 256 / 342 edge ones against 2048
     // slots) 0.159 / 0.150 / 0.173; 4096x512 (all fit) 0.085 / 0.093 / 0.088;
@@ -1052,7 +1105,10 @@ static int cg_ra_pass(sm_ctx *c) {
     const bool pipe = split && c->cg_face_pipe && ra_edge_owns_faces(c, fc, tb_lo, tb_hi);
     int exc = c->cg_edge_xchunk;
     if (exc < 0) {
-        const long slots = (long)c->n_cu * 8 / fc.wpb, inner = (long)nint * fc.XB;
+        const int form = angles ? c->link_fmt : 0;
+        int &per_cu = c->cg_shard_blocks_per_cu[form];
+        if (per_cu < 0) per_cu = cg_ra_shard_blocks_per_cu(fc, form);
+        const long slots = (long)c->n_cu * (per_cu > 0 ? per_cu : 8 / fc.wpb), inner = (long)nint * fc.XB;
         auto tiles = [&](int r) { return inner + (long)nedge * ((c->g.Nx + r - 1) / r); };
         exc = tiles(16) > slots && tiles(32) <= slots ? 32 : 16;
     }
@@ -1071,9 +1127,11 @@ static int cg_ra_pass(sm_ctx *c) {
     const bool red = tail && c->cg_red_shards;
     double2 *sums = red ? &c->sc->sumr[j & 1][0] : c->sc->sum3;  // this shard's sums (all-reduced below)
     auto pass = [&](const CGFusedCfg &cf, int tb0, int tbn, hipStream_t st, int pbase, double2 *fsend) {
-        launch_cg_ra(st, c->g, cf, c->kshards(), d1, d2, dn, c->cg_x, c->U, f1, f2, face4_recv_U(c), c->cg_mass, j,
-                     c->sc, c->partials, tb0, tbn, nullptr, ua, c->Uang_face, fsend, pbase, tail ? c->tick : nullptr,
-                     nparts_pass, c->gsum, sums, red ? 1 : 0, c->link_fmt);
+        const int lb = launch_cg_ra(st, c->g, cf, c->kshards(), d1, d2, dn, c->cg_x, c->U, f1, f2, face4_recv_U(c),
+                                    c->cg_mass, j, c->sc, c->partials, tb0, tbn, nullptr, ua, c->Uang_face, fsend,
+                                    pbase, tail ? c->tick : nullptr, nparts_pass, c->gsum, sums, red ? 1 : 0,
+                                    c->link_fmt);
+        if (lb) c->cg_link_bytes_last = lb;
     };
     HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
@@ -1115,7 +1173,9 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
             TRY(cg_ra_pass(c));
         } else if (c->cg_fused >= 4) {
             TRY(cg_onepass(c));
+            c->cg_link_bytes_last = 32;
         } else {
+            c->cg_link_bytes_last = 32;
             // the reference's sequence, six launches (src/conjugate_gradient.cpp:31-63):
             // Ad = D D^dag d with fused partials of <d, Ad>; alpha; x, r; beta; d
             double2 *d = c->field(F_D);

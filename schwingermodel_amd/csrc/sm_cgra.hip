@@ -656,13 +656,13 @@ static void ra_go(int xp, int tk, dim3 grid, dim3 block, size_t lds, hipStream_t
     else hipLaunchKernelGGL((cg_ra_kernel<SH, 0, F, RED, UC, 0>), grid, block, lds, s, a);
 }
 
-void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard, const double2 *d1,
-                  const double2 *d2, double2 *dn, double2 *x, const double2 *U, const double2 *f1,
+int launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard, const double2 *d1,
+                 const double2 *d2, double2 *dn, double2 *x, const double2 *U, const double2 *f1,
                   const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
                   int tb0, int tbn, const double2 *prev_partials, const double *Uang, const double *fUang,
                   double2 *fsend, int pbase, unsigned *tick, int ntiles, double2 *gsum, double2 *out3,
                   int red_sums, int link_fmt) {
-    if (tbn <= 0) return;
+    if (tbn <= 0) return 0;
     RAArgs a;
     a.d1 = d1; a.d2 = d2; a.dn = dn; a.x = x; a.U = U;
     a.f1 = f1; a.f2 = f2; a.fU = fU;
@@ -700,19 +700,20 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
     // one kernel per (shards, x pass, fold, scalar mode, link form, tail) combination
     const int f = c.fold >= 2 ? 2 : (c.fold ? 1 : 0);
     const int uc = Uang && f == 2 ? (link_fmt == 2 ? 2 : 1) : 0;  // link codes: with the fused multiply-add fold only
+    const int link_bytes = uc == 2 ? 17 : (uc ? 20 : 32);
     const int tk = tick != nullptr && f == 2;
     if (prev_partials && nshard == 1 && f == 2 && tb0 == 0 && tbn == c.TBk) {
         if (uc == 2) ra_go<0, 1, 2, 2>(xp, 0, grid, block, lds, s, a);
         else if (uc) ra_go<0, 1, 1, 2>(xp, 0, grid, block, lds, s, a);
         else ra_go<0, 1, 0, 2>(xp, 0, grid, block, lds, s, a);
-        return;
+        return link_bytes;
     }
     const bool sh = nshard > 1;
     if (red_sums && sh && f == 2 && tk) {  // t-shards: scalars from pass j-1's all-reduced sums (sc->sumr)
         if (uc == 2) ra_go<1, 2, 2, 2>(xp, tk, grid, block, lds, s, a);
         else if (uc) ra_go<1, 2, 1, 2>(xp, tk, grid, block, lds, s, a);
         else ra_go<1, 2, 0, 2>(xp, tk, grid, block, lds, s, a);
-        return;
+        return link_bytes;
     }
     // one shard with the ticketed tail: odd passes take the tiles in reverse
     // order and flip the march direction, so a pass starts on the rows its
@@ -750,6 +751,27 @@ void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsh
         if (sh) ra_go<1, 0, 0, 0>(xp, 0, grid, block, lds, s, a);
         else ra_go<0, 0, 0, 0>(xp, 0, grid, block, lds, s, a);
     }
+    return link_bytes;
+}
+
+// Resident blocks of the t-shard pass per CU (the edge-rows rule in
+// sm_capi.cpp cg_ra_pass): what the runtime computes for the kernel the
+// sharded pass launches (x-updating, ticketed tail, scalars from the
+// all-reduced sums), at this geometry's block size and LDS ring, so a change
+// of the kernel's register or LDS use moves the rule with it.
+int cg_ra_shard_blocks_per_cu(const CGFusedCfg &c, int link_fmt) {
+    const int block = 64 * c.wpb;
+    const size_t lds = sizeof(double2) * 6 * 64 * c.wpb;
+    int n = 0;
+    hipError_t e;
+    if (link_fmt == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, cg_ra_kernel<1, 1, 2, 2, 2, 1>, block, lds);
+    else if (link_fmt == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, cg_ra_kernel<1, 1, 2, 2, 1, 1>, block, lds);
+    else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, cg_ra_kernel<1, 1, 2, 2, 0, 1>, block, lds);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
 }
 
 // Link codes for the UC passes (sm_linkcode.h) for each of the n links (both

@@ -80,6 +80,7 @@ struct sm_ctx {
     int link_angles = 1;
     int uang_state = 0;
     int link_fmt = 1;               // codes in use: 2 = flag nibbles, one byte per site; 1 = 16-bit flag words
+    int cg_link_bytes_last = 0;     // link bytes per site the last CG pass launched read (sm_cg_link_bytes; 0: none yet)
     // Placement of the buffers the CG pass streams (stream_malloc): 5 = an
     // allocation of >= 2 GiB each with hipDeviceMallocContiguous (the
     // default; plain allocation of that size when the driver has no
@@ -100,6 +101,8 @@ struct sm_ctx {
     hipStream_t comm_stream = nullptr;  // halo exchange overlapped with interior compute (hosted: == stream)
     bool own_comm_stream = false;       // comm_stream created by (and destroyed with) this context
     hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
+    hipEvent_t ev_rccl_in = nullptr, ev_rccl_out = nullptr;  // RCCL operations joining another stream (rccl_enter)
+    int rccl_main = 1;              // every RCCL operation on the main stream (1) or on comm_stream (0); sm_capi.cpp
     // t-shards: the edge block-columns run on the comm stream right after the
     // halo, concurrently with the interior launch on the main stream.
     // recompute-Ad CG on t-shards: the edge launch packs d_j's faces and the
@@ -108,6 +111,7 @@ struct sm_ctx {
     int cg_face_pipe = 1;
     int apply_split = 1;            // t-shard Dirac apply: interior / edge launches around the faces (0: faces first)
     int cg_edge_xchunk = -1;        // -1: by the residency rule (launch_cg_ra_pass)
+    int cg_shard_blocks_per_cu[3] = {-1, -1, -1};  // occupancy of the t-shard pass by link form (-1: not asked yet)
     int n_cu = 256;                 // compute units of the device (residency of a launch)
     long cg_faces_for = -1;
     // recompute-Ad pass: ticketed tail (the pass's last block sums the partials
@@ -117,8 +121,7 @@ struct sm_ctx {
     int cg_flush_sums = 0;          // the pending flush evaluates sc->sumr (t-shards), not partials
     unsigned *tick = nullptr;       // 1 + kMaxTickGroups counters, zeroed at creation
     double2 *gsum = nullptr;        // 3 per group
-    ncclComm_t comm = nullptr;       // main-stream communicator (faces-first halos, ghost links, all-reduces)
-    ncclComm_t comm_side = nullptr;  // comm-stream communicator (overlapped faces), split from comm
+    ncclComm_t comm = nullptr;      // the context's one communicator, driven from one stream (rccl_main)
     bool hosted = false;            // host-callback transport instead of RCCL
     sm_host_transport tr{};
     double *h_face = nullptr;       // pinned: send_lo, send_hi, recv_lo, recv_hi (4 x up to 8Nx doubles)
@@ -206,13 +209,16 @@ int exchange_faces_on(sm_ctx *c, hipStream_t s, double2 *slo, double2 *shi, doub
 // point-to-point operations; the host-staged transport runs them in turn)
 int exchange_faces_multi(sm_ctx *c, hipStream_t s, int n, double2 *const *slo, double2 *const *shi,
                          double2 *const *rlo, double2 *const *rhi, size_t cnt);
-// RCCL contexts hold two communicators over the same ranks, one per stream:
-// operations issued on the comm stream use comm_side, those on the main
-// stream use comm. Each communicator thus sees ONE stream and runs its
-// operations in issue order (the same sequence on every rank) without
-// relying on RCCL to order a communicator's work across streams, and with
-// no cross-stream hand-off (measured ~10 us each through the loopback).
-ncclComm_t comm_for(const sm_ctx *c, hipStream_t s);
+// RCCL contexts hold ONE communicator and issue every RCCL operation on one
+// stream (the main stream, or the comm stream with rccl_main = 0), in host
+// issue order (the same sequence on every rank); an operation requested on
+// another stream s joins s by events before and after (sm_capi.cpp
+// rccl_enter / rccl_leave). n face exchanges in one group:
+// send_up[i] -> up rank's recv_down[i], send_down[i] -> down rank's recv_up[i].
+int rccl_p2p_group(sm_ctx *c, hipStream_t s, int n, const double2 *const *send_up, double2 *const *recv_down,
+                   const double2 *const *send_down, double2 *const *recv_up, size_t cnt);
+// shards 1..P-1 send cnt doubles to shard 0, which receives shard r's at recv + r*cnt
+int rccl_gather_to0(sm_ctx *c, hipStream_t s, const double *send, double *recv, size_t cnt);
 int exchange_faces(sm_ctx *c, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi, size_t cnt);
 int allreduce_dev(sm_ctx *c, double *dev, int n);
 int halo(sm_ctx *c, const double2 *field, int set, int kind, TFaces *f);  // kind: FaceKind

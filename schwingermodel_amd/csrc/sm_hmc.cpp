@@ -61,14 +61,14 @@ int sm_gather_gauge(sm_ctx *c, double *U0, double *U1) {
         HIP_TRY(hipMalloc(&buf, sizeof(double) * cnt * P));
         HIP_TRY(hipMemcpyAsync(buf, c->U, sizeof(double) * cnt, hipMemcpyDeviceToDevice, c->stream));
     }
-    ncclComm_t cm = comm_for(c, c->stream);
-    NCCL_TRY(ncclGroupStart());
-    if (c->shard == 0) {
-        for (int r = 1; r < P; r++) NCCL_TRY(ncclRecv(buf + (size_t)r * 2 * V, cnt, ncclDouble, r, cm, c->stream));
-    } else {
-        NCCL_TRY(ncclSend(c->U, cnt, ncclDouble, 0, cm, c->stream));
+    {
+        const int rc = rccl_gather_to0(c, c->stream, (const double *)c->U, (double *)buf, cnt);
+        if (rc != SM_OK) {
+            (void)hipStreamSynchronize(c->stream);
+            if (buf) (void)hipFree(buf);
+            return rc;
+        }
     }
-    NCCL_TRY(ncclGroupEnd());
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->shard == 0) {
         std::vector<double> h(cnt * P);
@@ -146,7 +146,7 @@ int sm_hmc_run(sm_ctx *c, const sm_hmc_params *p, int hot_start, uint64_t first_
     out->trajectories = ntraj;
     out->cg_iterations = cg_it;
     out->cg_failures = cg_fail;
-    TRY(sm_cg_link_bytes(c, &out->cg_link_bytes));  // the link form the solves ended on, reported
+    TRY(sm_cg_link_bytes(c, &out->cg_link_bytes));  // the link form the last solve's passes read (recorded at launch)
     if (sp_series)
         for (int i = 0; i < Nmeas; i++) sp_series[i] = sp[i];
     if (gs_series)

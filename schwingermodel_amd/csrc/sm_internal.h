@@ -135,13 +135,18 @@ void launch_cg_onepass(hipStream_t s, const Geometry &g, const CGFusedCfg &c, in
 // f2 = d_{j-2} (the previous pass's f1), fU = U.
 constexpr int kRAWaveCols = 56;  // output t-columns per wave (64 lanes - 2x4 halo)
 CGFusedCfg cg_ra_config(const Geometry &g);
-void launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard, const double2 *d1,
-                  const double2 *d2, double2 *dn, double2 *x, const double2 *U, const double2 *f1,
-                  const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
-                  int tb0, int tbn, const double2 *prev_partials = nullptr, const double *Uang = nullptr,
-                  const double *fUang = nullptr, double2 *fsend = nullptr, int pbase = 0,
-                  unsigned *tick = nullptr, int ntiles = 0, double2 *gsum = nullptr, double2 *out3 = nullptr,
-                  int red_sums = 0, int link_fmt = 1);
+// Returns the link bytes per site the launched pass reads: 32 (complex links),
+// 20 (codes, 16-bit flag words) or 17 (codes, packed flag bytes); 0 if nothing launched.
+int launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard, const double2 *d1,
+                 const double2 *d2, double2 *dn, double2 *x, const double2 *U, const double2 *f1,
+                 const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
+                 int tb0, int tbn, const double2 *prev_partials = nullptr, const double *Uang = nullptr,
+                 const double *fUang = nullptr, double2 *fsend = nullptr, int pbase = 0,
+                 unsigned *tick = nullptr, int ntiles = 0, double2 *gsum = nullptr, double2 *out3 = nullptr,
+                 int red_sums = 0, int link_fmt = 1);
+// Resident blocks per CU of the t-shard pass kernel at c's block size (0 if
+// the runtime cannot tell); link_fmt 0 = complex links, 1 / 2 = the code forms.
+int cg_ra_shard_blocks_per_cu(const CGFusedCfg &c, int link_fmt);
 // (tick != null: ticketed tail over the ntiles tiles of every launch of the
 // pass -- the last block forms the scalars in sc, or writes the shard's three
 // sums to out3; tick holds 1 + ceil(ntiles / 64) zeroed counters, gsum 3 per group)

@@ -93,6 +93,17 @@ size_t link_code_bytes(long n) { return (sizeof(double) + sizeof(uint16_t)) * (s
 // initial set and after each buffer's search, and which buffers moved.
 static int g_place_probe = 3;  // candidates per buffer for new contexts (sm_set_placement_probe)
 
+// The streamed buffers in the pass's operand order (d[0..2], x), and the
+// order the probe searches them in: entry i is bit i of place_chosen and of
+// sm_placement_report's mask, with the name sm_placement_buffer_name(i) gives
+// (bench.py reads the names from there). The one table for both.
+static const int kOperandField[4] = {F_D, F_D2, F_R, F_X};
+struct ProbeBuf {
+    int operand;  // index into kOperandField
+    const char *name;
+};
+static const ProbeBuf kProbeOrder[4] = {{3, "x"}, {1, "d1"}, {0, "d0"}, {2, "d2"}};
+
 int placement_probe_default() { return g_place_probe; }
 
 int placement_probe(sm_ctx *c, size_t fb) {
@@ -107,10 +118,9 @@ int placement_probe(sm_ctx *c, size_t fb) {
     // times the real pass (their placement does not move the state)
     if (!c->Uang) HIP_TRY(stream_malloc(c, (void **)&c->Uang, ub));
     HIP_TRY(hipMemsetAsync(c->Uang, 0, ub, c->own_stream));
-    static const int kSlot[4] = {F_D, F_D2, F_R, F_X};  // pass operands d[0..2], x
-    void *cur[4];
+    void *cur[4];  // by operand
     for (int i = 0; i < 4; ++i) {
-        cur[i] = c->fields[kSlot[i]];
+        cur[i] = c->fields[kOperandField[i]];
         HIP_TRY(hipMemsetAsync(cur[i], 0, fb, c->own_stream));
     }
     CGScalars *h = (CGScalars *)c->h_sc;
@@ -169,7 +179,7 @@ int placement_probe(sm_ctx *c, size_t fb) {
             if (!(now < 0.99 * sweep_start)) break;
             sweep_start = now;
         }
-        const int b = (int[]){3, 1, 0, 2}[step % 4];  // x, d1, d0, d2
+        const int b = kProbeOrder[step % 4].operand;
         std::vector<void *> cand;
         int keep = -1;
         double best = now;
@@ -195,7 +205,7 @@ int placement_probe(sm_ctx *c, size_t fb) {
         if (rc == SM_OK && keep >= 0 && best < 0.99 * now) {
             stream_free(c, cur[b]);
             cur[b] = cand[keep];
-            c->fields[kSlot[b]] = (double2 *)cur[b];
+            c->fields[kOperandField[b]] = (double2 *)cur[b];
             now = best;
             c->place_chosen |= 1 << (step % 4);
         }
@@ -228,10 +238,14 @@ int sm_set_placement_probe(int candidates_per_buffer) {
     return SM_OK;
 }
 
+int sm_get_placement_probe(void) { return g_place_probe; }
+
+const char *sm_placement_buffer_name(int i) { return i >= 0 && i < 4 ? kProbeOrder[i].name : nullptr; }
+
 int sm_placement_report(const sm_ctx *c, double *us_per_pass, int *n, int *chosen) {
     if (!c || !n || !chosen) return fail(SM_ERR_ARG, "null argument");
     *n = c->place_n;
-    *chosen = c->place_chosen;  // bit i: buffer i of the search order (x, d1, d0, d2) moved
+    *chosen = c->place_chosen;  // bit i: kProbeOrder[i] moved
     if (us_per_pass)
         for (int k = 0; k < c->place_n; ++k) us_per_pass[k] = c->place_us[k];
     return SM_OK;

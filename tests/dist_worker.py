@@ -562,6 +562,37 @@ def run_big(name, result_path, dist, rank, world):
     dist.destroy_process_group()
 
 
+def run_commworld(name, result_path, dist, rank, world):
+    """mode "commworld" (CPU, gloo): bench.py's comm_world over real ranks with
+    a stand-in context whose sm_comm_info reports the RCCL rank count given
+    per rank in `name` ("<transport>:<n0>,<n1>,..."): the min / max over ranks
+    and the refusal when RCCL's own count differs from WORLD_SIZE."""
+    sys.path.insert(0, REPO)
+    import argparse
+    import bench
+    transport, counts = name.split(":")
+    n = int(counts.split(",")[rank])
+
+    class FakeLattice:
+        def comm_info(self):
+            return transport, n, rank
+
+    sh = argparse.Namespace(L=FakeLattice())
+    args = argparse.Namespace(transport=transport)
+    rt = {"world": world, "rank": rank}
+    try:
+        out = {"ok": bench.comm_world(args, rt, sh)}
+    except SystemExit as e:
+        out = {"refused": str(e)}
+    gathered = [None] * world
+    dist.all_gather_object(gathered, out)
+    if rank == 0:
+        with open(result_path, "w") as f:
+            json.dump({"world": world, "ranks": gathered}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     mode, name, result_path = sys.argv[1], sys.argv[2], sys.argv[3]
     import datetime
@@ -580,6 +611,8 @@ def main():
         return run_angles(name, result_path, dist, rank, world)
     if mode == "big":
         return run_big(name, result_path, dist, rank, world)
+    if mode == "commworld":
+        return run_commworld(name, result_path, dist, rank, world)
     from conftest import bits_equal, load_fixture
     import schwingermodel_amd as sm
     from schwingermodel_amd import dist as smd
@@ -629,6 +662,9 @@ def main():
             local[key] = (out0, out1)
     else:
         ctx, tr = smd.create_hosted_context(Nx, Nt, device=int(os.environ.get("SM_DEVICE", "0")))
+        ci = [ctypes.c_int(-1) for _ in range(3)]
+        sm.check(sm.lib.sm_comm_info(ctx, *(ctypes.byref(v) for v in ci)))
+        local["comm_info"] = tuple(v.value for v in ci)  # host-staged: transport 1, no RCCL world
         sm.check(sm.lib.sm_upload_gauge(ctx, P(U[0]), P(U[1])))
         for key, src, fn in (("ref_Dpsi", psi, 0), ("ref_Ddagchi", chi, 1), ("ref_DDdagpsi", psi, 2)):
             out0, out1 = np.empty(V, complex), np.empty(V, complex)
@@ -668,6 +704,8 @@ def main():
             report["cg_converged"] = [d["cg"][0] for d in gathered]
             report["ref_cg_iters"] = meta["cg_iters"]
             report["dots"] = [list(d["dot"]) for d in gathered]
+        if "comm_info" in local:
+            report["comm_info"] = [list(d["comm_info"]) for d in gathered]
         with open(result_path, "w") as f:
             json.dump(report, f)
     dist.barrier()

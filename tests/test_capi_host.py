@@ -201,9 +201,32 @@ def test_conf_read_truncated_file_fails(tmp_path):
 
 def test_placement_probe_setting_is_validated():
     """sm_set_placement_probe takes 0 (no probe) .. 8 candidates per buffer and
-    rejects anything else without touching the current setting (sm_place.cpp)."""
-    for bad in (-1, 9, 100):
-        assert lib.sm_set_placement_probe(bad) == 1
-        assert b"0..8" in lib.sm_last_error()
-    for ok in (0, 8, 3):  # leaves the default (3) in place
-        assert lib.sm_set_placement_probe(ok) == 0
+    rejects anything else without touching the current setting (sm_place.cpp);
+    sm_get_placement_probe reads it, so the test restores what it found."""
+    before = lib.sm_get_placement_probe()
+    assert 0 <= before <= 8
+    try:
+        for bad in (-1, 9, 100):
+            assert lib.sm_set_placement_probe(bad) == 1
+            assert b"0..8" in lib.sm_last_error()
+            assert lib.sm_get_placement_probe() == before
+        for ok in (0, 8, 5):
+            assert lib.sm_set_placement_probe(ok) == 0
+            assert lib.sm_get_placement_probe() == ok
+    finally:
+        assert lib.sm_set_placement_probe(before) == 0
+
+
+def test_placement_buffer_names():
+    """Bit i of sm_placement_report's mask names buffer i of the probe's
+    search order (one table in sm_place.cpp serves the probe and this call)."""
+    names = [lib.sm_placement_buffer_name(i) for i in range(5)]
+    assert names == [b"x", b"d1", b"d0", b"d2", None]
+    assert lib.sm_placement_buffer_name(-1) is None
+
+
+def test_comm_info_null_context():
+    """sm_comm_info refuses a null context and writes nothing (no GPU needed)."""
+    t, n, r = ctypes.c_int(-7), ctypes.c_int(-7), ctypes.c_int(-7)
+    assert lib.sm_comm_info(None, ctypes.byref(t), ctypes.byref(n), ctypes.byref(r)) == 1
+    assert (t.value, n.value, r.value) == (-7, -7, -7)

@@ -171,6 +171,7 @@ def test_placement_probe_report():
         assert report(L)[0] == 0
     finally:
         L.close()
+    before = sm.lib.sm_get_placement_probe()
     sm.check(sm.lib.sm_set_placement_probe(0))
     try:
         L = sm.Lattice(4096, 2048)
@@ -179,7 +180,7 @@ def test_placement_probe_report():
         finally:
             L.close()
     finally:
-        sm.check(sm.lib.sm_set_placement_probe(3))
+        sm.check(sm.lib.sm_set_placement_probe(before))
     a = solve(sm, 4096, 2048, 0.2374, 0.3, {})
     b = solve(sm, 4096, 2048, 0.2374, 0.3, {"place_probe": 0})
     assert a[0] == b[0] and np.array_equal(a[1].view(np.uint64), b[1].view(np.uint64))

@@ -13,6 +13,24 @@ import pytest
 from distutil import run_world
 
 
+@pytest.mark.parametrize("name,world,expect", [
+    ("rccl:2,2", 2, [2, 2]),            # every communicator holds the job's ranks
+    ("rccl:2,1", 2, None),              # one rank's communicator is alone: refused
+    ("rccl:4,4,4,4", 4, [4, 4]),
+    ("hosted:1,1", 2, [1, 1]),          # host-staged shards: no RCCL world, not refused
+])
+def test_bench_rccl_world_check(tmp_path, name, world, expect):
+    """bench.py reports the RCCL world the communicators themselves hold
+    (sm_comm_info -> ncclCommCount), min and max over the ranks, and refuses to
+    report an RCCL run whose communicators disagree with WORLD_SIZE."""
+    rep = run_world("commworld", name, world, tmp_path, timeout=120)
+    for r in rep["ranks"]:
+        if expect is None:
+            assert "refused" in r and "WORLD_SIZE is 2" in r["refused"], r
+        else:
+            assert r["ok"]["rccl_ranks"] == expect, r
+
+
 @pytest.mark.parametrize("fixture,world", [("l64x64_b2_m0", 2), ("l32x48_b3_m-0p10", 2),
                                            ("l32x48_hot_m0", 4), ("l16x16_b2_m-0p19", 8)])
 def test_sharded_operator_matches_reference(tmp_path, fixture, world):

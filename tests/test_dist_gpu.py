@@ -33,6 +33,8 @@ def test_sharded_gpu_path_matches_reference(tmp_path, fixture, world):
     assert len(set(rep["cg_iters"])) == 1 and abs(rep["cg_iters"][0] - ref) <= max(1, ref // 100)
     assert all(rep["cg_converged"])
     assert len({tuple(d) for d in rep["dots"]}) == 1  # identical global dot on every shard
+    # sm_comm_info: host-staged transport, no RCCL world (bench.py's rccl_ranks = 1)
+    assert rep["comm_info"] == [[1, 1, 0]] * world, rep["comm_info"]
 
 
 @pytest.mark.parametrize("fixture,world", [("l32x48_b3_m-0p10", 4), ("gen:48x1024:0.3:-0.05", 2)])

@@ -90,6 +90,22 @@ CASES = [
 ]
 
 
+def test_loopback_comm_info(sm):
+    """sm_comm_info reads the world from the communicator itself: the loopback
+    is RCCL with ncclCommCount 1 and rank 0; a one-shard context has no
+    transport (bench.py reports these as rccl_ranks)."""
+    loop = sm.Lattice(32, 48, loopback=True)
+    try:
+        assert loop.comm_info() == ("rccl", 1, 0)
+    finally:
+        loop.close()
+    one = sm.Lattice(32, 48)
+    try:
+        assert one.comm_info() == ("none", 1, 0)
+    finally:
+        one.close()
+
+
 @pytest.mark.parametrize("shape,sigma,m0,fixture", CASES, ids=["32x48_fixture", "96x1024", "64x4096"])
 def test_loopback_equals_one_shard(sm, shape, sigma, m0, fixture):
     Nx, Nt = shape
