@@ -112,10 +112,11 @@ int sm_create_loopback(sm_ctx **out, int Nx, int Nt_global, int device, const vo
 int sm_destroy(sm_ctx *ctx);
 /* Launch on a caller stream (a hipStream_t, e.g. torch's current stream);
  * NULL restores the context's own stream. Synchronises the previous stream
- * first. A sharded context issues every RCCL operation with its one
- * communicator on ONE stream, in issue order: this stream (the default), so
- * after the switch they run here; overlapped work on the context's private
- * comm stream joins it by events. */
+ * first. A sharded context has ONE RCCL communicator and orders every RCCL
+ * operation on the GPU after the previous one (events between this stream and
+ * the context's private comm stream, which carries the faces that travel under
+ * an interior launch), in issue order: no two of its RCCL kernels are ever in
+ * flight at once. */
 int sm_set_stream(sm_ctx *ctx, void *hip_stream);
 /* The context's communication world, read from the transport itself:
  * transport 0 = none (one shard), 1 = host-staged (sm_create_hosted),
@@ -147,6 +148,14 @@ int sm_tune_cg(sm_ctx *ctx, int fused, int xchunk);
  * (1, 2 or 4; each wave owns 56 t-columns) and rows marched per block.
  * Values <= 0 keep the current setting. */
 int sm_tune_cg_geometry(sm_ctx *ctx, int waves_per_block, int xchunk);
+/* t-strip blocks of the recompute-Ad pass (one-shard contexts): strip = 1
+ * makes each block's waves (4, or 2 after sm_tune_cg_geometry(ctx, 2, .))
+ * march ONE strip of 64 * waves t-columns (8 of them halo; the stencil stages'
+ * t-hops between its waves go through LDS) instead of one window of 56 owned
+ * columns per wave; balanced = 1 splits x into XB equal chunks of
+ * ~Nx/XB rows instead of xchunk-row chunks. < 0 keeps. SM_ERR_ARG on a
+ * t-shard context. */
+int sm_tune_cg_strip(sm_ctx *ctx, int strip, int balanced);
 /* Compact links in the recompute-Ad CG pass (fused = 5, on by default from
  * 4M sites per shard): the pass reads each link as its smaller component v
  * (one double, exact) plus a 16-bit flag word -- which component v is, the

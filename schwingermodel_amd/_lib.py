@@ -105,6 +105,7 @@ def _load():
         "sm_link_code_check": ([vp, vp, ctypes.POINTER(cd), ctypes.POINTER(ctypes.c_long)], ci),
         "sm_cg_link_bytes": ([vp, ctypes.POINTER(ci)], ci),
         "sm_tune_cg_geometry": ([vp, ci, ci], ci),
+        "sm_tune_cg_strip": ([vp, ci, ci], ci),
         # gauge field / molecular dynamics / HMC
         "sm_download_gauge": ([vp, vp, vp], ci),
         "sm_fill_gauge_dev": ([vp, u64, cd], ci),

@@ -75,66 +75,65 @@ int down_rank(const sm_ctx *c) { return (c->shard - 1 + c->nshard) % c->nshard; 
 // column goes down (the down-neighbour's t = Wt). The face buffers are
 // [plane][x], 4*Nx doubles.
 
-// One communicator, one stream. Every RCCL operation of
-// a context -- face exchanges, scalar all-reduces, the gauge gather -- is
-// issued on ONE stream with the context's single communicator, in the order
-// the host issues them, which is the same on every rank. That stream runs
-// them one after another, so no two RCCL kernels of a context are ever in
-// flight at once and nothing relies on two communicators' kernels being
-// co-resident (round 5 split a second communicator off for the comm stream
-// and argued that they always were). The stream is the main stream
-// (rccl_main = 1, the default) or the private comm stream (0). An operation
-// requested on another stream joins the RCCL stream by events: that stream
-// -> RCCL stream before the operation (rccl_enter), RCCL stream -> that
-// stream after it (rccl_leave). Each such hop costs ~10 us of queue latency
-// on the critical path (RCCL loopback), so the default keeps the
-// critical chain of a CG pass -- interior launch, all-reduce, next pass --
-// on the main stream with no hop, and the pipelined face exchange joins it
-// behind the interior launch.
-static hipStream_t rccl_stream(const sm_ctx *c) { return c->rccl_main ? c->stream : c->comm_stream; }
-
-static int rccl_enter(sm_ctx *c, hipStream_t s) {
-    const hipStream_t r = rccl_stream(c);
-    if (s == r) return SM_OK;
-    HIP_TRY(hipEventRecord(c->ev_rccl_in, s));
-    HIP_TRY(hipStreamWaitEvent(r, c->ev_rccl_in, 0));
+// One communicator, RCCL operations in one total order.
+// Every RCCL operation of a context -- face exchanges, scalar all-reduces, the
+// gauge gather -- goes through the context's single communicator, and each
+// one is ordered on the GPU after the one issued before it, so no two RCCL
+// kernels of a context are ever in flight at once and nothing relies on two
+// communicators' kernels being co-resident (round 5 split a second
+// communicator off for the comm stream and argued that they always were).
+// The operations still run on the stream whose work they belong to (the main
+// stream, or the comm stream for the faces that travel under an interior
+// launch): rccl_order makes an operation on stream s wait for the previous
+// RCCL operation when that one ran on the other stream, by an event recorded
+// there at issue time. Streams that already joined by the launch schedule's
+// own events (rccl_joined) need no extra event. Measured on the RCCL loopback
+// (profiles/r06_b_rccl_stream.jsonl): issuing every operation on ONE
+// stream instead costs 15-31 us per CG iteration at 4096 x 512 .. 2048 (two
+// ~10-us cross-stream hops per pass on the critical path, or the face
+// exchange serialised behind the interior launch).
+static int rccl_order(sm_ctx *c, hipStream_t s) {
+    if (c->rccl_last && c->rccl_last != s && c->rccl_ordered) {
+        // recorded now: the other stream's work so far ends with its last RCCL
+        // operation wherever a schedule issues RCCL there last (the CG pass's
+        // pipelined faces, the apply's overlapped faces)
+        HIP_TRY(hipEventRecord(c->ev_rccl, c->rccl_last));
+        HIP_TRY(hipStreamWaitEvent(s, c->ev_rccl, 0));
+    }
+    c->rccl_last = s;
     return SM_OK;
 }
 
-static int rccl_leave(sm_ctx *c, hipStream_t s) {
-    const hipStream_t r = rccl_stream(c);
-    if (s == r) return SM_OK;
-    HIP_TRY(hipEventRecord(c->ev_rccl_out, r));
-    HIP_TRY(hipStreamWaitEvent(s, c->ev_rccl_out, 0));
-    return SM_OK;
+// `waiter` has just waited for an event recorded on `signaler` after its last
+// RCCL operation: later operations on `waiter` are ordered after it already.
+void rccl_joined(sm_ctx *c, hipStream_t waiter, hipStream_t signaler) {
+    if (c->rccl_last == signaler) c->rccl_last = waiter;
 }
 
 int rccl_p2p_group(sm_ctx *c, hipStream_t s, int n, const double2 *const *send_up, double2 *const *recv_down,
                    const double2 *const *send_down, double2 *const *recv_up, size_t cnt) {
-    TRY(rccl_enter(c, s));
-    const hipStream_t cs = rccl_stream(c);
+    TRY(rccl_order(c, s));
     NCCL_TRY(ncclGroupStart());
     for (int i = 0; i < n; ++i) {
-        NCCL_TRY(ncclSend(send_up[i], cnt, ncclDouble, up_rank(c), c->comm, cs));
-        NCCL_TRY(ncclRecv(recv_down[i], cnt, ncclDouble, down_rank(c), c->comm, cs));
-        NCCL_TRY(ncclSend(send_down[i], cnt, ncclDouble, down_rank(c), c->comm, cs));
-        NCCL_TRY(ncclRecv(recv_up[i], cnt, ncclDouble, up_rank(c), c->comm, cs));
+        NCCL_TRY(ncclSend(send_up[i], cnt, ncclDouble, up_rank(c), c->comm, s));
+        NCCL_TRY(ncclRecv(recv_down[i], cnt, ncclDouble, down_rank(c), c->comm, s));
+        NCCL_TRY(ncclSend(send_down[i], cnt, ncclDouble, down_rank(c), c->comm, s));
+        NCCL_TRY(ncclRecv(recv_up[i], cnt, ncclDouble, up_rank(c), c->comm, s));
     }
     NCCL_TRY(ncclGroupEnd());
-    return rccl_leave(c, s);
+    return SM_OK;
 }
 
 int rccl_gather_to0(sm_ctx *c, hipStream_t s, const double *send, double *recv, size_t cnt) {
-    TRY(rccl_enter(c, s));
-    const hipStream_t cs = rccl_stream(c);
+    TRY(rccl_order(c, s));
     NCCL_TRY(ncclGroupStart());
     if (c->shard == 0) {
-        for (int r = 1; r < c->nshard; r++) NCCL_TRY(ncclRecv(recv + (size_t)r * cnt, cnt, ncclDouble, r, c->comm, cs));
+        for (int r = 1; r < c->nshard; r++) NCCL_TRY(ncclRecv(recv + (size_t)r * cnt, cnt, ncclDouble, r, c->comm, s));
     } else {
-        NCCL_TRY(ncclSend(send, cnt, ncclDouble, 0, c->comm, cs));
+        NCCL_TRY(ncclSend(send, cnt, ncclDouble, 0, c->comm, s));
     }
     NCCL_TRY(ncclGroupEnd());
-    return rccl_leave(c, s);
+    return SM_OK;
 }
 
 int exchange_faces_on(sm_ctx *c, hipStream_t s, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi,
@@ -183,9 +182,9 @@ int allreduce_dev(sm_ctx *c, double *dev, int n) {
         HIP_TRY(hipStreamSynchronize(c->stream));
         return SM_OK;
     }
-    TRY(rccl_enter(c, c->stream));
-    NCCL_TRY(ncclAllReduce(dev, dev, n, ncclDouble, ncclSum, c->comm, rccl_stream(c)));
-    return rccl_leave(c, c->stream);
+    TRY(rccl_order(c, c->stream));
+    NCCL_TRY(ncclAllReduce(dev, dev, n, ncclDouble, ncclSum, c->comm, c->stream));
+    return SM_OK;
 }
 
 // 1-deep t-faces of `field` for the operator `kind` (FaceKind): spin-projected,
@@ -209,9 +208,7 @@ int apply(sm_ctx *c, const double2 *in, double2 *out, double mass, int dagger, c
           double2 *partials, const CGScalars *skip) {
     TFaces f;
     const int TB = (c->g.Wt + c->cfg.bt - 1) / c->cfg.bt;
-    // the split schedule overlaps the faces with the interior launch only when
-    // they travel on the comm stream (rccl_main = 0)
-    if (!c->sharded() || TB < 3 || !c->apply_split || c->rccl_main) {
+    if (!c->sharded() || TB < 3 || !c->apply_split) {
         // one shard, or a narrow t-shard: faces first, then one launch
         TRY(halo(c, in, 0, dagger ? FACE_DDAG : FACE_D, &f));
         launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip);
@@ -224,6 +221,7 @@ int apply(sm_ctx *c, const double2 *in, double2 *out, double mass, int dagger, c
         double2 *rlo = face_buf(c, 0, 2), *rhi = face_buf(c, 0, 3);
         HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
         HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
+        rccl_joined(c, c->comm_stream, c->stream);
         launch_pack_faces_proj(c->comm_stream, c->g, in, c->U, dagger ? FACE_DDAG : FACE_D, slo, shi);
         TRY(exchange_faces_on(c, c->comm_stream, slo, shi, rlo, rhi, (size_t)2 * c->g.Nx));
         f = faces_for(c, in, rlo, rhi);
@@ -233,6 +231,7 @@ int apply(sm_ctx *c, const double2 *in, double2 *out, double mass, int dagger, c
         launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip,
                       1, TB - 2);
         HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+        rccl_joined(c, c->stream, c->comm_stream);
     }
     HIP_TRY(hipGetLastError());
     return SM_OK;
@@ -433,10 +432,14 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //   ra_red_max_blocks=N one shard: redundant scalars up to N blocks
 //   fold=0|1|2          recompute-Ad pass arithmetic (2: fused multiply-adds)
 //   apply_split=0|1     t-shard Dirac apply: interior / edge launches around
-//                       the faces on the comm stream (1; default from Wt 2048,
-//                       with rccl_main=0 only) or faces first, then one launch (0)
-//   rccl_main=0|1       the stream every RCCL operation is issued on: the main
-//                       stream (1, the default) or the private comm stream (0)
+//                       the faces on the comm stream (1; default from Wt 2048)
+//                       or faces first, then one launch (0)
+//   rccl_order=0        no ordering events between RCCL operations on the two
+//                       streams (A/B only: the one communicator then relies on
+//                       RCCL's own ordering)
+//   ra_strip=0|1        recompute-Ad pass: the block's 4 waves share one t-strip
+//                       (one shard; ignored on t-shards)
+//   ra_xbal=0|1         recompute-Ad pass: balanced x-chunks (Nx / XB rows)
 //   ra_remap=0|1        recompute-Ad pass tile order (1: each XCD takes a
 //                       contiguous range of x-adjacent chunks, t-adjacent
 //                       tiles consecutive; 0: round-robin dispatch order)
@@ -491,8 +494,12 @@ static int apply_test_opts(sm_ctx *c) {
             c->racfg.rev_odd = iv;
         } else if (k == "apply_split") {
             c->apply_split = iv ? 1 : 0;
-        } else if (k == "rccl_main") {
-            c->rccl_main = iv ? 1 : 0;
+        } else if (k == "rccl_order") {
+            c->rccl_ordered = iv ? 1 : 0;
+        } else if (k == "ra_strip") {
+            cg_ra_set_strip(c->racfg, c->g, iv);
+        } else if (k == "ra_xbal") {
+            c->racfg.xbal = iv ? 1 : 0;
         } else if (k == "ra_remap") {
             if (iv < 0 || iv > 1) return fail(SM_ERR_ARG, "SM_TEST_OPTS: ra_remap must be 0 or 1");
             c->racfg.remap = iv;
@@ -587,6 +594,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
         delete c;
         return rc;
     }
+    if (c->sharded() && c->racfg.strip) cg_ra_set_strip(c->racfg, c->g, 0);  // t-strips: one-shard contexts only
     while (c->nparts_dslash > kMaxPartials && c->cfg.xchunk < Nx) {
         c->cfg.xchunk = std::min(Nx, 2 * c->cfg.xchunk);
         c->nparts_dslash = dslash_blocks(c->g, c->cfg);
@@ -629,8 +637,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     chk(hipMalloc(&c->faces4, sizeof(double2) * 64 * (size_t)Nx));
     chk(hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming));
     chk(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
-    chk(hipEventCreateWithFlags(&c->ev_rccl_in, hipEventDisableTiming));
-    chk(hipEventCreateWithFlags(&c->ev_rccl_out, hipEventDisableTiming));
+    chk(hipEventCreateWithFlags(&c->ev_rccl, hipEventDisableTiming));
     chk(hipMalloc(&c->partials, sizeof(double2) * 2 * (size_t)np));
     chk(hipMalloc(&c->sums, sizeof(double2) * 4));
     chk(hipMalloc(&c->Fbuf, sizeof(double) * 2 * (size_t)c->g.V));
@@ -713,7 +720,7 @@ int sm_destroy(sm_ctx *c) {
     if (c->h_face) (void)hipHostFree(c->h_face);
     if (c->h_red) (void)hipHostFree(c->h_red);
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
-    for (hipEvent_t ev : {c->ev_ready, c->ev_halo, c->ev_rccl_in, c->ev_rccl_out})
+    for (hipEvent_t ev : {c->ev_ready, c->ev_halo, c->ev_rccl})
         if (ev) (void)hipEventDestroy(ev);
     if (c->comm_stream && c->own_comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -743,14 +750,31 @@ int sm_tune_cg_geometry(sm_ctx *c, int waves_per_block, int xchunk) {
     if (waves_per_block > 0) {
         if (waves_per_block != 1 && waves_per_block != 2 && waves_per_block != 4)
             return fail(SM_ERR_ARG, "waves per block must be 1, 2 or 4");
+        if (f.strip && waves_per_block == 1) return fail(SM_ERR_ARG, "t-strip blocks are 2 or 4 waves");
         f.wpb = waves_per_block;
-        f.TBk = (f.NWT + f.wpb - 1) / f.wpb;
+        cg_ra_set_strip(f, c->g, f.strip);
     }
     if (xchunk > 0) f.xchunk = xchunk;
     f.XB = (c->g.Nx + f.xchunk - 1) / f.xchunk;
     if (3L * cg_fused_blocks(f) > 2L * kMaxPartials) return fail(SM_ERR_ARG, "too many blocks");
     c->racfg = f;
     for (int &n : c->cg_shard_blocks_per_cu) n = -1;  // the block size may have changed
+    return SM_OK;
+}
+
+int sm_tune_cg_strip(sm_ctx *c, int strip, int balanced) {
+    if (!c) return fail(SM_ERR_ARG, "null context");
+    CGFusedCfg f = c->racfg;
+    if (strip >= 0) {
+        if (strip && c->sharded()) return fail(SM_ERR_ARG, "t-strip blocks run on one-shard contexts");
+        if (strip && f.fold < 2) return fail(SM_ERR_ARG, "t-strip blocks take the fused multiply-add pass (fold 2)");
+        cg_ra_set_strip(f, c->g, strip);
+    }
+    if (balanced >= 0) f.xbal = balanced ? 1 : 0;
+    f.XB = (c->g.Nx + f.xchunk - 1) / f.xchunk;
+    if (3L * cg_fused_blocks(f) > 2L * kMaxPartials) return fail(SM_ERR_ARG, "too many blocks");
+    c->racfg = f;
+    for (int &n : c->cg_shard_blocks_per_cu) n = -1;
     return SM_OK;
 }
 
@@ -818,9 +842,10 @@ int sm_bench_stream(sm_ctx *c, int two_reads, long n, const double *a, const dou
 int sm_set_stream(sm_ctx *c, void *s) {
     if (!c) return fail(SM_ERR_ARG, "null context");
     // the old stream's work completes before any is issued on the new one
-    // (with rccl_main the RCCL operations follow it to the new stream, one
-    // stream at a time; else they stay on the comm stream)
+    // (its RCCL operations have completed: the next one needs no ordering
+    // event on it)
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->rccl_last == c->stream) c->rccl_last = nullptr;
     c->stream = s ? (hipStream_t)s : c->own_stream;
     if (c->hosted) c->comm_stream = c->stream;  // hosted contexts run on one stream
     return SM_OK;
@@ -1008,6 +1033,7 @@ static int cg_onepass(sm_ctx *c) {
     const bool split = tb_hi >= tb_lo && tb_hi >= 0;
     HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
+    rccl_joined(c, c->comm_stream, c->stream);
     TRY(halo2_multi(c, c->comm_stream, flds, fcs, 3));
     // edge t-blocks (tb_hi, TBk) and [0, tb_lo), wrapping: one launch, on the
     // comm stream behind the faces, concurrent with the interior launch
@@ -1015,6 +1041,7 @@ static int cg_onepass(sm_ctx *c) {
     HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
     if (split) pass(tb_lo, tb_hi - tb_lo + 1, c->stream);
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+    rccl_joined(c, c->stream, c->comm_stream);
     if (!split) pass(0, fc.TBk, c->stream);
     launch_cg1_local_sum(c->stream, nparts, c->partials, c->sc);
     TRY(allreduce_dev(c, (double *)c->sc->sum3, 6));
@@ -1054,10 +1081,10 @@ static int cg_ra_pass(sm_ctx *c) {
     if (one) {
         // redundant scalars on small grids (partials by pass parity; every block
         // of the next pass evaluates them; sm_cg_iterate flushes the last pass)
-        const bool red = fc.fold >= 2 && nparts <= c->cg_ra_red_max_blocks;
+        const bool red = fc.fold >= 2 && !fc.strip && nparts <= c->cg_ra_red_max_blocks;  // (t-strips: the tail)
         double2 *part = red ? c->partials + (j & 1) * 3 * (size_t)nparts : c->partials;
         const double2 *prev = red ? c->partials + ((j + 1) & 1) * 3 * (size_t)nparts : nullptr;
-        const bool tail = !red && c->cg_tail && fc.fold >= 2 && (nparts + 63) / 64 <= kMaxTickGroups;
+        const bool tail = !red && (c->cg_tail || fc.strip) && fc.fold >= 2 && (nparts + 63) / 64 <= kMaxTickGroups;
         c->cg_link_bytes_last =
             launch_cg_ra(c->stream, c->g, fc, 1, d1, d2, dn, c->cg_x, c->U, nullptr, nullptr, nullptr, c->cg_mass, j,
                          c->sc, part, 0, fc.TBk, prev, ua, nullptr, nullptr, 0, tail ? c->tick : nullptr, nparts,
@@ -1135,6 +1162,7 @@ static int cg_ra_pass(sm_ctx *c) {
     };
     HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
+    rccl_joined(c, c->comm_stream, c->stream);
     // d_{j-1}'s faces: already in slot j & 1 if pass j-1 sent them (pipe)
     if (!(pipe && c->cg_faces_for == j)) TRY(halo4(c, c->comm_stream, d1, f1));
     c->cg_faces_for = -1;
@@ -1150,6 +1178,7 @@ static int cg_ra_pass(sm_ctx *c) {
         c->cg_faces_for = j + 1;
     }
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+    if (!pipe) rccl_joined(c, c->stream, c->comm_stream);  // (pipe: ev_halo precedes the face exchange)
     if (!split) pass(fc, 0, fc.TBk, c->stream, 0, nullptr);
     if (!tail) launch_cg1_local_sum(c->stream, nparts_pass, c->partials, c->sc);
     TRY(allreduce_dev(c, (double *)sums, 6));
@@ -1205,6 +1234,7 @@ int sm_cg_finish(sm_ctx *c, sm_cg_result *res) {
     if (c->cg_active && c->sharded()) {  // the last pass's face exchange (pipelined faces) joins the main stream
         HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
         HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+        rccl_joined(c, c->stream, c->comm_stream);
     }
     if (c->cg_active && c->cg_pending_x == 2) {  // recompute-Ad pass: x rows by parity
         launch_cg_ra_finish_x(c->stream, c->g, c->cg_x, cg_dbuf(c, 0), cg_dbuf(c, 1), cg_dbuf(c, 2), c->sc);

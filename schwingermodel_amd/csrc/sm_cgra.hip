@@ -96,6 +96,7 @@ struct RAArgs {
     // dispatch order of its tiles and the march direction; alt = x-adjacent
     // chunks march in opposite directions
     int flip, alt;
+    int xbal;  // chunk xc covers rows [xc Nx / XB, (xc + 1) Nx / XB) (balanced) instead of xchunk-row chunks
 };
 
 // A link as the UC pass loads it: the code v and its flag word (UC 1), or the
@@ -171,15 +172,59 @@ __device__ __forceinline__ RSrc<T> rsrc(const T *base, const T *face, int c, con
 // sending lane t - 1 is at global t = Nt - 1, i.e. when the sender's SignR is,
 // so the sender's scaled U_t already carries it. 8 fp64 operations less per
 // stage.
-template <int FOLD, int DAG>
+// ST (t-strip blocks, round 6): the block's wpb waves form ONE strip of
+// 64 wpb consecutive lanes (columns), owning 64 wpb - 2 RH of them, instead of
+// wpb independent 64-lane windows of RW = 56 owned columns each. A stage's
+// t-hops between the waves of a strip cross through LDS: lane 0 of each wave
+// publishes its forward-hop combination qf, lane 63 its backward product bp,
+// one barrier, and the neighbour waves' values enter the DPP shifts as the
+// `old` operand (bound_ctrl off: the lane with no source lane in the wave
+// keeps it), so no select is needed. Only the strip's own ends are halo
+// lanes: 8 of 256 lanes instead of 8 of 64 (VALU work per owned site -8 % at
+// 4096 columns: 17 strips x 4 waves against 74 waves a row), and the waves
+// that share a row's lines run on one CU. xs: this stage's slots for this
+// row's parity (the next row of the same parity is behind one more barrier,
+// so one barrier per stage suffices).
+__device__ __forceinline__ double dpp_shr1_keep(double v, double old) {  // lane l <- lane l-1; lane 0 keeps old
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(v), 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), 0x138, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double dpp_shl1_keep(double v, double old) {  // lane l <- lane l+1; lane 63 keeps old
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(v), 0x130, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), 0x130, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ void strip_hop(double2 *xs, double2 qf, double2 bp, double2 &qt, double2 &C) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    if (lane == 0) xs[2 * w] = qf;
+    if (lane == 63) xs[2 * w + 1] = bp;
+    __syncthreads();
+    // the strip's first and last lanes are halo lanes: any finite value
+    const double2 fl = xs[2 * (w > 0 ? w - 1 : 0) + 1];
+    const double2 fr = xs[2 * (w + 1 < nw ? w + 1 : w)];
+    C = make_double2(dpp_shr1_keep(bp.x, fl.x), dpp_shr1_keep(bp.y, fl.y));
+    qt = make_double2(dpp_shl1_keep(qf.x, fr.x), dpp_shl1_keep(qf.y, fr.y));
+}
+
+template <int FOLD, int DAG, int ST = 0>
 __device__ __forceinline__ Sp ra_site(double mass, double sr0, double sl0, const Sp &p, const Sp &pxm, const Sp &pxp,
-                                      double2 ut, double2 ux, double2 uxm) {
+                                      double2 ut, double2 ux, double2 uxm, double2 *xs = nullptr) {
     Sp o;
+    static_assert(!ST || FOLD == 2, "t-strip blocks take the FOLD 2 arithmetic");
     if (FOLD == 2) {  // pre-scaled links: ut = -sr0 U_t / 2, ux = -U_x / 2, uxm = -U_x(x-1) / 2
         const double2 qf = DAG ? cadd(p.a, p.b) : csub(p.a, p.b);
         const double2 qb = DAG ? csub(p.a, p.b) : cadd(p.a, p.b);
-        const double2 C = dpp_shr1(cm<FOLD>(make_double2(ut.x, -ut.y), qb));  // lane t-1's -sl0 conj(U_t) qb / 2
-        const double2 A = cm<FOLD>(ut, dpp_shl1(qf));
+        const double2 bp = cm<FOLD>(make_double2(ut.x, -ut.y), qb);
+        double2 C, qt;  // C: lane t-1's -sl0 conj(U_t) qb / 2; qt: lane t+1's qf
+        if constexpr (ST != 0) {
+            strip_hop(xs, qf, bp, qt, C);
+        } else {
+            C = dpp_shr1(bp);
+            qt = dpp_shl1(qf);
+        }
+        const double2 A = cm<FOLD>(ut, qt);
         const double2 e = make_double2(uxm.x, -uxm.y);
         double2 h0, h1;  // -h / 2
         if (!DAG) {
@@ -242,9 +287,12 @@ void launch_cg_ra_flush_sums(hipStream_t s, CGScalars *sc, long pass) {
 
 // The row march of one tile (the kernel's body; see the header). REV = 1
 // marches the chunk from its last row to its first (phys below).
-template <int SH, int XP, int FOLD, int UC, int REV>
-__device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x0, int xe, double2 alpha,
-                                         double2 beta, double2 alpha2, double2 beta2, double2 *rlds,
+// The lane group owns columns [cbase, cbase + span): a wave (cbase = g RW,
+// span = RW, li = lane) or, ST, the block's t-strip (span = 64 wpb - 2 RH,
+// li = threadIdx.x); its lanes cover cbase - RH + li.
+template <int SH, int XP, int FOLD, int UC, int REV, int ST = 0>
+__device__ __forceinline__ void ra_march(const RAArgs &a, int cbase, int span, int li, int x0, int xe, double2 alpha,
+                                         double2 beta, double2 alpha2, double2 beta2, double2 *rlds, double2 *xl,
                                          double2 &acc_dA, double2 &acc_rA, double2 &acc_n) {
     const int Nx = a.Nx, Wt = a.Wt;
     // The wave owns columns [g RW, g RW + RW): its stores (lanes RH .. RW+RH-1)
@@ -254,8 +302,8 @@ __device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x
     // 153.3 B/site of counter bytes and 2092 against 2205 it/s (round 4,
     // interleaved bench.py, profiles/r04_a_window_shift_ab.jsonl). Partial
     // line writes cost more than a ninth line read through L2.
-    const int c = g * RW - RH + lane;
-    const bool own = lane >= RH && lane < RW + RH && c < Wt;
+    const int c = cbase - RH + li;
+    const bool own = li >= RH && li < span + RH && c < Wt;
     int tg = (a.t0 + c) % a.Ntg;
     if (tg < 0) tg += a.Ntg;
     const double sr0 = tg == a.Ntg - 1 ? -1.0 : 1.0;  // SignR[2n], include/dirac_operator.h:53-55
@@ -292,7 +340,7 @@ __device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x
     // x is read and written by the owned lanes only: the halo lanes load their
     // wave's nearest owned column (no partial line outside the owned ones;
     // 106.6 against 108.0 read B/site, profiles/r05_x_halo_variants_counters.jsonl)
-    const int co = min(max(c, g * RW), g * RW + RW - 1);
+    const int co = min(max(c, cbase), cbase + span - 1);
     const int cx = co < 0 ? 0 : (co >= Wt ? Wt - 1 : co);
     auto wrap = [Nx](int x) { int w = x % Nx; return w < 0 ? w + Nx : w; };
     // REV marches the chunk from its last row to its first: virtual row v
@@ -375,15 +423,16 @@ __device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x
         constexpr int M = decltype(mtag)::value;
         const Sp D4 = Ld;
         const double2 Ut3 = cvt(Lut), Ux3 = cvx(Lux);
+        double2 *const xr = ST ? xl + (y & 1) * 32 : nullptr;  // ST: this row's exchange slots, 8 per stage
         ld1(y + 5, Ld);
         ldu(y + 4, Lut, Lux);
         __builtin_amdgcn_sched_barrier(0);  // keep the next rows' loads issued here
-        const Sp P3 = REV ? ra_site<FOLD, 1>(mass, sr0, sl0, D3, D4, D2, Ut3, Ux2, Ux3)
-                          : ra_site<FOLD, 1>(mass, sr0, sl0, D3, D2, D4, Ut3, Ux3, Ux2);  // S1: T'(y+3)
+        const Sp P3 = REV ? ra_site<FOLD, 1, ST>(mass, sr0, sl0, D3, D4, D2, Ut3, Ux2, Ux3, xr)
+                          : ra_site<FOLD, 1, ST>(mass, sr0, sl0, D3, D2, D4, Ut3, Ux3, Ux2, xr);  // S1: T'(y+3)
         Sp J2 = zs, Q2 = zs;
         if constexpr ((M & 1) != 0) {
-            const Sp A = REV ? ra_site<FOLD, 0>(mass, sr0, sl0, P2, P3, P1, Ut2, Ux1, Ux2)
-                             : ra_site<FOLD, 0>(mass, sr0, sl0, P2, P1, P3, Ut2, Ux2, Ux1);  // S2: Ad_{j-1}(y+2)
+            const Sp A = REV ? ra_site<FOLD, 0, ST>(mass, sr0, sl0, P2, P3, P1, Ut2, Ux1, Ux2, xr + 8)
+                             : ra_site<FOLD, 0, ST>(mass, sr0, sl0, P2, P1, P3, Ut2, Ux2, Ux1, xr + 8);  // S2: Ad_{j-1}(y+2)
             // S3: r_j, d_j at row y+2
             const int xr = y + 2;
             const Sp Q = Mq, X = Mx;
@@ -418,11 +467,11 @@ __device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x
         }
         ld2(y + 3, Mq, Mx);  // consumed above: issued now, used next iteration
         if constexpr ((M & 2) != 0)  // S4: T(y+1)
-            Q2 = REV ? ra_site<FOLD, 1>(mass, sr0, sl0, J1, J2, J0, Ut1, Ux0, Ux1)
-                     : ra_site<FOLD, 1>(mass, sr0, sl0, J1, J0, J2, Ut1, Ux1, Ux0);
+            Q2 = REV ? ra_site<FOLD, 1, ST>(mass, sr0, sl0, J1, J2, J0, Ut1, Ux0, Ux1, xr + 16)
+                     : ra_site<FOLD, 1, ST>(mass, sr0, sl0, J1, J0, J2, Ut1, Ux1, Ux0, xr + 16);
         if constexpr ((M & 4) != 0) {
-            const Sp o = REV ? ra_site<FOLD, 0>(mass, sr0, sl0, Q1, Q2, Q0, Ut0, Uxm, Ux0)
-                             : ra_site<FOLD, 0>(mass, sr0, sl0, Q1, Q0, Q2, Ut0, Ux0, Uxm);  // S5: Ad_j(y)
+            const Sp o = REV ? ra_site<FOLD, 0, ST>(mass, sr0, sl0, Q1, Q2, Q0, Ut0, Uxm, Ux0, xr + 24)
+                             : ra_site<FOLD, 0, ST>(mass, sr0, sl0, Q1, Q0, Q2, Ut0, Ux0, Uxm, xr + 24);  // S5: Ad_j(y)
             if (own) {
                 const Sp R0 = Sp{rlds[(2 * s_r) * blockDim.x + threadIdx.x], rlds[(2 * s_r + 1) * blockDim.x + threadIdx.x]};
                 acc_dA = cfma<FOLD>(acc_dA, J0.a, cconj(o.a));  // dot(d, Ad)
@@ -465,9 +514,10 @@ __device__ __forceinline__ void ra_march(const RAArgs &a, int g, int lane, int x
     for (; y < xe; ++y) step(y, std::integral_constant<int, 7>());
 }
 
-template <int SH, int XP, int FOLD, int RED = 0, int UC = 0, int TK = 0, int REV = 0>
+template <int SH, int XP, int FOLD, int RED = 0, int UC = 0, int TK = 0, int REV = 0, int ST = 0>
 __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
     __shared__ double2 sh[4];
+    __shared__ double2 xl[ST ? 64 : 1];  // ST: t-hop exchange, 2 row parities x 4 stages x 4 waves x (qf, bp)
     extern __shared__ double2 rlds[];  // r_j ring: 3 slots x 2 planes x blockDim (dynamic: sized by waves per block)
     CGScalars *sc = a.sc;
     // Passes 0 and 1 take zero multipliers instead of branches: pass 0 has
@@ -531,20 +581,27 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
         if (tb >= a.TBk) tb -= a.TBk;  // edge block-columns TBk-1 and 0 in one launch
     }
     const int lane = threadIdx.x & 63;
+    // ST: the block's waves share strip tb (every wave marches, in step: the
+    // stages' barriers); else each wave owns its own window g
     const int g = tb * a.wpb + (threadIdx.x >> 6);
-    const int x0 = xc * a.xchunk;
-    const int xe = min(a.Nx, x0 + a.xchunk);
+    const int span = ST ? 64 * a.wpb - 2 * RH : RW;
+    const int cbase = ST ? tb * span : g * RW;
+    const int x0 = a.xbal ? (int)((long)xc * a.Nx / a.XB) : xc * a.xchunk;
+    const int xe = a.xbal ? (int)((long)(xc + 1) * a.Nx / a.XB) : min(a.Nx, x0 + a.xchunk);
     double2 acc_dA = make_double2(0.0, 0.0), acc_rA = make_double2(0.0, 0.0);
     double2 acc_n = make_double2(0.0, 0.0);  // (|r|^2, |Ad|^2)
-    if (g < a.NWT && x0 < xe) {
+    if ((ST || g < a.NWT) && x0 < xe) {  // ST: block-uniform
         // REV 0 / 1: every tile forward / backward; REV 2: per tile, backward
         // iff (x-chunk parity & alt) ^ flip, so x-adjacent chunks march
         // towards their shared boundary rows at the same time (alt = 1)
         const bool back = REV == 1 || (REV == 2 && (((xc & a.alt) ^ a.flip) & 1));
+        const int li = ST ? (int)threadIdx.x : lane;
         if (REV != 0 && back)
-            ra_march<SH, XP, FOLD, UC, 1>(a, g, lane, x0, xe, alpha, beta, alpha2, beta2, rlds, acc_dA, acc_rA, acc_n);
+            ra_march<SH, XP, FOLD, UC, 1, ST>(a, cbase, span, li, x0, xe, alpha, beta, alpha2, beta2, rlds, xl, acc_dA,
+                                              acc_rA, acc_n);
         else if (REV != 1)
-            ra_march<SH, XP, FOLD, UC, 0>(a, g, lane, x0, xe, alpha, beta, alpha2, beta2, rlds, acc_dA, acc_rA, acc_n);
+            ra_march<SH, XP, FOLD, UC, 0, ST>(a, cbase, span, li, x0, xe, alpha, beta, alpha2, beta2, rlds, xl, acc_dA,
+                                              acc_rA, acc_n);
     }
     const double2 s0 = block_sum(acc_dA, sh);
     __syncthreads();
@@ -656,6 +713,20 @@ static void ra_go(int xp, int tk, dim3 grid, dim3 block, size_t lds, hipStream_t
     else hipLaunchKernelGGL((cg_ra_kernel<SH, 0, F, RED, UC, 0>), grid, block, lds, s, a);
 }
 
+template <int UC>
+static void ra_strip(int xp, int rev, dim3 grid, dim3 block, size_t lds, hipStream_t s, const RAArgs &a) {
+    if (rev == 2) {
+        if (xp) hipLaunchKernelGGL((cg_ra_kernel<0, 1, 2, 0, UC, 1, 2, 1>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((cg_ra_kernel<0, 0, 2, 0, UC, 1, 2, 1>), grid, block, lds, s, a);
+    } else if (rev == 1) {
+        if (xp) hipLaunchKernelGGL((cg_ra_kernel<0, 1, 2, 0, UC, 1, 1, 1>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((cg_ra_kernel<0, 0, 2, 0, UC, 1, 1, 1>), grid, block, lds, s, a);
+    } else {
+        if (xp) hipLaunchKernelGGL((cg_ra_kernel<0, 1, 2, 0, UC, 1, 0, 1>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((cg_ra_kernel<0, 0, 2, 0, UC, 1, 0, 1>), grid, block, lds, s, a);
+    }
+}
+
 int launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard, const double2 *d1,
                  const double2 *d2, double2 *dn, double2 *x, const double2 *U, const double2 *f1,
                   const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
@@ -691,6 +762,7 @@ int launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsha
     a.out3 = out3;
     a.flip = 0;
     a.alt = 0;
+    a.xbal = c.xbal;
     const dim3 grid(tbn * c.XB), block(64 * c.wpb);
     const size_t lds = sizeof(double2) * 6 * 64 * c.wpb;  // the r_j ring
     // x takes passes j-1 and j together, on the rows of parity j & 1: every
@@ -702,7 +774,7 @@ int launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsha
     const int uc = Uang && f == 2 ? (link_fmt == 2 ? 2 : 1) : 0;  // link codes: with the fused multiply-add fold only
     const int link_bytes = uc == 2 ? 17 : (uc ? 20 : 32);
     const int tk = tick != nullptr && f == 2;
-    if (prev_partials && nshard == 1 && f == 2 && tb0 == 0 && tbn == c.TBk) {
+    if (prev_partials && nshard == 1 && f == 2 && tb0 == 0 && tbn == c.TBk && !c.strip) {
         if (uc == 2) ra_go<0, 1, 2, 2>(xp, 0, grid, block, lds, s, a);
         else if (uc) ra_go<0, 1, 1, 2>(xp, 0, grid, block, lds, s, a);
         else ra_go<0, 1, 0, 2>(xp, 0, grid, block, lds, s, a);
@@ -733,6 +805,12 @@ int launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsha
         a.flip = (int)(pass & 1);
         a.alt = 1;
     }
+    if (c.strip && !sh && tk && f == 2) {  // t-strip blocks (one shard, ticketed tail)
+        if (uc == 2) ra_strip<2>(xp, rev, grid, block, lds, s, a);
+        else if (uc) ra_strip<1>(xp, rev, grid, block, lds, s, a);
+        else ra_strip<0>(xp, rev, grid, block, lds, s, a);
+        return link_bytes;
+    }
     if (f == 2) {
         if (uc == 2) {
             if (sh) ra_go<1, 0, 2, 2>(xp, tk, grid, block, lds, s, a);
@@ -759,6 +837,17 @@ int launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsha
 // sharded pass launches (x-updating, ticketed tail, scalars from the
 // all-reduced sums), at this geometry's block size and LDS ring, so a change
 // of the kernel's register or LDS use moves the rule with it.
+int cg_ra_set_strip(CGFusedCfg &c, const Geometry &g, int strip) {
+    c.strip = strip ? 1 : 0;
+    if (c.strip) {
+        if (c.wpb != 2 && c.wpb != 4) c.wpb = 4;  // strips of 2 or 4 waves (128 / 256 lanes)
+        c.TBk = (g.Wt + 64 * c.wpb - 2 * RH - 1) / (64 * c.wpb - 2 * RH);
+    } else {
+        c.TBk = (c.NWT + c.wpb - 1) / c.wpb;
+    }
+    return c.TBk;
+}
+
 int cg_ra_shard_blocks_per_cu(const CGFusedCfg &c, int link_fmt) {
     const int block = 64 * c.wpb;
     const size_t lds = sizeof(double2) * 6 * 64 * c.wpb;

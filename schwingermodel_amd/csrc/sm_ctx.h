@@ -101,8 +101,9 @@ struct sm_ctx {
     hipStream_t comm_stream = nullptr;  // halo exchange overlapped with interior compute (hosted: == stream)
     bool own_comm_stream = false;       // comm_stream created by (and destroyed with) this context
     hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
-    hipEvent_t ev_rccl_in = nullptr, ev_rccl_out = nullptr;  // RCCL operations joining another stream (rccl_enter)
-    int rccl_main = 1;              // every RCCL operation on the main stream (1) or on comm_stream (0); sm_capi.cpp
+    hipEvent_t ev_rccl = nullptr;   // orders an RCCL operation after the previous one on the other stream
+    hipStream_t rccl_last = nullptr;  // stream of the last RCCL operation (sm_capi.cpp rccl_order)
+    int rccl_ordered = 1;           // test option rccl_order=0: no ordering events (A/B)
     // t-shards: the edge block-columns run on the comm stream right after the
     // halo, concurrently with the interior launch on the main stream.
     // recompute-Ad CG on t-shards: the edge launch packs d_j's faces and the
@@ -121,7 +122,7 @@ struct sm_ctx {
     int cg_flush_sums = 0;          // the pending flush evaluates sc->sumr (t-shards), not partials
     unsigned *tick = nullptr;       // 1 + kMaxTickGroups counters, zeroed at creation
     double2 *gsum = nullptr;        // 3 per group
-    ncclComm_t comm = nullptr;      // the context's one communicator, driven from one stream (rccl_main)
+    ncclComm_t comm = nullptr;      // the context's one communicator; its operations in one total order
     bool hosted = false;            // host-callback transport instead of RCCL
     sm_host_transport tr{};
     double *h_face = nullptr;       // pinned: send_lo, send_hi, recv_lo, recv_hi (4 x up to 8Nx doubles)
@@ -209,16 +210,18 @@ int exchange_faces_on(sm_ctx *c, hipStream_t s, double2 *slo, double2 *shi, doub
 // point-to-point operations; the host-staged transport runs them in turn)
 int exchange_faces_multi(sm_ctx *c, hipStream_t s, int n, double2 *const *slo, double2 *const *shi,
                          double2 *const *rlo, double2 *const *rhi, size_t cnt);
-// RCCL contexts hold ONE communicator and issue every RCCL operation on one
-// stream (the main stream, or the comm stream with rccl_main = 0), in host
-// issue order (the same sequence on every rank); an operation requested on
-// another stream s joins s by events before and after (sm_capi.cpp
-// rccl_enter / rccl_leave). n face exchanges in one group:
+// RCCL contexts hold ONE communicator; every RCCL operation runs on the
+// stream it is issued on, ordered on the GPU after the previous RCCL
+// operation (sm_capi.cpp rccl_order), in host issue order -- the same
+// sequence on every rank. n face exchanges in one group:
 // send_up[i] -> up rank's recv_down[i], send_down[i] -> down rank's recv_up[i].
 int rccl_p2p_group(sm_ctx *c, hipStream_t s, int n, const double2 *const *send_up, double2 *const *recv_down,
                    const double2 *const *send_down, double2 *const *recv_up, size_t cnt);
 // shards 1..P-1 send cnt doubles to shard 0, which receives shard r's at recv + r*cnt
 int rccl_gather_to0(sm_ctx *c, hipStream_t s, const double *send, double *recv, size_t cnt);
+// waiter has waited for an event recorded on signaler after its last RCCL
+// operation (a launch schedule's own join): no ordering event needed
+void rccl_joined(sm_ctx *c, hipStream_t waiter, hipStream_t signaler);
 int exchange_faces(sm_ctx *c, double2 *slo, double2 *shi, double2 *rlo, double2 *rhi, size_t cnt);
 int allreduce_dev(sm_ctx *c, double *dev, int n);
 int halo(sm_ctx *c, const double2 *field, int set, int kind, TFaces *f);  // kind: FaceKind

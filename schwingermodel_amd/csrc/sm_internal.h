@@ -117,6 +117,8 @@ struct CGFusedCfg {
     int fold = 0;        // sm_cgra.hip: folded hopping-bracket arithmetic (dirac_bracket_folded)
     int wpb = 4;         // sm_cgra.hip: waves per block (1, 2, 4)
     int rev_odd = 0;     // sm_cgra.hip: odd one-shard tail passes march backwards over reversed tiles
+    int strip = 0;       // sm_cgra.hip: the block's 4 waves share one t-strip (one shard; TBk = strips)
+    int xbal = 0;        // sm_cgra.hip: XB balanced chunks of Nx / XB rows instead of xchunk-row chunks
 };
 CGFusedCfg cg_fused_config(const Geometry &g);
 int cg_fused_blocks(const CGFusedCfg &c);
@@ -135,6 +137,9 @@ void launch_cg_onepass(hipStream_t s, const Geometry &g, const CGFusedCfg &c, in
 // f2 = d_{j-2} (the previous pass's f1), fU = U.
 constexpr int kRAWaveCols = 56;  // output t-columns per wave (64 lanes - 2x4 halo)
 CGFusedCfg cg_ra_config(const Geometry &g);
+// t-strip blocks on (strip = 1: 4 waves, 248 owned columns per block) or off;
+// sets wpb / TBk accordingly and returns TBk
+int cg_ra_set_strip(CGFusedCfg &c, const Geometry &g, int strip);
 // Returns the link bytes per site the launched pass reads: 32 (complex links),
 // 20 (codes, 16-bit flag words) or 17 (codes, packed flag bytes); 0 if nothing launched.
 int launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nshard, const double2 *d1,

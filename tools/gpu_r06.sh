@@ -34,6 +34,52 @@ b() {
     > gpurun_out/r06b_tests.log 2>&1
 }
 
+# c: the RCCL total order (one communicator, events between the two streams) against round 5 on the
+#    loopback, twice; the RCCL / t-shard tests; the link-offset drift histogram at config 3
+c() {
+  local L="python -u tools/loopback_probe.py --shapes 4096x512,4096x1024,4096x2048 --iters 200 --rounds 3 --applies 20"
+  for i in 1 2; do
+    timeout -k 10 300 $L > gpurun_out/r06c_order_$i.log 2>&1 &&
+    SM_LIB_PATH=$PWD/tools/ab_libs/libsm_hip_r05.so SM_LIB_AB=1 timeout -k 10 300 $L > gpurun_out/r06c_r05_$i.log 2>&1 || return 1
+  done
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_rccl_loopback_gpu.py \
+    tests/test_dist_gpu.py tests/test_gpu_parity.py -k "loopback or sharded or link" \
+    > gpurun_out/r06c_tests.log 2>&1 &&
+  timeout -k 10 300 python -u tools/link_drift.py --at 0,50,500,2000 > gpurun_out/r06c_drift.jsonl 2>&1
+}
+
+# d: the t-strip CG pass -- its tests, then the strip against the window pass at 4096^2 (one process,
+#    interleaved; chunk lengths for whole dispatch rounds), and the loopback / drift runs of c
+d() {
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_cg_strip_gpu.py \
+    > gpurun_out/r06d_tests.log 2>&1 &&
+  timeout -k 10 400 python3 -u tools/tune_shapes.py 4096x4096:1,64,1 4096x4096:4,64,1,1,0 4096x4096:4,69,1,1,1 \
+    4096x4096:4,32,1,1,0 4096x4096:4,128,1,1,0 4096x4096:4,137,1,1,1 --iters 100 --rounds 4 > gpurun_out/r06d_shapes.log 2>&1 &&
+  c
+}
+
+# e: RCCL ordering events on / off on the loopback; t-strip shapes (4 and 2 waves) at 4096^2 and their
+#    L2 / SQ counters against the window pass
+e() {
+  rm -rf gpurun_out/r06e_*
+  local L="python -u tools/loopback_probe.py --shapes 4096x512,4096x1024 --iters 200 --rounds 3 --applies 5"
+  for i in 1 2; do
+    timeout -k 10 300 $L > gpurun_out/r06e_order_$i.log 2>&1 &&
+    SM_TEST_OPTS=rccl_order=0 timeout -k 10 300 $L > gpurun_out/r06e_noorder_$i.log 2>&1 || return 1
+  done
+  timeout -k 10 400 python3 -u tools/tune_shapes.py 4096x4096:1,64,1 4096x4096:4,69,1,1,1 4096x4096:2,71,1,1,1 \
+    4096x4096:2,141,1,1,1 4096x4096:2,32,1,1,0 4096x4096:4,69,1,1,0 --iters 100 --rounds 4 > gpurun_out/r06e_shapes.log 2>&1 || return 1
+  for g in 1,64,1 4,69,1,1,1 2,71,1,1,1; do
+    local t=${g//,/_}
+    timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum --output-format csv \
+      -d gpurun_out/r06e_tcc_$t -o run -- python3 tools/tune_shapes.py 4096x4096:$g --iters 30 --rounds 1 \
+      > gpurun_out/r06e_tcc_$t.log 2>&1 &&
+    timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU \
+      SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES --output-format csv -d gpurun_out/r06e_sq_$t -o run -- \
+      python3 tools/tune_shapes.py 4096x4096:$g --iters 30 --rounds 1 > gpurun_out/r06e_sq_$t.log 2>&1 || return 1
+  done
+}
+
 # gate: the full GPU gate in natural order, then smoke (tag $1)
 gate() {
   local T=${1:-cur}

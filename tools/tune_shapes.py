@@ -6,7 +6,8 @@ block, link angles) the library's own CG loop (sm_cg_begin / sm_cg_iterate, the
 scalar kernel or redundant scalars included) is timed with events on the ctx
 stream; candidates are interleaved over rounds and the median is printed.
 
-    python tools/tune_shapes.py 4096x512:1,48,0 4096x512:4,32,0 ...
+    python tools/tune_shapes.py 4096x512:1,48,0 4096x512:4,32,0 4096x4096:4,64,1,1,0 ...
+(optional 4th / 5th values: t-strip blocks and balanced x-chunks, sm_tune_cg_strip)
 """
 import argparse
 import ctypes
@@ -21,7 +22,7 @@ sys.path.insert(0, REPO)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("cands", nargs="+", help="NxxNt:wpb,xchunk,angles (wpb/xchunk 0 = the default)")
+    ap.add_argument("cands", nargs="+", help="NxxNt:wpb,xchunk,angles[,strip[,balanced]] (wpb/xchunk 0 = the default)")
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
@@ -52,8 +53,10 @@ def main():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for _ in range(a.rounds):
             for c in cands:
-                wpb, xc, ang = c
+                wpb, xc, ang = c[:3]
+                strip, bal = (tuple(c[3:]) + (0, 0))[:2]
                 L2 = L
+                sm.check(sm.lib.sm_tune_cg_strip(L2.ctx, strip, bal))
                 if wpb or xc:
                     sm.check(sm.lib.sm_tune_cg_geometry(L2.ctx, wpb, xc))
                 sm.check(sm.lib.sm_cg_link_angles(L2.ctx, ang, None))
@@ -66,7 +69,9 @@ def main():
                 res[c].append(e0.elapsed_time(e1) / a.iters)
         for c in cands:
             med = statistics.median(res[c])
-            print(json.dumps({"shape": shp, "wpb": c[0], "xchunk": c[1], "angles": c[2], "ms_per_it": round(med, 5),
+            print(json.dumps({"shape": shp, "wpb": c[0], "xchunk": c[1], "angles": c[2],
+                              "strip": c[3] if len(c) > 3 else 0, "balanced": c[4] if len(c) > 4 else 0,
+                              "ms_per_it": round(med, 5),
                               "ps_per_site": round(med * 1e9 / V, 3), "all": [round(v, 5) for v in res[c]]}),
                   flush=True)
         L.close()
