@@ -427,7 +427,10 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //   cg=0|4|5            CG path (six launches / stored Ad / recompute Ad)
 //   tail=0              scalar kernel instead of the ticketed tail
 //   red_shards=0        t-shards: scalar kernel after the all-reduce
-//   face_pipe=0         t-shards: no pipelined d_j faces
+//   face_pipe=0|1|2     t-shards: d_j's faces packed by a kernel at the next
+//                       pass (0), packed by the edge launch and sent right
+//                       behind it (1), or packed by it and sent at the start of
+//                       the next pass, after the all-reduce (2)
 //   edge_xchunk=N       t-shards: rows per edge block (0: the interior's; -1: rule)
 //   ra_red_max_blocks=N one shard: redundant scalars up to N blocks
 //   fold=0|1|2          recompute-Ad pass arithmetic (2: fused multiply-adds)
@@ -974,6 +977,7 @@ int sm_cg_begin(sm_ctx *c, const double *phi, double *x, double m0, double tol) 
     c->cg_flush_sums = 0;
     c->cg_pending_x = 0;
     c->cg_faces_for = -1;
+    c->cg_faces_packed = 0;
     return SM_OK;
 }
 
@@ -1130,6 +1134,14 @@ static int cg_ra_pass(sm_ctx *c) {
     // 4096x2048 (the interior alone overflows) 0.257 / 0.261-0.271 / 0.260.
     CGFusedCfg ec = fc;
     const bool pipe = split && c->cg_face_pipe && ra_edge_owns_faces(c, fc, tb_lo, tb_hi);
+    // face_pipe 2 (deferred): the edge launch still packs d_j's faces, but
+    // they are SENT at the start of pass j+1, after this pass's all-reduce in
+    // the communicator's order (comm stream behind ev_ready), so the RCCL
+    // operations alternate exchange, all-reduce, exchange, ... and the
+    // launch schedule's own events order them (no ordering event on the
+    // critical path: the all-reduce waits only for the edge launch it needs
+    // anyway, ev_halo, which follows the exchange)
+    const bool deferred = pipe && c->cg_face_pipe == 2;
     int exc = c->cg_edge_xchunk;
     if (exc < 0) {
         const int form = angles ? c->link_fmt : 0;
@@ -1163,22 +1175,33 @@ static int cg_ra_pass(sm_ctx *c) {
     HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
     rccl_joined(c, c->comm_stream, c->stream);
-    // d_{j-1}'s faces: already in slot j & 1 if pass j-1 sent them (pipe)
-    if (!(pipe && c->cg_faces_for == j)) TRY(halo4(c, c->comm_stream, d1, f1));
+    // d_{j-1}'s faces: already in slot j & 1 if pass j-1 sent them (pipe), or
+    // packed by pass j-1's edge launch and sent now (deferred)
+    if (!(pipe && c->cg_faces_for == j)) {
+        TRY(halo4(c, c->comm_stream, d1, f1));
+    } else if (c->cg_faces_packed) {
+        TRY(exchange_faces_on(c, c->comm_stream, face4_send(c, 0), face4_send(c, 1), f1, f1 + (size_t)8 * c->g.Nx,
+                              (size_t)16 * c->g.Nx));
+    }
     c->cg_faces_for = -1;
+    c->cg_faces_packed = 0;
     // edge t-blocks (tb_hi, TBk) and [0, tb_lo), wrapping: one launch on the
     // comm stream behind the faces, concurrent with the interior launch
     if (split) pass(ec, tb_hi + 1, nedge, c->comm_stream, nint * fc.XB, pipe ? face4_send(c, 0) : nullptr);
     HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
     if (split) pass(fc, tb_lo, nint, c->stream, 0, nullptr);
-    if (pipe) {  // d_j's faces into slot (j+1) & 1 (d_{j-2}'s, read by this pass's edge launch above)
+    if (deferred) {  // d_j's faces stay packed until pass j+1
+        c->cg_faces_for = j + 1;
+        c->cg_faces_packed = 1;
+    } else if (pipe) {  // d_j's faces into slot (j+1) & 1 (d_{j-2}'s, read by this pass's edge launch above)
         double2 *r = face4_recv_d(c, j + 1);
         TRY(exchange_faces_on(c, c->comm_stream, face4_send(c, 0), face4_send(c, 1), r, r + (size_t)8 * c->g.Nx,
                               (size_t)16 * c->g.Nx));
         c->cg_faces_for = j + 1;
     }
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
-    if (!pipe) rccl_joined(c, c->stream, c->comm_stream);  // (pipe: ev_halo precedes the face exchange)
+    // (face_pipe 1: ev_halo precedes the face exchange issued after it)
+    if (!pipe || deferred) rccl_joined(c, c->stream, c->comm_stream);
     if (!split) pass(fc, 0, fc.TBk, c->stream, 0, nullptr);
     if (!tail) launch_cg1_local_sum(c->stream, nparts_pass, c->partials, c->sc);
     TRY(allreduce_dev(c, (double *)sums, 6));

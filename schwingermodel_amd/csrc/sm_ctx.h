@@ -115,6 +115,7 @@ struct sm_ctx {
     int cg_shard_blocks_per_cu[3] = {-1, -1, -1};  // occupancy of the t-shard pass by link form (-1: not asked yet)
     int n_cu = 256;                 // compute units of the device (residency of a launch)
     long cg_faces_for = -1;
+    int cg_faces_packed = 0;        // face_pipe 2: cg_faces_for's faces are packed, not yet sent
     // recompute-Ad pass: ticketed tail (the pass's last block sums the partials
     // by groups of 64 and forms the scalars / the shard's sums), no scalar kernel
     int cg_tail = 1;

@@ -82,7 +82,9 @@ size_t link_code_bytes(long n) { return (sizeof(double) + sizeof(uint16_t)) * (s
 // the rest before the next buffer; a sweep that improved the pass by > 1 % is
 // followed by another (at most 3). One sweep reached 430-439 us in 24 of 24
 // trials on one box (r05_b_descent.jsonl) but stayed at 456-460 in 2 of 12 on
-// another, where each of those had still moved (r05_l_probe_sweeps.jsonl). Transient memory:
+// another, where each of those had still moved (r05_l_probe_sweeps.jsonl).
+// Each candidate is timed over 42 passes after a 40-pass warm burst (round 6),
+// the clock state a solve sustains. Transient memory:
 // place_probe allocations of one buffer (3 x 2 GiB at 4096^2), and only while
 // 16 GiB stay free besides them; a candidate that cannot be allocated ends
 // that buffer's search (not the context). Only where the rule applies (fields
@@ -143,14 +145,19 @@ int placement_probe(sm_ctx *c, size_t fb) {
         return fail(SM_ERR_HIP, "placement probe: events");
     }
     long j = 2;
-    // median us per pass of 3 rounds of 6 passes (one warm-up round first)
-    auto time_set = [&](void *const *f, double *us) -> int {
-        constexpr int kRounds = 3, kPasses = 6;
+    // median us per pass of 3 rounds of 14 passes (one warm-up round first),
+    // so every candidate is timed over 42 passes in the clock state of a
+    // sustained solve (timed over 6-pass rounds, the kept
+    // set's time was the burst clock's, 1.9-3 % below what the bench then
+    // sustained); `burst` passes first warm the chip up to that state
+    auto time_set = [&](void *const *f, double *us, int burst) -> int {
+        constexpr int kRounds = 3, kPasses = 14;
         float t[kRounds];
-        for (int r = -1; r < kRounds; ++r) {
+        for (int r = -1 - (burst > 0); r < kRounds; ++r) {
             double2 *d[3] = {(double2 *)f[0], (double2 *)f[1], (double2 *)f[2]};
             if (hipEventRecord(ev[0], c->own_stream) != hipSuccess) return fail(SM_ERR_HIP, "placement probe");
-            for (int p = 0; p < kPasses; ++p, ++j)
+            const int np = r == -2 ? burst : kPasses;
+            for (int p = 0; p < np; ++p, ++j)
                 launch_cg_ra(c->own_stream, g, c->racfg, 1, d[(j + 2) % 3], d[(j + 1) % 3], d[j % 3], (double2 *)f[3],
                              nullptr, nullptr, nullptr, nullptr, 1.94, j, c->sc, c->partials, 0, c->racfg.TBk,
                              nullptr, c->Uang, nullptr, nullptr, 0, tail ? c->tick : nullptr, nparts, c->gsum,
@@ -159,14 +166,14 @@ int placement_probe(sm_ctx *c, size_t fb) {
             if (hipEventRecord(ev[1], c->own_stream) != hipSuccess || hipEventSynchronize(ev[1]) != hipSuccess ||
                 hipEventElapsedTime(&ms, ev[0], ev[1]) != hipSuccess || hipGetLastError() != hipSuccess)
                 return fail(SM_ERR_HIP, "placement probe timing");
-            if (r >= 0) t[r] = ms * 1000.f / kPasses;
+            if (r >= 0) t[r] = ms * 1000.f / np;
         }
         std::sort(t, t + kRounds);
         *us = t[kRounds / 2];
         return SM_OK;
     };
     double now = 0.0;
-    int rc = time_set(cur, &now);
+    int rc = time_set(cur, &now, 40);
     c->place_us[c->place_n++] = now;
     const size_t bytes = stream_alloc_bytes(fb);
     // sweeps over the four buffers, another one while the last improved the
@@ -199,7 +206,7 @@ int placement_probe(sm_ctx *c, size_t fb) {
             void *trial[4] = {cur[0], cur[1], cur[2], cur[3]};
             trial[b] = p;
             double us = 0.0;
-            rc = time_set(trial, &us);
+            rc = time_set(trial, &us, 0);
             if (rc == SM_OK && us < best) best = us, keep = (int)cand.size() - 1;
         }
         if (rc == SM_OK && keep >= 0 && best < 0.99 * now) {

@@ -79,9 +79,12 @@ def test_even_odd_tail_matches_scalar_kernel(sm):
     {},
     {"red_shards": 0},
     {"face_pipe": 0},
+    {"face_pipe": 1},
+    {"face_pipe": 2},
+    {"face_pipe": 1, "rccl_order": 0},
     {"edge_xchunk": 0},
     {"tail": 0},
-], ids=["default", "no_red", "no_pipe", "long_edge", "no_tail"])
+], ids=["default", "no_red", "no_pipe", "pipe_behind_edge", "pipe_deferred", "pipe_unordered", "long_edge", "no_tail"])
 def test_tshard_schedules_agree(sm, opts):
     old = {"face_pipe": 0, "red_shards": 0, "tail": 0}
     agree(solve(sm, 64, 4096, 0.2374, -0.06, opts, loopback=True),

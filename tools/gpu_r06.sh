@@ -80,6 +80,31 @@ e() {
   done
 }
 
+# f: chunk alignment (power-of-two vs balanced chunks) for the window and strip passes at 4096^2;
+#    the t-shard edge rows per block under the RCCL ordering events on the loopback
+f() {
+  timeout -k 10 500 python3 -u tools/tune_shapes.py 4096x4096:1,64,1 4096x4096:1,69,1,0,1 4096x4096:4,69,1,1,1 \
+    4096x4096:4,64,1,1,0 4096x4096:2,64,1,1,0 4096x4096:4,32,1,1,0 4096x4096:1,32,1 4096x4096:1,128,1 \
+    --iters 100 --rounds 4 > gpurun_out/r06f_shapes.log 2>&1 || return 1
+  local L="python -u tools/loopback_probe.py --shapes 4096x512,4096x1024 --iters 200 --rounds 3 --applies 5"
+  for e in 16 8 12 24; do
+    SM_TEST_OPTS=edge_xchunk=$e timeout -k 10 300 $L > gpurun_out/r06f_edge$e.log 2>&1 || return 1
+  done
+}
+
+# g: t-shard face schedules on the loopback (pipelined behind the edge launch with ordering events, the same
+#    without them, deferred to the next pass), and their tests
+g() {
+  local L="python -u tools/loopback_probe.py --shapes 4096x512,4096x1024,4096x2048 --iters 200 --rounds 3 --applies 5"
+  for i in 1 2; do
+    SM_TEST_OPTS=face_pipe=1 timeout -k 10 300 $L > gpurun_out/r06g_pipe1_$i.log 2>&1 &&
+    SM_TEST_OPTS=face_pipe=2 timeout -k 10 300 $L > gpurun_out/r06g_pipe2_$i.log 2>&1 &&
+    SM_TEST_OPTS=face_pipe=1,rccl_order=0 timeout -k 10 300 $L > gpurun_out/r06g_pipe1_noorder_$i.log 2>&1 || return 1
+  done
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_cg_paths_gpu.py \
+    tests/test_rccl_loopback_gpu.py -k "tshard or loopback" > gpurun_out/r06g_tests.log 2>&1
+}
+
 # gate: the full GPU gate in natural order, then smoke (tag $1)
 gate() {
   local T=${1:-cur}
