@@ -90,8 +90,8 @@ size_t link_code_bytes(long n) { return (sizeof(double) + sizeof(uint16_t)) * (s
 // that buffer's search (not the context). Only where the rule applies (fields
 // >= 256 MiB, the recompute-Ad pass with fused multiply-adds; not on
 // host-staged contexts, where shard processes share one GPU). The timings run
-// on zero data (NaN iterates), so the kept buffers are zeroed again and the
-// scalars and tickets reset. sm_placement_report returns the pass time of the
+// on drawn data (a field, its codes, Gaussian CG directions), so the kept
+// buffers, U and the codes are zeroed again and the scalars and tickets reset. sm_placement_report returns the pass time of the
 // initial set and after each buffer's search, and which buffers moved.
 static int g_place_probe = 3;  // candidates per buffer for new contexts (sm_set_placement_probe)
 
@@ -119,20 +119,24 @@ int placement_probe(sm_ctx *c, size_t fb) {
     // the link codes are the pass's fifth stream: allocated here so the probe
     // times the real pass (their placement does not move the state)
     if (!c->Uang) HIP_TRY(stream_malloc(c, (void **)&c->Uang, ub));
-    HIP_TRY(hipMemsetAsync(c->Uang, 0, ub, c->own_stream));
+    Geometry g = c->g;
+    g.t0 = 0;
+    g.Ntg = g.Wt;  // one shard's pass over this shard's streams
+    // The pass is timed on REAL data (round 6): a config-3-like field drawn
+    // into the context's U (the caller's upload replaces it) and its packed
+    // codes, and a CG started from complex-Gaussian directions and x, redrawn
+    // before every set is timed. Round 5 timed zero / NaN data, whose lower
+    // switching power let the capped board clock higher: the kept set's time
+    // came out 2-3 % below the pass time the bench then sustained.
+    launch_draw_gauge(c->own_stream, g, 0x9a1ce5eedull, 0.2374, c->U);
+    (void)launch_link_codes(c->own_stream, 2 * c->g.V, c->U, c->Uang, c->partials);
+    launch_link_nibbles(c->own_stream, c->g.V, c->Uang);
     void *cur[4];  // by operand
-    for (int i = 0; i < 4; ++i) {
-        cur[i] = c->fields[kOperandField[i]];
-        HIP_TRY(hipMemsetAsync(cur[i], 0, fb, c->own_stream));
-    }
+    for (int i = 0; i < 4; ++i) cur[i] = c->fields[kOperandField[i]];
     CGScalars *h = (CGScalars *)c->h_sc;
     memset(h, 0, sizeof(CGScalars));
     h->max_iter = 1 << 30;
     h->phi_norm = 1.0;
-    HIP_TRY(hipMemcpyAsync(c->sc, h, sizeof(CGScalars), hipMemcpyHostToDevice, c->own_stream));
-    Geometry g = c->g;
-    g.t0 = 0;
-    g.Ntg = g.Wt;  // one shard's pass over this shard's streams
     const int nparts = cg_fused_blocks(c->racfg);
     const bool tail = (nparts + 63) / 64 <= kMaxTickGroups;
     hipEvent_t ev[2] = {nullptr, nullptr};
@@ -145,6 +149,15 @@ int placement_probe(sm_ctx *c, size_t fb) {
         return fail(SM_ERR_HIP, "placement probe: events");
     }
     long j = 2;
+    // a fresh CG state on the set: d_{j-1}, d_{j-2}, d_j's buffer and x
+    // Gaussian, zero scalars (pass j = 2 then runs r = d_{j-1}: a CG step)
+    auto fresh = [&](void *const *f) -> int {
+        for (int i = 0; i < 4; ++i) launch_draw_source(c->own_stream, g, 0x5eed0000ull + i, (double2 *)f[i]);
+        if (hipMemcpyAsync(c->sc, h, sizeof(CGScalars), hipMemcpyHostToDevice, c->own_stream) != hipSuccess)
+            return fail(SM_ERR_HIP, "placement probe: scalars");
+        j = 2;
+        return SM_OK;
+    };
     // median us per pass of 3 rounds of 14 passes (one warm-up round first),
     // so every candidate is timed over 42 passes in the clock state of a
     // sustained solve (timed over 6-pass rounds, the kept
@@ -153,6 +166,7 @@ int placement_probe(sm_ctx *c, size_t fb) {
     auto time_set = [&](void *const *f, double *us, int burst) -> int {
         constexpr int kRounds = 3, kPasses = 14;
         float t[kRounds];
+        if (int rc = fresh(f); rc != SM_OK) return rc;
         for (int r = -1 - (burst > 0); r < kRounds; ++r) {
             double2 *d[3] = {(double2 *)f[0], (double2 *)f[1], (double2 *)f[2]};
             if (hipEventRecord(ev[0], c->own_stream) != hipSuccess) return fail(SM_ERR_HIP, "placement probe");
@@ -199,10 +213,6 @@ int placement_probe(sm_ctx *c, size_t fb) {
                 break;
             }
             cand.push_back(p);
-            if (hipMemsetAsync(p, 0, fb, c->own_stream) != hipSuccess) {
-                rc = fail(SM_ERR_HIP, "placement probe: memset");
-                break;
-            }
             void *trial[4] = {cur[0], cur[1], cur[2], cur[3]};
             trial[b] = p;
             double us = 0.0;
@@ -222,10 +232,11 @@ int placement_probe(sm_ctx *c, size_t fb) {
     }
     drop_events();
     if (rc != SM_OK) return rc;
-    // the probe's iterates are NaN (0/0 scalars on zero data): clear them, as
-    // a fresh allocation would be (pass 0 weights d_{-2} by a zero multiplier)
+    // clear the probe's iterates, field and codes, as fresh allocations would be
+    // (pass 0 weights d_{-2} by a zero multiplier; the caller uploads U)
     for (void *p : cur) HIP_TRY(hipMemsetAsync(p, 0, fb, c->own_stream));
     HIP_TRY(hipMemsetAsync(c->Uang, 0, ub, c->own_stream));
+    HIP_TRY(hipMemsetAsync(c->U, 0, sizeof(double2) * 2 * (size_t)c->g.V, c->own_stream));
     HIP_TRY(hipMemsetAsync(c->sc, 0, sizeof(CGScalars), c->own_stream));
     HIP_TRY(hipMemsetAsync(c->tick, 0, sizeof(unsigned) * (1 + kMaxTickGroups), c->own_stream));
     HIP_TRY(hipStreamSynchronize(c->own_stream));

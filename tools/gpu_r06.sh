@@ -105,6 +105,15 @@ g() {
     tests/test_rccl_loopback_gpu.py -k "tshard or loopback" > gpurun_out/r06g_tests.log 2>&1
 }
 
+# h: the full GPU gate and smoke, then the driver's bench command twice and the 200-step default
+#    (probe kept time against the sustained pass)
+h() {
+  gate h &&
+  timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r06h_bench_driver1.log 2>&1 &&
+  timeout -k 10 400 python3 bench.py > gpurun_out/r06h_bench200.log 2>&1 &&
+  timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r06h_bench_driver2.log 2>&1
+}
+
 # gate: the full GPU gate in natural order, then smoke (tag $1)
 gate() {
   local T=${1:-cur}
