@@ -1123,8 +1123,9 @@ static int cg_ra_pass(sm_ctx *c) {
     // them on the comm stream, under the interior launch and the scalar step;
     // the edge launch marches short chunks so it ends long before the interior
     // one (its blocks otherwise run as long as the whole pass, AFTER the faces).
-    // Edge rows per block: 16, or 32 where only the longer chunks let the
-    // edge tiles join the interior ones in one residency round (the resident
+    // Edge rows per block: 8 where those tiles still join the interior ones
+    // in one residency round, else 16, or 32 where only the longer chunks let
+    // the edge tiles join the interior ones in one residency round (the resident
     // blocks per CU come from the runtime's occupancy of the launched kernel,
     // cg_ra_shard_blocks_per_cu: 8 one-wave blocks at 2 waves per SIMD for
     // the round-5 kernel). RCCL loopback, ms per
@@ -1149,7 +1150,10 @@ static int cg_ra_pass(sm_ctx *c) {
         if (per_cu < 0) per_cu = cg_ra_shard_blocks_per_cu(fc, form);
         const long slots = (long)c->n_cu * (per_cu > 0 ? per_cu : 8 / fc.wpb), inner = (long)nint * fc.XB;
         auto tiles = [&](int r) { return inner + (long)nedge * ((c->g.Nx + r - 1) / r); };
-        exc = tiles(16) > slots && tiles(32) <= slots ? 32 : 16;
+        // 8 rows where even those tiles join the interior ones in one round
+        // (round 6, with the RCCL order: 4096x512 0.0951 against 0.0987 ms
+        // per iteration for 16, profiles/r06_f_chunk_alignment_edge_rows.jsonl)
+        exc = tiles(8) <= slots ? 8 : (tiles(16) > slots && tiles(32) <= slots ? 32 : 16);
     }
     if (pipe && exc > 0 && exc < fc.xchunk) {
         ec.xchunk = exc;

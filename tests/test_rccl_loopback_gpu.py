@@ -231,11 +231,12 @@ def test_loopback_apply_modes_bitwise(sm, shape, sigma, split):
         assert bits_equal(g, r), (split, k)
 
 
-@pytest.mark.parametrize("shape", [(4096, 1024), (4096, 512)], ids=["4096x1024_edge32", "4096x512_edge16"])
+@pytest.mark.parametrize("shape", [(4096, 1024), (4096, 512)], ids=["4096x1024_edge32", "4096x512_edge8"])
 def test_loopback_cg_edge_rows_rule(sm, shape):
-    """The t-shard CG pass's edge launch marches 32-row chunks where only those
-    let its tiles join the interior ones in one residency round (4096 x 1024)
-    and 16 elsewhere (sm_capi.cpp cg_ra_pass): the loopback solve equals the
+    """The t-shard CG pass's edge launch marches 8-row chunks where even those
+    let its tiles join the interior ones in one residency round (4096 x 512),
+    32 where only those do (4096 x 1024) and 16 elsewhere (sm_capi.cpp
+    cg_ra_pass): the loopback solve equals the
     one-shard solve (iterations within one, x to 1e-12) either way, and forcing the
     other chunk length (test option edge_xchunk) changes only the partial
     sums' partition."""
@@ -245,7 +246,7 @@ def test_loopback_cg_edge_rows_rule(sm, shape):
     U, psi, _, _ = fields(sm, Nx, Nt, 0.2374)
     h = lambda a: (ptr(a[:2 * S]), ptr(a[2 * S:]))  # noqa: E731
     out = {}
-    other = 16 if Nt == 1024 else 32
+    other = 16
     for name, kw, opts in (("one", {}, {}), ("loop", {"loopback": True}, {}),
                            ("loop_other", {"loopback": True}, {"edge_xchunk": other})):
         with opts_env(**opts):

@@ -114,6 +114,36 @@ h() {
   timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r06h_bench_driver2.log 2>&1
 }
 
+# i: the placement probe on drawn data -- its tests, ten contexts in one process, the driver's bench command
+#    three times (probe kept time against the sustained pass)
+i() {
+  timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_cg_paths_gpu.py \
+    -k placement > gpurun_out/r06i_tests.log 2>&1 &&
+  timeout -k 10 300 python -u tools/probe_trials.py --n 10 --hold 5 > gpurun_out/r06i_trials.jsonl 2>&1 || return 1
+  for k in 1 2 3; do
+    timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 >> gpurun_out/r06i_bench.jsonl 2>> gpurun_out/r06i_bench.err || return 1
+  done
+}
+
+# fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
+#      passes, the loopback, and the placement probe over 10 contexts
+fin() {
+  local T=${1:-cur}
+  rm -rf gpurun_out/prof_stats_$T gpurun_out/prof_fetch_$T gpurun_out/prof_write_$T
+  local P="python3 bench.py --steps 10 --warmup 2 --applies 10 --no-cpu-baseline --no-weak --evolved-trajectories 0"
+  python3 -c "import schwingermodel_amd as s; print(s.lib.sm_build_id().decode())" > gpurun_out/build_id_$T.txt &&
+  timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver_$T.log 2>&1 &&
+  timeout -k 10 400 python3 bench.py > gpurun_out/bench_$T.log 2>&1 &&
+  timeout -k 10 300 python3 bench.py --gpus 2 --transport hosted --steps 50 --warmup 10 --no-weak > gpurun_out/bench2_$T.log 2>&1 &&
+  timeout -k 10 300 python3 bench.py --config 5 > gpurun_out/bench_c5_$T.log 2>&1 &&
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_stats_$T -o run -- python3 bench.py --steps 200 --warmup 20 --applies 20 --no-cpu-baseline --no-weak --evolved-trajectories 0 > gpurun_out/prof_stats_$T.log 2>&1 &&
+  python3 tools/step_gap.py gpurun_out/prof_stats_$T/run_kernel_trace.csv --last 200 > gpurun_out/step_gap_$T.log 2>&1 &&
+  timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch_$T -o run -- $P > gpurun_out/prof_fetch_$T.log 2>&1 &&
+  timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write_$T -o run -- $P > gpurun_out/prof_write_$T.log 2>&1 &&
+  timeout -k 10 300 python -u tools/loopback_probe.py --shapes 4096x512,4096x1024,4096x2048,4096x4096 --iters 100 --rounds 2 > gpurun_out/loopback_$T.log 2>&1 &&
+  timeout -k 10 300 python -u tools/probe_trials.py --n 10 --hold 5 > gpurun_out/probe_trials_$T.jsonl 2>&1
+}
+
 # gate: the full GPU gate in natural order, then smoke (tag $1)
 gate() {
   local T=${1:-cur}
