@@ -458,6 +458,47 @@ def test_link_codes_device_decode_matches_stored_links(sm):
         sm.check(sm.lib.sm_cg_link_codes(L.ctx, 1, None))
 
 
+def test_link_bytes_recorded_at_launch(sm):
+    """sm_cg_link_bytes reports what the last CG pass launched read (ADVICE
+    r05): 0 before any pass, the packed codes' 17 after a solve on a fresh
+    field, STILL 17 after a gauge upload that no solve has used yet (a field
+    with one link off the circle, which the next solve reads as complex links),
+    then 32 after that solve, and 32 for the stored-Ad pass."""
+    Nx, Nt = 256, 256
+    S = Nx * Nt
+    L = sm.init(Nx, Nt)
+    U, psi = sm.spinor(S), sm.spinor(S)
+    P = lambda a: a.ctypes.data  # noqa: E731
+    sm.lib.sm_fill_gauge(4321, 0.2374, Nt, 0, Nx, 0, Nt, P(U.mu0), P(U.mu1))
+    sm.lib.sm_fill_spinor(5678, Nt, 0, Nx, 0, Nt, P(psi.mu0), P(psi.mu1))
+
+    def link_bytes():
+        b = ctypes.c_int(-1)
+        sm.check(sm.lib.sm_cg_link_bytes(L.ctx, ctypes.byref(b)))
+        return b.value
+
+    assert link_bytes() == 0
+    sm.check(sm.lib.sm_tune_cg(L.ctx, 5, 0))
+    sm.check(sm.lib.sm_cg_link_codes(L.ctx, 1, None))
+    try:
+        x = sm.spinor(S)
+        assert sm.conjugate_gradient(U, psi, x, -0.1) == 1
+        assert link_bytes() == 17
+        far = U.copy()
+        far.mu0[77] *= 1.0 + 1e-9
+        L.upload_gauge(far)
+        assert link_bytes() == 17  # no pass has read the new field yet
+        x = sm.spinor(S)
+        assert sm.conjugate_gradient(far, psi, x, -0.1) == 1
+        assert link_bytes() == 32
+        sm.check(sm.lib.sm_tune_cg(L.ctx, 4, 0))
+        x = sm.spinor(S)
+        assert sm.conjugate_gradient(U, psi, x, -0.1) == 1
+        assert link_bytes() == 32
+    finally:
+        sm.check(sm.lib.sm_cg_link_codes(L.ctx, 1, None))
+
+
 @pytest.mark.parametrize("drift", [False, True], ids=["packed_flags", "flag_words"])
 def test_link_codes_tshard_path_bitwise(sm, drift):
     """The t-shard form of the code pass (faces of codes and flags through
