@@ -125,6 +125,20 @@ i() {
   done
 }
 
+# j: device-initiated transport feasibility (tools/peer_probe: one process against itself, two processes
+#    on one GPU over IPC-opened uncached / coarse regions), then RCCL launch settings on the loopback
+j() {
+  local P="timeout -k 5 90 tools/peer_probe"
+  $P loop 2000 8192 1 > gpurun_out/r06j_peer.jsonl 2>&1 &&
+  $P ipc 2000 8192 1 >> gpurun_out/r06j_peer.jsonl 2>&1 &&
+  $P ipc 2000 8192 0 >> gpurun_out/r06j_peer.jsonl 2>&1 &&
+  $P ipc 2000 16 1 >> gpurun_out/r06j_peer.jsonl 2>&1 || return 1
+  local L="python -u tools/loopback_probe.py --shapes 4096x512,4096x1024 --iters 200 --rounds 2 --applies 20"
+  timeout -k 10 300 $L > gpurun_out/r06j_default.log 2>&1 &&
+  NCCL_GRAPH_MIXING_SUPPORT=0 timeout -k 10 300 $L > gpurun_out/r06j_nomix.log 2>&1 &&
+  NCCL_LAUNCH_MODE=GROUP timeout -k 10 300 $L > gpurun_out/r06j_group.log 2>&1
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
