@@ -109,6 +109,34 @@ int sm_create_hosted(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard,
  * unique_id (sm_comm_unique_id). The results equal sm_create's one-shard
  * context; it exists so the RCCL data path can be verified on a single GPU. */
 int sm_create_loopback(sm_ctx **out, int Nx, int Nt_global, int device, const void *unique_id);
+/* Device-initiated shard transport ("peer", round 6; replaces the halo
+ * MPI_Send/MPI_Recv of src/dirac_operator.cpp:66-88 and the dot's
+ * MPI_Allreduce of include/variables.h:190 like the RCCL path does, without
+ * RCCL). Each shard owns one region of uncached device memory; kernels store
+ * faces and scalar sums straight into the neighbours' / every shard's region
+ * over xGMI and publish sequence flags there; the receiving kernel waits on
+ * the flags in its own region (one waiting thread, a time limit on every
+ * wait). The recompute-Ad CG pass writes d_j's faces into the neighbours'
+ * rings and all-reduces its sums in its own last block, so a pass is ONE
+ * launch on ONE stream. Works between processes on one GPU as well (the
+ * one-GPU tests) and needs no RCCL communicator.
+ * Two steps, with any host-side all-gather in between:
+ *   sm_create_peer writes this shard's region handle (sm_peer_handle_bytes()
+ *   bytes) to handle_out; sm_peer_connect takes the nshard handles in rank
+ *   order (handle_bytes_each apart), maps the others' regions, and checks the
+ *   world with one all-reduce. The context is unusable for sharded work until
+ *   then. */
+int sm_peer_handle_bytes(void);
+int sm_create_peer(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device, void *handle_out,
+                   int handle_bytes);
+int sm_peer_connect(sm_ctx *ctx, const void *handles, int handle_bytes_each);
+/* One shard through the peer transport's t-shard path, its own neighbour on
+ * both sides (the peer counterpart of sm_create_loopback). */
+int sm_create_peer_loopback(sm_ctx **out, int Nx, int Nt_global, int device);
+/* Synchronises the context's stream; SM_ERR_RCCL if a peer-transport wait
+ * timed out (*timed_out_seq = its sequence number, 0 if none; may be NULL).
+ * sm_cg_finish checks it too. SM_OK on other transports. */
+int sm_peer_status(sm_ctx *ctx, unsigned long long *timed_out_seq);
 int sm_destroy(sm_ctx *ctx);
 /* Launch on a caller stream (a hipStream_t, e.g. torch's current stream);
  * NULL restores the context's own stream. Synchronises the previous stream
@@ -120,7 +148,9 @@ int sm_destroy(sm_ctx *ctx);
 int sm_set_stream(sm_ctx *ctx, void *hip_stream);
 /* The context's communication world, read from the transport itself:
  * transport 0 = none (one shard), 1 = host-staged (sm_create_hosted),
- * 2 = RCCL (sm_create with nshard > 1, or sm_create_loopback); *nranks /
+ * 2 = RCCL (sm_create with nshard > 1, or sm_create_loopback), 3 = peer
+ * (sm_create_peer: *nranks / *rank = the shards its connected view holds and
+ * this one's place in it; the peer loopback: 1 / 0); for RCCL *nranks /
  * *rank = ncclCommCount / ncclCommUserRank of the RCCL communicator, and
  * 1 / 0 without one (the RCCL world of a host-staged or one-shard context is
  * this process alone). Any output pointer may be NULL. */

@@ -91,7 +91,11 @@ class Lattice:
         uid = None
         if unique_id is not None:
             uid = ctypes.create_string_buffer(bytes(unique_id), len(unique_id))
-        if loopback:  # one shard through the t-shard path over a one-rank RCCL communicator
+        if loopback == "peer":  # one shard through the t-shard path over the peer transport, to itself
+            if nshard != 1:
+                raise ValueError("loopback is one shard")
+            check(lib.sm_create_peer_loopback(ctypes.byref(h), Nx, Nt, device))
+        elif loopback:  # one shard through the t-shard path over a one-rank RCCL communicator
             if nshard != 1:
                 raise ValueError("loopback is one shard")
             if uid is None:
@@ -103,7 +107,7 @@ class Lattice:
         self.ctx = h
         self.last_cg = CGResult()
 
-    TRANSPORTS = {0: "none", 1: "hosted", 2: "rccl"}
+    TRANSPORTS = {0: "none", 1: "hosted", 2: "rccl", 3: "peer"}
 
     def comm_info(self):
         """(transport, nranks, rank) as the context's transport reports them

@@ -70,6 +70,11 @@ def _load():
         "sm_create": ([ctypes.POINTER(vp), ci, ci, ci, ci, ci, vp], ci),
         "sm_create_hosted": ([ctypes.POINTER(vp), ci, ci, ci, ci, ci, vp], ci),
         "sm_create_loopback": ([ctypes.POINTER(vp), ci, ci, ci, vp], ci),
+        "sm_peer_handle_bytes": ([], ci),
+        "sm_create_peer": ([ctypes.POINTER(vp), ci, ci, ci, ci, ci, vp, ci], ci),
+        "sm_peer_connect": ([vp, vp, ci], ci),
+        "sm_create_peer_loopback": ([ctypes.POINTER(vp), ci, ci, ci], ci),
+        "sm_peer_status": ([vp, ctypes.POINTER(ctypes.c_ulonglong)], ci),
         "sm_destroy": ([vp], ci),
         "sm_set_stream": ([vp, vp], ci),
         "sm_synchronize": ([vp], ci),

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <array>
 #include <cstdarg>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -124,7 +125,56 @@ int rccl_p2p_group(sm_ctx *c, hipStream_t s, int n, const double2 *const *send_u
     return SM_OK;
 }
 
+// ---- device-initiated transport (sm_peer.h, sm_peer.hip) ----
+static int peer_ready(const sm_ctx *c) {
+    if (!c->peer_connected) return fail(SM_ERR_STATE, "peer transport: sm_peer_connect has not run on this context");
+    return SM_OK;
+}
+
+// n (<= 3) exchanges through the receivers' mailboxes (generic faces)
+static int peer_exchange(sm_ctx *c, hipStream_t s, int n, const double2 *const *slo, const double2 *const *shi,
+                         double2 *const *rlo, double2 *const *rhi, size_t cnt) {
+    TRY(peer_ready(c));
+    if (n < 1 || n > 3 || (long)n * (long)cnt > kMailDoubles * (long)c->g.Nx)
+        return fail(SM_ERR_ARG, "peer exchange of %d x %zu doubles exceeds the mailbox", n, cnt);
+    PeerXfer x{};
+    for (int i = 0; i < n; ++i) {
+        x.slo[i] = (const double *)slo[i];
+        x.shi[i] = (const double *)shi[i];
+        x.rlo[i] = (double *)rlo[i];
+        x.rhi[i] = (double *)rhi[i];
+    }
+    x.n = n;
+    x.cnt = (long)cnt;
+    launch_peer_exchange(s, x, c->peer_view, ++c->peer_face_seq, c->peer_tick);
+    return SM_OK;
+}
+
+// Gather to shard 0 through its mailbox (cold path: the gauge field for a conf
+// file): a barrier so no earlier exchange still needs shard 0's mailbox, then
+// per sender and chunk: put, barrier, shard 0 copies out, barrier.
+static int peer_gather_to0(sm_ctx *c, hipStream_t s, const double *send, double *recv, size_t cnt) {
+    TRY(peer_ready(c));
+    const long cap = 4 * kMailDoubles * (long)c->g.Nx;  // shard 0's four mailbox slots, contiguous
+    double *mail0 = (double *)(c->peer_view.base[0] + peer_mail_off(c->g.Nx, 0, 0));
+    double *scratch = (double *)(c->sums + 3);
+    auto barrier = [&] { launch_peer_allreduce(s, scratch, 0, c->peer_view, ++c->peer_coll_seq); };
+    if (c->shard == 0 && cnt) HIP_TRY(hipMemcpyAsync(recv, send, cnt * sizeof(double), hipMemcpyDeviceToDevice, s));
+    barrier();
+    for (int r = 1; r < c->nshard; ++r)
+        for (size_t off = 0; off < cnt; off += (size_t)cap) {
+            const long len = (long)std::min(cnt - off, (size_t)cap);
+            if (c->shard == r) launch_peer_put(s, send + off, len, mail0);
+            barrier();
+            if (c->shard == 0) launch_peer_get(s, mail0, len, recv + (size_t)r * cnt + off);
+            barrier();
+        }
+    HIP_TRY(hipGetLastError());
+    return SM_OK;
+}
+
 int rccl_gather_to0(sm_ctx *c, hipStream_t s, const double *send, double *recv, size_t cnt) {
+    if (c->peer) return peer_gather_to0(c, s, send, recv, cnt);
     TRY(rccl_order(c, s));
     NCCL_TRY(ncclGroupStart());
     if (c->shard == 0) {
@@ -151,6 +201,11 @@ int exchange_faces_on(sm_ctx *c, hipStream_t s, double2 *slo, double2 *shi, doub
         HIP_TRY(hipStreamSynchronize(s));  // staging buffers are reused
         return SM_OK;
     }
+    if (c->peer) {
+        const double2 *sl[1] = {slo}, *sh[1] = {shi};
+        double2 *rl[1] = {rlo}, *rh[1] = {rhi};
+        return peer_exchange(c, s, 1, sl, sh, rl, rh, cnt);
+    }
     const double2 *su[1] = {shi}, *sd[1] = {slo};
     double2 *rd[1] = {rlo}, *ru[1] = {rhi};
     return rccl_p2p_group(c, s, 1, su, rd, sd, ru, cnt);
@@ -163,6 +218,7 @@ int exchange_faces_multi(sm_ctx *c, hipStream_t s, int n, double2 *const *slo, d
         return SM_OK;
     }
     if (cnt > kMaxFaceDoubles * (size_t)c->g.Nx) return fail(SM_ERR_ARG, "face too large (%zu)", cnt);
+    if (c->peer) return peer_exchange(c, s, n, slo, shi, rlo, rhi, cnt);
     return rccl_p2p_group(c, s, n, shi, rlo, slo, rhi, cnt);
 }
 
@@ -182,6 +238,12 @@ int allreduce_dev(sm_ctx *c, double *dev, int n) {
         HIP_TRY(hipStreamSynchronize(c->stream));
         return SM_OK;
     }
+    if (c->peer) {
+        TRY(peer_ready(c));
+        if (n > 8) return fail(SM_ERR_ARG, "peer all-reduce of %d doubles (at most 8)", n);
+        launch_peer_allreduce(c->stream, dev, n, c->peer_view, ++c->peer_coll_seq);
+        return SM_OK;
+    }
     TRY(rccl_order(c, c->stream));
     NCCL_TRY(ncclAllReduce(dev, dev, n, ncclDouble, ncclSum, c->comm, c->stream));
     return SM_OK;
@@ -192,6 +254,14 @@ int allreduce_dev(sm_ctx *c, double *dev, int n) {
 int halo(sm_ctx *c, const double2 *field, int set, int kind, TFaces *f) {
     if (!c->sharded()) {
         *f = faces_for(c, field, nullptr, nullptr);
+        return SM_OK;
+    }
+    if (c->peer) {  // packed straight into the neighbours' apply slots (sm_peer.hip)
+        TRY(peer_ready(c));
+        const unsigned long long seq = ++c->peer_face_seq;
+        launch_peer_pack_proj(c->stream, c->g, field, c->U, kind, c->peer_view, seq, c->peer_tick);
+        const double2 *slot = (const double2 *)(c->peer_region + peer_apply_off(c->g.Nx, (int)(seq & 3)));
+        *f = faces_for(c, field, slot, slot + c->g.Nx);
         return SM_OK;
     }
     double2 *slo = face_buf(c, set, 0), *shi = face_buf(c, set, 1);
@@ -208,7 +278,7 @@ int apply(sm_ctx *c, const double2 *in, double2 *out, double mass, int dagger, c
           double2 *partials, const CGScalars *skip) {
     TFaces f;
     const int TB = (c->g.Wt + c->cfg.bt - 1) / c->cfg.bt;
-    if (!c->sharded() || TB < 3 || !c->apply_split) {
+    if (!c->sharded() || TB < 3 || !c->apply_split || c->peer) {
         // one shard, or a narrow t-shard: faces first, then one launch
         TRY(halo(c, in, 0, dagger ? FACE_DDAG : FACE_D, &f));
         launch_dslash(c->stream, c->g, c->cfg, dagger, in, out, c->U, loU(c), f, mass, aux, partials, skip);
@@ -286,6 +356,17 @@ int halo2_multi(sm_ctx *c, hipStream_t s, const double2 *const *fields, double2 
             TRY(exchange_faces_on(c, s, face2_send(c, f, 0), face2_send(c, f, 1), faces[f],
                                   faces[f] + (size_t)4 * c->g.Nx, cnt));
         return SM_OK;
+    }
+    if (c->peer) {
+        const double2 *sl[3], *sh[3];
+        double2 *rl[3], *rh[3];
+        for (int f = 0; f < nf && f < 3; ++f) {
+            sl[f] = face2_send(c, f, 0);
+            sh[f] = face2_send(c, f, 1);
+            rl[f] = faces[f];
+            rh[f] = faces[f] + (size_t)4 * c->g.Nx;
+        }
+        return peer_exchange(c, s, nf, sl, sh, rl, rh, cnt);
     }
     const double2 *su[3], *sd[3];
     double2 *rd[3], *ru[3];
@@ -538,13 +619,13 @@ static int apply_test_opts(sm_ctx *c) {
 }
 
 static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device,
-                         const void *unique_id, const sm_host_transport *tr, bool loop = false) {
+                         const void *unique_id, const sm_host_transport *tr, bool loop = false, bool peer = false) {
     if (!out) return fail(SM_ERR_ARG, "null out");
     *out = nullptr;
     int t0, Wt;
     if (Nx < 1) return fail(SM_ERR_ARG, "Nx=%d", Nx);
     TRY(sm_shard_plan(Nt_global, nshard, shard, &t0, &Wt));
-    if (nshard > 1 && !unique_id && !tr) return fail(SM_ERR_ARG, "nshard > 1 needs a unique id or a transport");
+    if (nshard > 1 && !unique_id && !tr && !peer) return fail(SM_ERR_ARG, "nshard > 1 needs a unique id or a transport");
     if (tr && (!tr->exchange || !tr->allreduce_sum)) return fail(SM_ERR_ARG, "incomplete host transport");
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
@@ -555,6 +636,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->n_cu <= 0)
         c->n_cu = 256;
     c->loop = loop;
+    c->peer = peer;
     c->nshard = nshard;
     c->shard = shard;
     c->g.Nx = Nx;
@@ -618,7 +700,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     // on ONE stream (one hardware queue per process, the fewest when several
     // shards share a GPU). RCCL contexts overlap faces and edge blocks with
     // the interior on a separate comm stream.
-    if (c->hosted) {
+    if (c->hosted || c->peer) {
         c->comm_stream = c->own_stream;
     } else {
         chk(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
@@ -651,6 +733,13 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     chk(hipHostMalloc(&c->h_sums, sizeof(double2) * 4));
     chk(hipHostMalloc(&c->h_face, sizeof(double) * 4 * kMaxFaceDoubles * (size_t)Nx));
     chk(hipHostMalloc(&c->h_red, sizeof(double) * 8));
+    if (c->peer) {  // the region the other shards store into (sm_peer.h), uncached
+        chk(hipExtMallocWithFlags((void **)&c->peer_region, (size_t)peer_region_bytes(Nx), hipDeviceMallocUncached));
+        chk(hipMalloc(&c->peer_tick, sizeof(unsigned)));
+        chk(hipMalloc(&c->peer_view_dev, sizeof(PeerView)));
+        if (e == hipSuccess) chk(hipMemsetAsync(c->peer_region, 0, (size_t)peer_region_bytes(Nx), c->own_stream));
+        if (e == hipSuccess) chk(hipMemsetAsync(c->peer_tick, 0, sizeof(unsigned), c->own_stream));
+    }
     // on the context's stream, not the null stream (which would be one more
     // hardware queue per process); face slots start as zeros, not whatever
     // the allocator hands back
@@ -670,6 +759,8 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     }
     if (c->hosted) {
         c->tr = *tr;
+    } else if (c->peer) {
+        // connected by sm_peer_connect (the loopback: here, to itself)
     } else if (c->sharded()) {
         ncclUniqueId id;
         memcpy(&id, unique_id, sizeof id);
@@ -694,6 +785,95 @@ int sm_create_loopback(sm_ctx **out, int Nx, int Nt_global, int device, const vo
     return create_common(out, Nx, Nt_global, 1, 0, device, unique_id, nullptr, true);
 }
 
+// ---- the peer transport (sm_peer.h) ----
+int sm_peer_handle_bytes(void) { return (int)sizeof(hipIpcMemHandle_t); }
+
+static int peer_set_view(sm_ctx *c) {
+    PeerView &v = c->peer_view;
+    v.me = c->loop ? 0 : c->shard;
+    v.n = c->loop ? 1 : c->nshard;
+    v.down = c->loop ? 0 : down_rank(c);
+    v.up = c->loop ? 0 : up_rank(c);
+    v.Nx = c->g.Nx;
+    v.base[v.me] = c->peer_region;
+    HIP_TRY(hipMemcpyAsync(c->peer_view_dev, &v, sizeof v, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->peer_connected = true;
+    // handshake: one all-reduce of the shard numbers (every shard's region is
+    // reachable and its flags move), checked here
+    double *chk = (double *)(c->sums + 3);
+    const double mine = (double)v.me;
+    HIP_TRY(hipMemcpyAsync(chk, &mine, sizeof mine, hipMemcpyHostToDevice, c->stream));
+    TRY(allreduce_dev(c, chk, 1));
+    double got = -1.0;
+    HIP_TRY(hipMemcpyAsync(&got, chk, sizeof got, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    TRY(sm_peer_status(c, nullptr));
+    if (got != 0.5 * v.n * (v.n - 1))
+        return fail(SM_ERR_STATE, "peer transport handshake: sum of shard numbers %g, expected %g", got,
+                    0.5 * v.n * (v.n - 1));
+    return SM_OK;
+}
+
+int sm_create_peer(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device, void *handle_out,
+                   int handle_bytes) {
+    if (nshard < 2 || nshard > kPeerMaxRanks)
+        return fail(SM_ERR_ARG, "peer transport: 2..%d shards (one shard: sm_create_peer_loopback)", kPeerMaxRanks);
+    if (!handle_out || handle_bytes < sm_peer_handle_bytes())
+        return fail(SM_ERR_ARG, "peer transport: the handle buffer must hold %d bytes", sm_peer_handle_bytes());
+    TRY(create_common(out, Nx, Nt_global, nshard, shard, device, nullptr, nullptr, false, true));
+    hipIpcMemHandle_t h;
+    const hipError_t e = hipIpcGetMemHandle(&h, (*out)->peer_region);
+    if (e != hipSuccess) {
+        sm_destroy(*out);
+        *out = nullptr;
+        return fail(SM_ERR_HIP, "hipIpcGetMemHandle: %s", hipGetErrorString(e));
+    }
+    memcpy(handle_out, &h, sizeof h);
+    return SM_OK;
+}
+
+int sm_peer_connect(sm_ctx *c, const void *handles, int handle_bytes_each) {
+    if (!c || !c->peer || c->loop) return fail(SM_ERR_ARG, "sm_peer_connect: not a peer-transport context");
+    if (c->peer_connected) return fail(SM_ERR_STATE, "sm_peer_connect: already connected");
+    if (!handles || handle_bytes_each < sm_peer_handle_bytes())
+        return fail(SM_ERR_ARG, "sm_peer_connect: %d-byte handles expected", sm_peer_handle_bytes());
+    HIP_TRY(hipSetDevice(c->device));
+    for (int r = 0; r < c->nshard; ++r) {
+        if (r == c->shard) continue;
+        hipIpcMemHandle_t h;
+        memcpy(&h, (const char *)handles + (size_t)r * handle_bytes_each, sizeof h);
+        void *p = nullptr;
+        const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) return fail(SM_ERR_HIP, "hipIpcOpenMemHandle of shard %d: %s", r, hipGetErrorString(e));
+        c->peer_open[r] = (char *)p;
+        c->peer_view.base[r] = (char *)p;
+    }
+    return peer_set_view(c);
+}
+
+int sm_create_peer_loopback(sm_ctx **out, int Nx, int Nt_global, int device) {
+    TRY(create_common(out, Nx, Nt_global, 1, 0, device, nullptr, nullptr, true, true));
+    const int rc = peer_set_view(*out);
+    if (rc != SM_OK) {
+        sm_destroy(*out);
+        *out = nullptr;
+    }
+    return rc;
+}
+
+int sm_peer_status(sm_ctx *c, unsigned long long *timed_out_seq) {
+    if (!c) return fail(SM_ERR_ARG, "null context");
+    unsigned long long err = 0;
+    if (c->peer && c->peer_region) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipMemcpy(&err, c->peer_region + offsetof(PeerHdr, err), sizeof err, hipMemcpyDeviceToHost));
+    }
+    if (timed_out_seq) *timed_out_seq = err;
+    if (err) return fail(SM_ERR_RCCL, "peer transport: a wait timed out (sequence %llu)", err);
+    return SM_OK;
+}
+
 int sm_create_hosted(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device,
                      const sm_host_transport *transport) {
     if (!transport) return fail(SM_ERR_ARG, "null transport");
@@ -706,6 +886,14 @@ int sm_destroy(sm_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);  // e.g. a CG's trailing face exchange
     if (c->comm) ncclCommDestroy(c->comm);
+    for (char *&p : c->peer_open)
+        if (p) {
+            (void)hipIpcCloseMemHandle(p);
+            p = nullptr;
+        }
+    if (c->peer_region) (void)hipFree(c->peer_region);
+    if (c->peer_tick) (void)hipFree(c->peer_tick);
+    if (c->peer_view_dev) (void)hipFree(c->peer_view_dev);
     for (double2 *&f : c->fields)
         if (f) {
             stream_free(c, f);
@@ -850,7 +1038,7 @@ int sm_set_stream(sm_ctx *c, void *s) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->rccl_last == c->stream) c->rccl_last = nullptr;
     c->stream = s ? (hipStream_t)s : c->own_stream;
-    if (c->hosted) c->comm_stream = c->stream;  // hosted contexts run on one stream
+    if (c->hosted || c->peer) c->comm_stream = c->stream;  // hosted and peer contexts run on one stream
     return SM_OK;
 }
 
@@ -859,6 +1047,10 @@ int sm_comm_info(const sm_ctx *c, int *transport, int *nranks, int *rank) {
     int t = 0, n = 1, r = 0;
     if (c->hosted) {
         t = 1;
+    } else if (c->peer) {
+        t = 3;  // the shards the peer view holds (sm_peer_connect)
+        n = c->peer_view.n;
+        r = c->peer_view.me;
     } else if (c->comm) {
         t = 2;
         NCCL_TRY(ncclCommCount(c->comm, &n));  // what the communicator itself holds, not the creation arguments
@@ -1068,6 +1260,47 @@ static bool ra_edge_owns_faces(const sm_ctx *c, const CGFusedCfg &fc, int tb_lo,
     return true;
 }
 
+// The recompute-Ad pass on t-shards over the peer transport: ONE launch over
+// every t-block on the main stream. The blocks owning columns 0..3 / Wt-4..Wt-1
+// store d_j's 4-deep faces straight into ring slot j % 3 of the down / up
+// neighbour's region, and the pass's last block all-reduces the shard's sums
+// in-kernel (cg_ticketed_tail) -- it returns only once every shard's sums of
+// pass j are in, and every shard's pass j has written its faces before its own
+// sums, so pass j+1 finds d_j's faces in its ring when it starts. Pass 0 reads
+// d_0's faces from a generic exchange into slot 2 (= -1 mod 3); shards narrower
+// than 8 columns (the lo and hi face columns overlap) exchange d_{j-1} at every
+// pass that way. Ring slots by j % 3: pass j reads slots j-1, j-2 and its
+// neighbours write slot j, which nobody reads before pass j+1.
+static double2 *peer_ring(const sm_ctx *c, int r, long j) {
+    return (double2 *)(c->peer_view.base[r] + peer_ring_off(c->g.Nx, (int)(((j % 3) + 3) % 3)));
+}
+
+static int cg_ra_pass_peer(sm_ctx *c, const double2 *d1, const double2 *d2, double2 *dn, const double *ua) {
+    TRY(peer_ready(c));
+    const long j = c->cg_issued;
+    const bool first = j == 0;
+    const CGFusedCfg &fc = c->racfg;
+    const int nparts = cg_fused_blocks(fc);
+    if (fc.fold < 2 || (nparts + 63) / 64 > kMaxTickGroups)
+        return fail(SM_ERR_STATE, "peer transport: the recompute-Ad pass needs the ticketed tail");
+    const int me = c->peer_view.me;
+    double2 *f1 = peer_ring(c, me, j - 1), *f2 = first ? f1 : peer_ring(c, me, j - 2);
+    const bool direct = c->g.Wt >= 8;
+    if (first || !direct) TRY(halo4(c, c->stream, d1, f1));
+    const long Nx = c->g.Nx;
+    double2 *fs = direct ? peer_ring(c, c->peer_view.down, j) + 8 * Nx : nullptr;  // my columns 0..3: its Wt..Wt+3
+    double2 *fsh = direct ? peer_ring(c, c->peer_view.up, j) : nullptr;             // my Wt-4..Wt-1: its -4..-1
+    double2 *sums = &c->sc->sumr[j & 1][0];
+    const int lb = launch_cg_ra(c->stream, c->g, fc, c->kshards(), d1, d2, dn, c->cg_x, c->U, f1, f2, face4_recv_U(c),
+                                c->cg_mass, j, c->sc, c->partials, 0, fc.TBk, nullptr, ua, c->Uang_face, fs, 0,
+                                c->tick, nparts, c->gsum, sums, 1, c->link_fmt, fsh, c->peer_view_dev,
+                                ++c->peer_coll_seq);
+    if (lb) c->cg_link_bytes_last = lb;
+    c->cg_flush_pass = j;
+    c->cg_flush_sums = 1;
+    return SM_OK;
+}
+
 static int cg_ra_pass(sm_ctx *c) {
     const long j = c->cg_issued;
     const bool first = j == 0;
@@ -1101,6 +1334,7 @@ static int cg_ra_pass(sm_ctx *c) {
         }
         return SM_OK;
     }
+    if (c->peer) return cg_ra_pass_peer(c, d1, d2, dn, ua);
     // pass 0 has no d_{-2}: its (zero-weighted) faces are d_0's own, never the
     // other slot, which holds nothing of this solve yet (the zero multiplier
     // beta2 = 0 would turn a stale NaN there into a NaN iterate)
@@ -1278,7 +1512,9 @@ int sm_cg_finish(sm_ctx *c, sm_cg_result *res) {
         c->cg_x_user = nullptr;
     }
     c->cg_active = 0;
-    return sm_cg_status(c, res);
+    TRY(sm_cg_status(c, res));
+    if (c->peer) return sm_peer_status(c, nullptr);  // a timed-out wait makes the solve an error
+    return SM_OK;
 }
 
 int sm_cg_status(sm_ctx *c, sm_cg_result *res) {

@@ -86,6 +86,9 @@ struct RAArgs {
     int xpar;                // XP: this pass updates x on the rows of parity xpar (= pass & 1)
     int pbase;               // partial slots: tile pbase + (t-block - tb0) * XB + x-chunk
     double2 *fsend;          // SH: != null -> the edge blocks also write d_j's 4-deep send faces
+    double2 *fsendh;         //   (lo part at fsend, hi part at fsendh)
+    const PeerView *peer;    // peer transport: faces as system-scope stores, the tail all-reduces (pseq)
+    unsigned long long pseq;
     // TK (ticketed tail): counters tick[0] (groups) and tick[1 + g] (64 tiles
     // each), ntiles tiles over every launch of the pass, group sums gsum; the
     // last block forms the scalars (out3 == null) or writes the 3 sums to out3
@@ -451,8 +454,14 @@ __device__ __forceinline__ void ra_march(const RAArgs &a, int cbase, int span, i
                 if (SH && a.fsend) {  // fused face pack ([col][plane][x], lo: columns 0..3, hi: Wt-4..Wt-1)
                     const int fcol = c < RH ? c : (c >= Wt - RH ? c - (Wt - RH) + RH : -1);
                     if (fcol >= 0) {
-                        a.fsend[(long)(2 * fcol) * Nx + Xr] = J2.a;
-                        a.fsend[(long)(2 * fcol + 1) * Nx + Xr] = J2.b;
+                        double2 *fb = fcol < RH ? a.fsend + (long)(2 * fcol) * Nx : a.fsendh + (long)(2 * (fcol - RH)) * Nx;
+                        if (a.peer) {  // into the neighbour's region: write-through (sm_peer.h)
+                            sys_st2(fb + Xr, J2.a);
+                            sys_st2(fb + Nx + Xr, J2.b);
+                        } else {
+                            fb[Xr] = J2.a;
+                            fb[Nx + Xr] = J2.b;
+                        }
                     }
                 }
                 if (XP && (Xr & 1) == a.xpar) {  // x_j = (x_{j-2} + alpha_{j-2} d_{j-2}) + alpha_{j-1} d_{j-1}
@@ -618,7 +627,7 @@ __global__ void __launch_bounds__(256) cg_ra_kernel(RAArgs a) {
         }
         return;
     }
-    cg_ticketed_tail(a.partials, tile, a.ntiles, a.tick, a.gsum, a.out3, sc, a.first, s0, s1, s2);
+    cg_ticketed_tail(a.partials, tile, a.ntiles, a.tick, a.gsum, a.out3, sc, a.first, s0, s1, s2, SH ? a.peer : nullptr, a.pseq);
 }
 
 CGFusedCfg cg_ra_config(const Geometry &g) {
@@ -732,7 +741,7 @@ int launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsha
                   const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
                   int tb0, int tbn, const double2 *prev_partials, const double *Uang, const double *fUang,
                   double2 *fsend, int pbase, unsigned *tick, int ntiles, double2 *gsum, double2 *out3,
-                  int red_sums, int link_fmt) {
+                  int red_sums, int link_fmt, double2 *fsendh, const PeerView *peer, unsigned long long pseq) {
     if (tbn <= 0) return 0;
     RAArgs a;
     a.d1 = d1; a.d2 = d2; a.dn = dn; a.x = x; a.U = U;
@@ -755,6 +764,9 @@ int launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsha
     a.Ub = Uang ? reinterpret_cast<const uint8_t *>(a.Uf + 2 * g.V) : nullptr;
     a.fUb = fUang ? reinterpret_cast<const uint8_t *>(a.fUf + 16 * (long)g.Nx) : nullptr;
     a.fsend = fsend;
+    a.fsendh = fsendh ? fsendh : (fsend ? fsend + 8 * (long)g.Nx : nullptr);
+    a.peer = peer;
+    a.pseq = pseq;
     a.pbase = pbase;
     a.tick = tick;
     a.ntiles = ntiles;

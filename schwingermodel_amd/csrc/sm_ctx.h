@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "sm_internal.h"
+#include "sm_peer.h"
 
 namespace sm_host {
 
@@ -124,6 +125,17 @@ struct sm_ctx {
     unsigned *tick = nullptr;       // 1 + kMaxTickGroups counters, zeroed at creation
     double2 *gsum = nullptr;        // 3 per group
     ncclComm_t comm = nullptr;      // the context's one communicator; its operations in one total order
+    // Device-initiated transport (sm_peer.h; sm_create_peer / sm_peer_connect,
+    // sm_create_peer_loopback): every shard's region mapped here, kernels store
+    // into the neighbours' regions and wait on flags in their own. One stream.
+    bool peer = false;
+    bool peer_connected = false;
+    char *peer_region = nullptr;    // mine (uncached, IPC-exported)
+    char *peer_open[sm::kPeerMaxRanks] = {};  // the others' regions as opened here (null: mine / not open)
+    sm::PeerView peer_view{};       // host copy (kernel arguments)
+    sm::PeerView *peer_view_dev = nullptr;  // device copy (the CG pass's tail)
+    unsigned long long peer_coll_seq = 0, peer_face_seq = 0;  // the next collective / face exchange is seq + 1
+    unsigned *peer_tick = nullptr;  // zeroed ticket counter of the transport kernels
     bool hosted = false;            // host-callback transport instead of RCCL
     sm_host_transport tr{};
     double *h_face = nullptr;       // pinned: send_lo, send_hi, recv_lo, recv_hi (4 x up to 8Nx doubles)

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include "sm_internal.h"
+#include "sm_peer.h"
 
 #pragma clang fp contract(off)
 
@@ -423,6 +424,20 @@ __device__ __forceinline__ bool last_block_arrive(unsigned *counter, unsigned nb
     if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // block-uniform: the winner only
     return last;
 }
+// One spin-projected face value (TFaces::proj; launch_pack_faces_proj and the
+// peer transport's pack): side 0 = the t = 0 column's forward-hop combination
+// (sent down), side 1 = conj(U_t(t = Wt-1)) times the backward combination
+// (sent up). The reference's own sums and product (src/dirac_operator.cpp:31-43,
+// 255-267; force :493-506).
+__device__ __forceinline__ double2 proj_face_value(int kind, int side, double2 p0, double2 p1, const double2 *Ut) {
+    if (!side) return (kind == FACE_DDAG || kind == FACE_FORCE_L) ? cadd(p0, p1) : csub(p0, p1);
+    switch (kind) {
+        case FACE_D: return cmul(cconj(*Ut), cadd(p0, p1));
+        case FACE_DDAG: return cmul(cconj(*Ut), csub(p0, p1));
+        default: return make_double2(0.0, 0.0);  // the force reads only t+1 neighbours: the lo face sent down
+    }
+}
+
 // Fixed-order wave sum (butterfly; every lane gets the same bits).
 __device__ __forceinline__ double2 wave_sum(double2 v) {
 #pragma unroll
@@ -439,9 +454,13 @@ __device__ __forceinline__ double2 wave_sum(double2 v) {
 // lane, fixed butterfly order), the last group's block sums the group sums in
 // order and forms the scalars in sc (out3 == null) or writes the three sums
 // to out3 (a t-shard's, for the all-reduce). Every thread of the block calls it.
+// peer != null (t-shards over the peer transport, sm_peer.h): the last block
+// all-reduces the three sums over every shard (collective number pseq) before
+// writing them to out3.
 __device__ __forceinline__ void cg_ticketed_tail(double2 *partials, long tile, int ntiles, unsigned *tick,
                                                  double2 *gsum, double2 *out3, CGScalars *sc, int first, double2 s0,
-                                                 double2 s1, double2 s2) {
+                                                 double2 s1, double2 s2, const PeerView *peer = nullptr,
+                                                 unsigned long long pseq = 0) {
     double2 *p = partials + 3 * tile;
     if (threadIdx.x == 0) {
         publish_partial(p, s0);
@@ -485,6 +504,13 @@ __device__ __forceinline__ void cg_ticketed_tail(double2 *partials, long tile, i
         v2 = wave_sum(v2);
         if (lane == 0) {
             if (out3) {
+                if (peer) {
+                    double val[6] = {v0.x, v0.y, v1.x, v1.y, v2.x, v2.y};
+                    peer_allreduce_thread(*peer, pseq, val, 6);
+                    v0 = make_double2(val[0], val[1]);
+                    v1 = make_double2(val[2], val[3]);
+                    v2 = make_double2(val[4], val[5]);
+                }
                 out3[0] = v0;
                 out3[1] = v1;
                 out3[2] = v2;

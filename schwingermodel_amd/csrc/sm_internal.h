@@ -28,6 +28,8 @@ struct TFaces {
 };
 enum FaceKind { FACE_D = 0, FACE_DDAG = 1, FACE_FORCE_L = 2, FACE_FORCE_R = 3 };
 
+struct PeerView;  // sm_peer.h
+
 struct Geometry {
     int Nx, Wt;          // local block (all x, Wt t-values)
     int t0, Ntg;         // global t offset of this shard, global Nt
@@ -148,7 +150,8 @@ int launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsha
                  int tb0, int tbn, const double2 *prev_partials = nullptr, const double *Uang = nullptr,
                  const double *fUang = nullptr, double2 *fsend = nullptr, int pbase = 0,
                  unsigned *tick = nullptr, int ntiles = 0, double2 *gsum = nullptr, double2 *out3 = nullptr,
-                 int red_sums = 0, int link_fmt = 1);
+                 int red_sums = 0, int link_fmt = 1, double2 *fsendh = nullptr, const PeerView *peer = nullptr,
+                 unsigned long long pseq = 0);
 // Resident blocks per CU of the t-shard pass kernel at c's block size (0 if
 // the runtime cannot tell); link_fmt 0 = complex links, 1 / 2 = the code forms.
 int cg_ra_shard_blocks_per_cu(const CGFusedCfg &c, int link_fmt);
@@ -158,7 +161,11 @@ int cg_ra_shard_blocks_per_cu(const CGFusedCfg &c, int link_fmt);
 constexpr int kMaxTickGroups = 1024;
 // (partial slot of a tile: pbase + (t-block - tb0) * XB + x-chunk; fsend (t-shards):
 // the blocks owning columns 0..3 / Wt-4..Wt-1 also write d_j's 4-deep send
-// faces, lo at fsend and hi at fsend + 8 Nx, as launch_pack_faces_k would)
+// faces, lo at fsend and hi at fsendh (default fsend + 8 Nx), as
+// launch_pack_faces_k would; peer (device copy of the peer view): those faces
+// go out as write-through system-scope stores (fsend / fsendh then point into
+// the neighbours' regions) and the tail all-reduces the shard's sums itself,
+// collective number pseq, into out3)
 // Link codes of U for the passes above (Uang: 20 instead of 32 B/site of
 // links, sm_linkcode.h): writes the codes v of n links to Ua[0, n) and their
 // flag words to the n uint16 right after them, and per block the count of
@@ -290,5 +297,25 @@ void launch_pack_faces(hipStream_t s, const Geometry &g, const double2 *field, d
 // t = Wt-1, sent up) = conj(U_t) * the backward combination; Nx complex each.
 void launch_pack_faces_proj(hipStream_t s, const Geometry &g, const double2 *field, const double2 *U, int kind,
                             double2 *lo_face, double2 *hi_face);
+
+// ---- device-initiated shard transport (sm_peer.hip, layout in sm_peer.h) ----
+// n (<= 3) face exchanges of cnt doubles per field and side, as exchange_faces_on:
+// slo[f] goes down (arriving as the receiver's rhi[f]), shi[f] up (its rlo[f])
+struct PeerXfer {
+    const double *slo[3], *shi[3];
+    double *rlo[3], *rhi[3];
+    int n;
+    long cnt;
+};
+// in-place sum of n <= 8 doubles over every shard, in rank order
+void launch_peer_allreduce(hipStream_t s, double *dev, int n, const PeerView &v, unsigned long long seq);
+// the exchange through the receivers' mailboxes (two kernels; tick: a zeroed counter)
+void launch_peer_exchange(hipStream_t s, const PeerXfer &x, const PeerView &v, unsigned long long seq,
+                          unsigned *tick);
+// launch_pack_faces_proj's faces stored into the neighbours' apply slot seq % 4, then the handoff
+void launch_peer_pack_proj(hipStream_t s, const Geometry &g, const double2 *field, const double2 *U, int kind,
+                           const PeerView &v, unsigned long long seq, unsigned *tick);
+void launch_peer_put(hipStream_t s, const double *src, long cnt, double *dst_remote);
+void launch_peer_get(hipStream_t s, const double *src_local, long cnt, double *dst);
 
 }  // namespace sm

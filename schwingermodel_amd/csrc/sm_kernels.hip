@@ -674,17 +674,9 @@ __global__ void __launch_bounds__(256) pack_faces_proj_kernel(int Nx, int Wt, lo
     const int x = i >> 1, side = i & 1;
     const long n = (long)x * Wt + (side ? Wt - 1 : 0);
     const double2 p0 = f[n], p1 = f[n + V];
-    if (!side) {
-        // lo: D sends p0 - p1 down; D^dag and the force's left field p0 + p1,
-        // its right field p0 - p1
-        lo[x] = (kind == FACE_DDAG || kind == FACE_FORCE_L) ? cadd(p0, p1) : csub(p0, p1);
-        return;
-    }
-    switch (kind) {
-        case FACE_D: hi[x] = cmul(cconj(U[n]), cadd(p0, p1)); break;
-        case FACE_DDAG: hi[x] = cmul(cconj(U[n]), csub(p0, p1)); break;
-        default: hi[x] = make_double2(0.0, 0.0); break;  // the force reads only t+1 neighbours: the lo face sent down
-    }
+    const double2 v = proj_face_value(kind, side, p0, p1, U + n);
+    if (!side) lo[x] = v;
+    else hi[x] = v;
 }
 
 void launch_pack_faces_proj(hipStream_t s, const Geometry &g, const double2 *field, const double2 *U, int kind,

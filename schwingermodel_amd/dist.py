@@ -112,6 +112,31 @@ def create_hosted_context(Nx, Nt, device=0):
     return h, tr
 
 
+def create_peer_context(Nx, Nt, device=0):
+    """sm_create_peer + sm_peer_connect over the current torch.distributed group:
+    the region handles are all-gathered in rank order (control plane only; the
+    data path is the device-initiated transport). Returns the context."""
+    import torch.distributed as dist
+    nb = lib.sm_peer_handle_bytes()
+    buf = ctypes.create_string_buffer(nb)
+    h = ctypes.c_void_p()
+    check(lib.sm_create_peer(ctypes.byref(h), Nx, Nt, dist.get_world_size(), dist.get_rank(), device, buf, nb))
+    handles = [None] * dist.get_world_size()
+    dist.all_gather_object(handles, bytes(buf.raw))
+    allh = ctypes.create_string_buffer(b"".join(handles), nb * len(handles))
+    check(lib.sm_peer_connect(h, allh, nb))
+    return h
+
+
+def create_shard_context(Nx, Nt, device=0, transport="hosted"):
+    """One t-shard of the current torch.distributed group on `device`, over the
+    host-staged transport ("hosted": returns (ctx, transport object to keep
+    alive)) or the peer transport ("peer": returns (ctx, None))."""
+    if transport == "peer":
+        return create_peer_context(Nx, Nt, device), None
+    return create_hosted_context(Nx, Nt, device)
+
+
 def broadcast_unique_id():
     """RCCL unique id created on rank 0 (needs a GPU there) and broadcast to all."""
     import torch.distributed as dist

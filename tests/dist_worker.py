@@ -33,6 +33,10 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, HERE)
 
 
+# the shard transport of the one-GPU worlds: "hosted" (sm_create_hosted + gloo) or "peer"
+# (sm_create_peer: device-initiated stores between the processes' regions)
+TRANSPORT = os.environ.get("SM_WORKER_TRANSPORT", "hosted")
+
 def shard_field(flat, Nx, Nt, t0, Wt):
     """Global two-plane interleaved field -> this shard's block (same layout)."""
     S = Nx * Nt
@@ -113,7 +117,7 @@ def run_md(name, result_path, dist, rank, world):
     Pm = shard_real(a["P"], Nx, Nt, t0, Wt)
     prm = sm.HMCParams(meta["m0"], meta["beta"], meta["tau"], meta["md_steps"], 1e-10, 10000, 99)
     dev = int(os.environ.get("SM_DEVICE", "0"))
-    ctx, tr = smd.create_hosted_context(Nx, Nt, device=dev)
+    ctx, tr = smd.create_shard_context(Nx, Nt, transport=TRANSPORT, device=dev)
     sm.check(sm.lib.sm_upload_gauge(ctx, P_(U[0]), P_(U[1])))
     local = {}
     sp, act = ctypes.c_double(), ctypes.c_double()
@@ -246,7 +250,7 @@ def run_eo(name, result_path, dist, rank, world):
     V = Nx * Wt
     mine = [shard_field(g[k], Nx, Nt, t0, Wt) for k in ("U", "psi", "phi")]
     dev = int(os.environ.get("SM_DEVICE", "0"))
-    ctx, tr = smd.create_hosted_context(Nx, Nt, device=dev)
+    ctx, tr = smd.create_shard_context(Nx, Nt, transport=TRANSPORT, device=dev)
     sm.check(sm.lib.sm_upload_gauge(ctx, ctypes.c_void_p(mine[0][0].ctypes.data),
                                     ctypes.c_void_p(mine[0][1].ctypes.data)))
     local = eo_ops(sm, ctx, V, mine, m0, prm)
@@ -308,7 +312,7 @@ def run_eocg(name, result_path, dist, rank, world):
 
     mine = [shard_field(g[k], Nx, Nt, t0, Wt) for k in ("U", "psi")]
     dev = int(os.environ.get("SM_DEVICE", "0"))
-    ctx, tr = smd.create_hosted_context(Nx, Nt, device=dev)
+    ctx, tr = smd.create_shard_context(Nx, Nt, transport=TRANSPORT, device=dev)
     x, cg = solve(ctx, Nx * Wt, mine[0], mine[1])
     sm.lib.sm_destroy(ctx)
     gathered = [None] * world
@@ -360,7 +364,7 @@ def run_angles(name, result_path, dist, rank, world):
     sm.check(sm.lib.sm_shard_plan(Nt, world, rank, ctypes.byref(t0), ctypes.byref(Wt)))
     U, p = (shard_field(g[k], Nx, Nt, t0.value, Wt.value) for k in ("U", "psi"))
     P_ = lambda x: ctypes.c_void_p(x.ctypes.data)  # noqa: E731
-    ctx, tr = smd.create_hosted_context(Nx, Nt, device=int(os.environ.get("SM_DEVICE", "0")))
+    ctx, tr = smd.create_shard_context(Nx, Nt, transport=TRANSPORT, device=int(os.environ.get("SM_DEVICE", "0")))
     sm.check(sm.lib.sm_tune_cg(ctx, 5, 0))
     sm.check(sm.lib.sm_cg_link_angles(ctx, int(wish[rank]), None))
     out = []
@@ -502,7 +506,7 @@ def run_big(name, result_path, dist, rank, world):
     t0, Wt = t0.value, Wt.value
     V = Nx * Wt
     f = fill_block(sm, Nx, Nt, t0, Wt, sigma, nthreads=2)
-    ctx, tr = smd.create_hosted_context(Nx, Nt, device=dev)
+    ctx, tr = smd.create_shard_context(Nx, Nt, transport=TRANSPORT, device=dev)
     sm.check(sm.lib.sm_upload_gauge(ctx, ctypes.c_void_p(f["U"].ctypes.data),
                                     ctypes.c_void_p(f["U"][2 * V:].ctypes.data)))
     ts = time.time()
@@ -661,7 +665,7 @@ def main():
                                  P(r_hi[:2 * Nx]), P(r_hi[2 * Nx:]), P(out0), P(out1), m0, dag)
             local[key] = (out0, out1)
     else:
-        ctx, tr = smd.create_hosted_context(Nx, Nt, device=int(os.environ.get("SM_DEVICE", "0")))
+        ctx, tr = smd.create_shard_context(Nx, Nt, transport=TRANSPORT, device=int(os.environ.get("SM_DEVICE", "0")))
         ci = [ctypes.c_int(-1) for _ in range(3)]
         sm.check(sm.lib.sm_comm_info(ctx, *(ctypes.byref(v) for v in ci)))
         local["comm_info"] = tuple(v.value for v in ci)  # host-staged: transport 1, no RCCL world

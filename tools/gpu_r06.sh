@@ -139,6 +139,15 @@ j() {
   NCCL_LAUNCH_MODE=GROUP timeout -k 10 300 $L > gpurun_out/r06j_group.log 2>&1
 }
 
+# k: the peer transport -- its tests (loopback and 2-8 processes on the one GPU), then the loopback probe
+#    with the plain shard, the RCCL loopback and the peer loopback side by side
+k() {
+  timeout -k 10 900 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_peer_gpu.py \
+    > gpurun_out/r06k_tests.log 2>&1 &&
+  timeout -k 10 400 python -u tools/loopback_probe.py --shapes 4096x512,4096x1024,4096x2048 --iters 200 --rounds 3 \
+    --applies 20 > gpurun_out/r06k_loopback.log 2>&1
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--m0", type=float, default=-0.06)
     ap.add_argument("--sigma", type=float, default=0.2374)
     ap.add_argument("--geom", default="", help="waves per block,rows per block of the CG pass (sm_tune_cg_geometry)")
+    ap.add_argument("--contexts", default="one,loopback,peer",
+                    help="one (plain shard), loopback (RCCL to itself), peer (the peer transport to itself)")
     a = ap.parse_args()
     import torch
     import schwingermodel_amd as sm
@@ -51,7 +53,9 @@ def main():
         sm.lib.sm_fill_spinor(91011, Nt, 0, Nx, 0, Nt, cn.ctypes.data, cn[2 * V:].ctypes.data)
         dU, phi = U.cuda(), chi.cuda()
         x = torch.empty_like(phi)
-        ctxs = {"one": sm.Lattice(Nx, Nt), "loopback": sm.Lattice(Nx, Nt, loopback=True)}
+        make = {"one": lambda: sm.Lattice(Nx, Nt), "loopback": lambda: sm.Lattice(Nx, Nt, loopback=True),
+                "peer": lambda: sm.Lattice(Nx, Nt, loopback="peer")}
+        ctxs = {k: make[k]() for k in a.contexts.split(",")}
         times = {k: [] for k in ctxs}
         host = {k: [] for k in ctxs}  # host seconds to ENQUEUE the timed iterations (host-bound if ~ the GPU time)
         for L in ctxs.values():
