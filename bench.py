@@ -24,9 +24,18 @@ Multi-GPU: one process per GPU. Launched by the driver as
 `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`
 (WORLD_SIZE must equal --gpus). `python bench.py --gpus N` with no
 WORLD_SIZE spawns the N ranks itself, before anything touches the GPU.
-torch.distributed (gloo) is control plane only: the RCCL unique id, barriers
-and the max-over-ranks timing. `--transport hosted` runs the shards over the
-host-staged transport (several ranks may share one GPU; tests / rehearsal).
+torch.distributed (gloo) is control plane only: the RCCL unique id / the peer
+regions' IPC handles, barriers and the max-over-ranks timing.
+
+Transports (N > 1): `--transport peer` (the default) is the device-initiated
+one (include/sm_hip.h sm_create_peer: kernels store faces and sums straight
+into the other GPUs' regions over xGMI); before timing, every rank checks it
+against the host-staged transport on the same shard (D and D^dag bitwise, 30
+CG iterations to 1e-12) and the run falls back to RCCL if that check or the
+setup fails anywhere (the line says which ran and why). `--transport rccl`
+forces RCCL; `--transport hosted` runs the shards over the host-staged
+transport (several ranks may share one GPU; tests / rehearsal; `--device 0`
+puts peer ranks on one GPU too).
 """
 import argparse
 import ctypes
@@ -79,8 +88,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="host cores for the CPU baseline (default: this process's CPU share)")
     ap.add_argument("--cpu-iters", type=int, default=50, help="CG iterations of the CPU baseline sample")
-    ap.add_argument("--transport", choices=["rccl", "hosted"], default="rccl",
-                    help="multi-GPU wire: RCCL (production) or the host-staged test transport")
+    ap.add_argument("--transport", choices=["peer", "rccl", "hosted"], default="peer",
+                    help="multi-GPU wire: the device-initiated peer transport (checked against the host-staged "
+                         "one first, RCCL if that fails), RCCL, or the host-staged test transport")
     ap.add_argument("--device", type=int, default=None, help="override the rank -> GPU mapping")
     ap.add_argument("--cg-path", choices=list(CG_PATH_ID), default="recompute")
     ap.add_argument("--rank-timeout", type=float, default=900.0,
@@ -299,7 +309,7 @@ def load_traffic(nx, nt, build_id):
 class Shard:
     """This rank's t-shard of an Nx x Nt lattice with its fields resident in HBM."""
 
-    def __init__(self, rt, Nx, Nt, sigma):
+    def __init__(self, rt, Nx, Nt, sigma, transport=None):
         import torch
         import schwingermodel_amd as sm
         from schwingermodel_amd import dist as smd
@@ -307,9 +317,10 @@ class Shard:
         world, rank, device = rt["world"], rt["rank"], rt["device"]
         if Nt % world:
             raise SystemExit(f"Nt={Nt} is not divisible by {world} GPUs")
+        self.kind = (transport or rt["transport"]) if world > 1 else None
         self.transport = None
-        if world > 1 and rt["transport"] == "hosted":
-            ctx, self.transport = smd.create_hosted_context(Nx, Nt, device=device)
+        if world > 1 and self.kind in ("hosted", "peer"):
+            ctx, self.transport = smd.create_shard_context(Nx, Nt, device=device, transport=self.kind)
             L = sm.Lattice.__new__(sm.Lattice)
             L.ctx, L.Nx, L.Nt, L.Wt, L.t0 = ctx, Nx, Nt, Nt // world, rank * (Nt // world)
             L.V, L.shard, L.nshard = Nx * L.Wt, rank, world
@@ -335,6 +346,73 @@ class Shard:
 
     def close(self):
         self.L.close()
+
+
+def peer_check(rt, sh, m0, iters=30):
+    """The peer transport against the host-staged one on this rank's shard,
+    before anything is timed: D and D^dag of the bench RHS must be bitwise
+    equal, and `iters` CG iterations (tol 0, same x0) within 1e-12 of each
+    other (the passes' partial sums are added in another tile order, so the
+    iterates agree to rounding). Every rank runs it; the verdict is the worst
+    over ranks. A stale or missing face anywhere shows as a bitwise mismatch
+    of D on the shard that read it."""
+    import torch
+    sm = sh.sm
+    from schwingermodel_amd import dist as smd
+    ctx_h, tr_h = smd.create_hosted_context(sh.Nx, sh.Nt, device=rt["device"])
+    outs = {}
+    try:
+        sm.check(sm.lib.sm_set_stream(ctx_h, ctypes.c_void_p(rt["stream"].cuda_stream)))
+        sm.check(sm.lib.sm_upload_gauge_dev(ctx_h, sh.p(sh.U)))
+        for name, ctx in (("peer", sh.L.ctx), ("hosted", ctx_h)):
+            o = [torch.empty_like(sh.phi) for _ in range(2)]
+            for dag in (0, 1):
+                sm.check(sm.lib.sm_dirac_dev(ctx, sh.p(sh.phi), sh.p(o[dag]), m0, dag))
+            x = torch.empty_like(sh.phi)
+            sm.check(sm.lib.sm_cg_begin(ctx, sh.p(sh.phi), sh.p(x), m0, 0.0))
+            sm.check(sm.lib.sm_cg_iterate(ctx, iters))
+            res = sm.CGResult()
+            sm.check(sm.lib.sm_cg_finish(ctx, ctypes.byref(res)))
+            torch.cuda.synchronize()
+            outs[name] = (o, x, res.iterations)
+    finally:
+        sm.lib.sm_destroy(ctx_h)
+        del tr_h
+    (op, xp, ip), (oh, xh, ih) = outs["peer"], outs["hosted"]
+    d_bad = float(not (torch.equal(op[0], oh[0]) and torch.equal(op[1], oh[1])))
+    num, den = float(torch.sum((xp - xh) ** 2)), float(torch.sum(xh ** 2))
+    bad, it_bad, num, den = max_over_ranks(rt, [d_bad, float(ip != ih), num, den])
+    # (the max of the per-rank sums bounds the global ones' ratio within a factor N)
+    rel = (num / den) ** 0.5 if den > 0 else float("inf")
+    ok = bad == 0.0 and it_bad == 0.0 and rel <= 1e-12
+    return {"against": "host-staged transport, same shard", "D_Ddag_bitwise": bad == 0.0,
+            "cg_iterations": iters, "cg_x_rel": rel, "ok": ok}
+
+
+def make_shard(args, rt, Nx, Nt, sigma, m0):
+    """This rank's shard over args.transport; for the peer transport (N > 1)
+    after peer_check, falling back to RCCL on every rank if the setup or the
+    check failed on any. Returns (shard, check report or None)."""
+    if rt["world"] == 1 or args.transport != "peer":
+        return Shard(rt, Nx, Nt, sigma), None
+    err, sh, chk = "", None, None
+    try:
+        sh = Shard(rt, Nx, Nt, sigma, "peer")
+    except Exception as e:  # noqa: BLE001 -- every rank must reach the vote below
+        err = f"peer setup: {e}"
+    (bad,) = max_over_ranks(rt, [float(bool(err))])
+    if not bad:
+        chk = peer_check(rt, sh, m0)
+        if not chk["ok"]:
+            err = "peer transport differs from the host-staged one"
+    elif not err:
+        err = "peer setup failed on another rank"
+    if not err:
+        return sh, chk
+    print(f"[bench] rank {rt['rank']}: {err}; falling back to RCCL", file=sys.stderr, flush=True)
+    if sh is not None:
+        sh.close()
+    return Shard(rt, Nx, Nt, sigma, "rccl"), dict(chk or {}, fallback="rccl", reason=err)
 
 
 def _fill(sm, Nx, Nt, t0, Wt, sigma, U, chi, nthreads=8):
@@ -406,26 +484,27 @@ def placement_report(sh):
 
 
 def check_rccl_world(transport, world, nmin, nmax):
-    """The RCCL world the communicators themselves report (sm_comm_info:
-    ncclCommCount), min and max over ranks, against the job: under
-    --transport rccl with N > 1 every rank's communicator must hold exactly
-    WORLD_SIZE ranks, or the line would describe a job that did not run.
-    Returns None when it holds, else the reason."""
-    if transport == "rccl" and world > 1 and not nmin == nmax == world:
-        return f"RCCL communicators hold {nmin}..{nmax} ranks, WORLD_SIZE is {world}"
+    """The world the transport itself reports (sm_comm_info: ncclCommCount of
+    the RCCL communicator, or the shards the peer transport connected), min and
+    max over ranks, against the job: with N > 1 every rank's RCCL / peer world
+    must hold exactly WORLD_SIZE ranks, or the line would describe a job that
+    did not run. Returns None when it holds, else the reason."""
+    if transport in ("rccl", "peer") and world > 1 and not nmin == nmax == world:
+        return f"{transport} worlds hold {nmin}..{nmax} ranks, WORLD_SIZE is {world}"
     return None
 
 
 def comm_world(args, rt, sh):
-    """{"transport", "rccl_ranks": [min, max] over ranks} from sm_comm_info;
-    exits non-zero when RCCL's own count differs from WORLD_SIZE."""
+    """{"transport", "rccl_ranks" | "peer_ranks": [min, max] over ranks} from
+    sm_comm_info (the transport that actually runs, after any fallback);
+    exits non-zero when its own count differs from WORLD_SIZE."""
     transport, n, _ = sh.L.comm_info()
     mx, neg_mn = max_over_ranks(rt, [float(n), float(-n)])
     nmin, nmax = int(-neg_mn), int(mx)
-    why = check_rccl_world(args.transport, rt["world"], nmin, nmax)
+    why = check_rccl_world(transport, rt["world"], nmin, nmax)
     if why:
         raise SystemExit(f"[bench] {why}: refusing to report this run")
-    return {"transport": transport, "rccl_ranks": [nmin, nmax]}
+    return {"transport": transport, ("peer_ranks" if transport == "peer" else "rccl_ranks"): [nmin, nmax]}
 
 
 def cg_bytes_per_site(sh, cg_path):
@@ -515,6 +594,10 @@ def true_relres(sh, m0):
     return float(np.sqrt(rr[0] / pp[0]))
 
 
+WIRES = {"rccl": " (RCCL halos over xGMI)", "peer": " (device-initiated stores over xGMI)",
+         "hosted": " (host-staged halos)"}
+
+
 def base_line(args, rt, cfg, Nx, Nt, sh):
     world = rt["world"]
     return {
@@ -531,9 +614,8 @@ def base_line(args, rt, cfg, Nx, Nt, sh):
                                                  else ""),
                    "Nx": Nx, "Nt": Nt, "m0": cfg["m0"], "sigma": cfg["sigma"],
                    "sites_per_gpu": sh.V, "shard": f"{Nx}x{sh.Wt}",
-                   "transport": args.transport if world > 1 else None,
-                   "parallelism": f"t-shard x{world}" + ((" (RCCL halos over xGMI)" if args.transport == "rccl"
-                                                          else " (host-staged halos)") if world > 1 else "")},
+                   "transport": sh.kind if world > 1 else None,
+                   "parallelism": f"t-shard x{world}" + (WIRES[sh.kind] if world > 1 else "")},
     }
 
 
@@ -542,7 +624,7 @@ def run_config34(args, rt, cfg_id):
     cfg = CONFIGS[cfg_id]
     Nx, Nt = args.nx or cfg["Nx"], args.nt or cfg["Nt"]
     m0, world, rank = cfg["m0"], rt["world"], rt["rank"]
-    sh = Shard(rt, Nx, Nt, cfg["sigma"])
+    sh, tcheck = make_shard(args, rt, Nx, Nt, cfg["sigma"], m0)
     placement = placement_report(sh)
     world_seen = comm_world(args, rt, sh)
     begin_cg(sh, m0, args.cg_path, args.no_link_angles)
@@ -561,7 +643,7 @@ def run_config34(args, rt, cfg_id):
     if not args.no_weak:
         # config 4's weak-scaling curve: 4096 x 512N sites, 4096 x 512 per GPU
         wNt = (Nt // 8) * world
-        shw = Shard(rt, Nx, wNt, cfg["sigma"])
+        shw = Shard(rt, Nx, wNt, cfg["sigma"], sh.kind)
         tw, _ = time_cg_steps(rt, shw, m0, args.cg_path, args.warmup, args.steps, args.no_link_angles)
         (tw,) = max_over_ranks(rt, [tw])
         weak = {"lattice": f"{Nx}x{wNt}", "sites_per_gpu": shw.V, "ms_per_step": round(1e3 * tw / args.steps, 4),
@@ -613,6 +695,8 @@ def run_config34(args, rt, cfg_id):
         "placement_probe": placement,
         "comm": world_seen,
     })
+    if tcheck is not None:
+        line["comm"]["transport_check"] = tcheck
     print(json.dumps(line), flush=True)
 
 
@@ -621,7 +705,7 @@ def run_config5(args, rt):
     Nx, Nt = args.nx or cfg["Nx"], args.nt or cfg["Nt"]
     m0, world, rank = cfg["m0"], rt["world"], rt["rank"]
     sm = None
-    sh = Shard(rt, Nx, Nt, cfg["sigma"])
+    sh, tcheck = make_shard(args, rt, Nx, Nt, cfg["sigma"], m0)
     placement = placement_report(sh)
     world_seen = comm_world(args, rt, sh)
     sm = sh.sm
@@ -660,6 +744,8 @@ def run_config5(args, rt):
         "placement_probe": placement,
         "comm": world_seen,
     })
+    if tcheck is not None:
+        line["comm"]["transport_check"] = tcheck
     print(json.dumps(line), flush=True)
     if not res.converged or not rel < 1e-9:
         raise SystemExit(f"config 5: converged={res.converged} true relres {rel:.3e}")
@@ -689,6 +775,8 @@ def main():
     ndev = torch.cuda.device_count()  # does not initialise the GPU on this image
     if args.device is not None:
         device = args.device
+        if args.transport == "rccl" and world > 1:
+            raise SystemExit("--device with --transport rccl: RCCL needs one GPU per rank")
     elif args.transport == "hosted":
         device = local_rank % max(1, ndev)
     else:

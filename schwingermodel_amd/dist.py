@@ -19,7 +19,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import check, lib
+from ._lib import SMError, check, lib
 
 EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long)
@@ -120,11 +120,24 @@ def create_peer_context(Nx, Nt, device=0):
     nb = lib.sm_peer_handle_bytes()
     buf = ctypes.create_string_buffer(nb)
     h = ctypes.c_void_p()
-    check(lib.sm_create_peer(ctypes.byref(h), Nx, Nt, dist.get_world_size(), dist.get_rank(), device, buf, nb))
+    err = None
+    try:
+        check(lib.sm_create_peer(ctypes.byref(h), Nx, Nt, dist.get_world_size(), dist.get_rank(), device, buf, nb))
+    except Exception as e:  # noqa: BLE001 -- the all-gather below must still run on every rank
+        err = e
     handles = [None] * dist.get_world_size()
-    dist.all_gather_object(handles, bytes(buf.raw))
+    dist.all_gather_object(handles, bytes(buf.raw) if err is None else b"")
+    if err is not None:
+        raise err
+    if any(len(x) != nb for x in handles):
+        lib.sm_destroy(h)
+        raise RuntimeError("peer transport: sm_create_peer failed on another rank")
     allh = ctypes.create_string_buffer(b"".join(handles), nb * len(handles))
-    check(lib.sm_peer_connect(h, allh, nb))
+    rc = lib.sm_peer_connect(h, allh, nb)
+    if rc != 0:
+        msg = lib.sm_last_error().decode(errors="replace")
+        lib.sm_destroy(h)
+        raise SMError(f"sm_hip error {rc}: {msg}")
     return h
 
 

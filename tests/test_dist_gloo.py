@@ -18,17 +18,21 @@ from distutil import run_world
     ("rccl:2,1", 2, None),              # one rank's communicator is alone: refused
     ("rccl:4,4,4,4", 4, [4, 4]),
     ("hosted:1,1", 2, [1, 1]),          # host-staged shards: no RCCL world, not refused
+    ("peer:2,2", 2, [2, 2]),            # the peer transport's connected view holds the job's ranks
+    ("peer:2,1", 2, None),              # one rank's view is alone: refused
 ])
 def test_bench_rccl_world_check(tmp_path, name, world, expect):
-    """bench.py reports the RCCL world the communicators themselves hold
-    (sm_comm_info -> ncclCommCount), min and max over the ranks, and refuses to
-    report an RCCL run whose communicators disagree with WORLD_SIZE."""
+    """bench.py reports the world the transport itself holds (sm_comm_info ->
+    ncclCommCount, or the peer transport's connected shards), min and max over
+    the ranks, and refuses to report an RCCL or peer run whose worlds disagree
+    with WORLD_SIZE."""
     rep = run_world("commworld", name, world, tmp_path, timeout=120)
     for r in rep["ranks"]:
         if expect is None:
             assert "refused" in r and "WORLD_SIZE is 2" in r["refused"], r
         else:
-            assert r["ok"]["rccl_ranks"] == expect, r
+            key = "peer_ranks" if name.startswith("peer") else "rccl_ranks"
+            assert r["ok"][key] == expect and r["ok"]["transport"] == name.split(":")[0], r
 
 
 @pytest.mark.parametrize("fixture,world", [("l64x64_b2_m0", 2), ("l32x48_b3_m-0p10", 2),

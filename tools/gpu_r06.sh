@@ -148,6 +148,18 @@ k() {
     --applies 20 > gpurun_out/r06k_loopback.log 2>&1
 }
 
+# l: bench with the peer transport rehearsed on one GPU (2 and 4 ranks sharing it: the check against the
+#    host-staged transport, the path, not a scaling figure), the one-GPU bench, and the RCCL / hosted tests
+l() {
+  timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r06l_bench1.log 2>&1 &&
+  timeout -k 10 400 python3 bench.py --gpus 2 --device 0 --steps 50 --warmup 10 --no-cpu-baseline \
+    > gpurun_out/r06l_bench2_peer.log 2>&1 &&
+  timeout -k 10 400 python3 bench.py --gpus 4 --device 0 --steps 50 --warmup 10 --no-cpu-baseline --no-weak \
+    > gpurun_out/r06l_bench4_peer.log 2>&1 &&
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_rccl_loopback_gpu.py \
+    tests/test_dist_gpu.py -k "loopback_equals or sharded_gpu_path or recompute" > gpurun_out/r06l_tests.log 2>&1
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
