@@ -521,6 +521,9 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //   rccl_order=0        no ordering events between RCCL operations on the two
 //                       streams (A/B only: the one communicator then relies on
 //                       RCCL's own ordering)
+//   peer_store=0|1|2    peer transport: the CG pass's face stores as 16-B
+//                       write-through buffer stores (0), 8-B atomic stores (1)
+//                       or plain stores into the uncached ring (2)
 //   ra_strip=0|1        recompute-Ad pass: the block's 4 waves share one t-strip
 //                       (one shard; ignored on t-shards)
 //   ra_xbal=0|1         recompute-Ad pass: balanced x-chunks (Nx / XB rows)
@@ -580,6 +583,9 @@ static int apply_test_opts(sm_ctx *c) {
             c->apply_split = iv ? 1 : 0;
         } else if (k == "rccl_order") {
             c->rccl_ordered = iv ? 1 : 0;
+        } else if (k == "peer_store") {
+            if (iv < 0 || iv > 2) return fail(SM_ERR_ARG, "SM_TEST_OPTS: peer_store must be 0, 1 or 2");
+            c->peer_store = iv;
         } else if (k == "ra_strip") {
             cg_ra_set_strip(c->racfg, c->g, iv);
         } else if (k == "ra_xbal") {
@@ -1294,7 +1300,7 @@ static int cg_ra_pass_peer(sm_ctx *c, const double2 *d1, const double2 *d2, doub
     const int lb = launch_cg_ra(c->stream, c->g, fc, c->kshards(), d1, d2, dn, c->cg_x, c->U, f1, f2, face4_recv_U(c),
                                 c->cg_mass, j, c->sc, c->partials, 0, fc.TBk, nullptr, ua, c->Uang_face, fs, 0,
                                 c->tick, nparts, c->gsum, sums, 1, c->link_fmt, fsh, c->peer_view_dev,
-                                ++c->peer_coll_seq);
+                                ++c->peer_coll_seq, c->peer_store);
     if (lb) c->cg_link_bytes_last = lb;
     c->cg_flush_pass = j;
     c->cg_flush_sums = 1;

@@ -87,8 +87,9 @@ struct RAArgs {
     int pbase;               // partial slots: tile pbase + (t-block - tb0) * XB + x-chunk
     double2 *fsend;          // SH: != null -> the edge blocks also write d_j's 4-deep send faces
     double2 *fsendh;         //   (lo part at fsend, hi part at fsendh)
-    const PeerView *peer;    // peer transport: faces as system-scope stores, the tail all-reduces (pseq)
-    unsigned long long pseq;
+    const PeerView *peer;    // peer transport: faces as 16-B write-through stores into the neighbours'
+    unsigned long long pseq; //   rings, the tail all-reduces the sums (collective pseq)
+    int pstore;              //   face store form: 0 16-B buffer stores sc0 sc1, 1 8-B atomic, 2 plain (A/B)
     // TK (ticketed tail): counters tick[0] (groups) and tick[1 + g] (64 tiles
     // each), ntiles tiles over every launch of the pass, group sums gsum; the
     // last block forms the scalars (out3 == null) or writes the 3 sums to out3
@@ -454,11 +455,26 @@ __device__ __forceinline__ void ra_march(const RAArgs &a, int cbase, int span, i
                 if (SH && a.fsend) {  // fused face pack ([col][plane][x], lo: columns 0..3, hi: Wt-4..Wt-1)
                     const int fcol = c < RH ? c : (c >= Wt - RH ? c - (Wt - RH) + RH : -1);
                     if (fcol >= 0) {
-                        double2 *fb = fcol < RH ? a.fsend + (long)(2 * fcol) * Nx : a.fsendh + (long)(2 * (fcol - RH)) * Nx;
-                        if (a.peer) {  // into the neighbour's region: write-through (sm_peer.h)
-                            sys_st2(fb + Xr, J2.a);
-                            sys_st2(fb + Nx + Xr, J2.b);
+                        if (a.peer && a.pstore == 0) {  // into the neighbour's ring: 16-B write-through stores
+                            // (sm_peer.h; one resource per side, both from kernel arguments: uniform)
+                            const __amdgpu_buffer_rsrc_t rlo = sys_rsrc(a.fsend, 16u * 8u * Nx);
+                            const __amdgpu_buffer_rsrc_t rhi = sys_rsrc(a.fsendh, 16u * 8u * Nx);
+                            const int fo = 16 * ((fcol & (RH - 1)) * 2 * Nx + Xr);
+                            if (fcol < RH) {
+                                sys_st16(rlo, fo, J2.a);
+                                sys_st16(rlo, fo + 16 * Nx, J2.b);
+                            } else {
+                                sys_st16(rhi, fo, J2.a);
+                                sys_st16(rhi, fo + 16 * Nx, J2.b);
+                            }
+                        } else if (a.peer && a.pstore == 1) {  // 8-B write-through (atomic) stores (A/B)
+                            double2 *fb = fcol < RH ? a.fsend + (long)(2 * fcol) * Nx : a.fsendh + (long)(2 * (fcol - RH)) * Nx;
+                            sys_st(&fb[Xr].x, J2.a.x);
+                            sys_st(&fb[Xr].y, J2.a.y);
+                            sys_st(&fb[Nx + Xr].x, J2.b.x);
+                            sys_st(&fb[Nx + Xr].y, J2.b.y);
                         } else {
+                            double2 *fb = fcol < RH ? a.fsend + (long)(2 * fcol) * Nx : a.fsendh + (long)(2 * (fcol - RH)) * Nx;
                             fb[Xr] = J2.a;
                             fb[Nx + Xr] = J2.b;
                         }
@@ -741,7 +757,8 @@ int launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsha
                   const double2 *f2, const double2 *fU, double mass, long pass, CGScalars *sc, double2 *partials,
                   int tb0, int tbn, const double2 *prev_partials, const double *Uang, const double *fUang,
                   double2 *fsend, int pbase, unsigned *tick, int ntiles, double2 *gsum, double2 *out3,
-                  int red_sums, int link_fmt, double2 *fsendh, const PeerView *peer, unsigned long long pseq) {
+                  int red_sums, int link_fmt, double2 *fsendh, const PeerView *peer, unsigned long long pseq,
+                  int pstore) {
     if (tbn <= 0) return 0;
     RAArgs a;
     a.d1 = d1; a.d2 = d2; a.dn = dn; a.x = x; a.U = U;
@@ -767,6 +784,7 @@ int launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsha
     a.fsendh = fsendh ? fsendh : (fsend ? fsend + 8 * (long)g.Nx : nullptr);
     a.peer = peer;
     a.pseq = pseq;
+    a.pstore = pstore;
     a.pbase = pbase;
     a.tick = tick;
     a.ntiles = ntiles;

@@ -136,6 +136,7 @@ struct sm_ctx {
     sm::PeerView *peer_view_dev = nullptr;  // device copy (the CG pass's tail)
     unsigned long long peer_coll_seq = 0, peer_face_seq = 0;  // the next collective / face exchange is seq + 1
     unsigned *peer_tick = nullptr;  // zeroed ticket counter of the transport kernels
+    int peer_store = 0;             // CG pass face stores: 0 16-B write-through, 1 8-B atomic, 2 plain (test option)
     bool hosted = false;            // host-callback transport instead of RCCL
     sm_host_transport tr{};
     double *h_face = nullptr;       // pinned: send_lo, send_hi, recv_lo, recv_hi (4 x up to 8Nx doubles)

@@ -69,9 +69,17 @@ __device__ __forceinline__ PeerHdr *peer_hdr(const PeerView &v, int r) { return 
 __device__ __forceinline__ void sys_st(double *p, double v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ void sys_st2(double2 *p, double2 v) {
-    sys_st(&p->x, v.x);
-    sys_st(&p->y, v.y);
+// 16-byte write-through store at system scope (buffer_store_dwordx4 ... sc0
+// sc1) at byte offset `off` of a raw buffer resource: the face payloads, one
+// coalesced 16-B element per lane (a wave covers 1 KiB of consecutive rows).
+typedef unsigned int sm_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sys_rsrc(void *base, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000);  // gfx9 raw-buffer dword3
+}
+__device__ __forceinline__ void sys_st16(__amdgpu_buffer_rsrc_t r, int off, double2 v) {
+    sm_v4u w;
+    __builtin_memcpy(&w, &v, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 17);  // cache policy SC0 | SC1
 }
 __device__ __forceinline__ double sys_ld(const double *p) {
     return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

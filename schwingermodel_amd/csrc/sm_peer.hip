@@ -97,11 +97,11 @@ __global__ void __launch_bounds__(256) peer_pack_proj_kernel(int Nx, int Wt, lon
     double2 *down_hi = reinterpret_cast<double2 *>(v.base[v.down] + peer_apply_off(Nx, slot)) + Nx;
     double2 *up_lo = reinterpret_cast<double2 *>(v.base[v.up] + peer_apply_off(Nx, slot));
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < 2 * Nx) {
-        const int x = i >> 1, side = i & 1;
+    if (i < 2 * Nx) {  // side-major: a wave's 64 rows of one side, 1 KiB of consecutive stores
+        const int side = i >= Nx, x = side ? i - Nx : i;
         const long n = (long)x * Wt + (side ? Wt - 1 : 0);
         const double2 val = proj_face_value(kind, side, f[n], f[n + V], U + n);
-        sys_st2(side ? up_lo + x : down_hi + x, val);
+        sys_st16(sys_rsrc(side ? up_lo : down_hi, 16u * (unsigned)Nx), 16 * x, val);
     }
     peer_face_handoff(v, seq, tick);
 }

@@ -26,7 +26,13 @@ from test_rccl_loopback_gpu import fields, run_all
 
 pytestmark = pytest.mark.gpu
 
-PEER = {"SM_WORKER_TRANSPORT": "peer"}
+# One hardware queue per worker process: 2-8 processes share the one GPU here, and
+# each spins one wave in a publishing kernel until the others' kernels have run.
+# With several queues per process the GPU's hardware queue slots run out at 8
+# processes and the scheduler time-slices whole queues, which can stretch a
+# wait by orders of magnitude (a round-6 8-process run hit the time limits).
+# Production runs one process per GPU.
+PEER = {"SM_WORKER_TRANSPORT": "peer", "GPU_MAX_HW_QUEUES": "1"}
 
 
 @pytest.fixture(scope="module")
@@ -157,7 +163,7 @@ def test_peer_world_matches_reference(tmp_path, fixture, world):
     """D, D^dag, D D^dag and the force bitwise against the reference; CG (the
     one-launch peer pass) in the reference's iterations to 1e-12; the same dot
     on every shard; sm_comm_info = (peer, world, rank)."""
-    rep = run_world("gpu", fixture, world, tmp_path, timeout=160, extra_env=PEER)
+    rep = run_world("gpu", fixture, world, tmp_path, timeout=220, extra_env=PEER)
     c = rep["checks"]
     for k in ("ref_Dpsi", "ref_Ddagchi", "ref_DDdagpsi", "ref_force"):
         assert c[k] is True, (k, c)

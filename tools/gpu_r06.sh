@@ -160,6 +160,41 @@ l() {
     tests/test_dist_gpu.py -k "loopback_equals or sharded_gpu_path or recompute" > gpurun_out/r06l_tests.log 2>&1
 }
 
+# m: peer faces staged in LDS and written out coalesced -- the peer tests, the loopback probe, and the
+#    one-GPU bench against the library before the peer transport (tools/ab_libs/libsm_hip_pre_peer.so), ABAB
+m() {
+  timeout -k 10 900 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_peer_gpu.py \
+    > gpurun_out/r06m_tests.log 2>&1 &&
+  timeout -k 10 400 python -u tools/loopback_probe.py --shapes 4096x512,4096x1024,4096x2048 --iters 200 --rounds 3 \
+    --applies 20 > gpurun_out/r06m_loopback.log 2>&1 || return 1
+  local B="python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --evolved-trajectories 0"
+  for i in 1 2; do
+    timeout -k 10 300 $B >> gpurun_out/r06m_ab_new.jsonl 2>> gpurun_out/r06m_ab.err &&
+    SM_LIB_PATH=$PWD/tools/ab_libs/libsm_hip_pre_peer.so SM_LIB_AB=1 timeout -k 10 300 $B \
+      >> gpurun_out/r06m_ab_old.jsonl 2>> gpurun_out/r06m_ab.err || return 1
+  done
+}
+
+# n: the peer tests and the loopback probe (plain / RCCL / peer) on the current build
+n() {
+  timeout -k 10 900 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_peer_gpu.py \
+    > gpurun_out/r06n_tests.log 2>&1 &&
+  timeout -k 10 400 python -u tools/loopback_probe.py --shapes 4096x512,4096x1024,4096x2048 --iters 200 --rounds 3 \
+    --applies 20 > gpurun_out/r06n_loopback.log 2>&1
+}
+
+# o: the peer pass's face-store forms A/B on the peer loopback (16-B write-through, 8-B atomic, plain), twice
+o() {
+  local L="python -u tools/loopback_probe.py --shapes 4096x512,4096x1024,4096x2048 --iters 200 --rounds 3 --applies 5 --contexts one,peer"
+  for i in 1 2; do
+    for m in 0 1 2; do
+      SM_TEST_OPTS=peer_store=$m timeout -k 10 300 $L > gpurun_out/r06o_store${m}_$i.log 2>&1 || return 1
+    done
+  done
+  SM_TEST_OPTS=peer_store=2 timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread \
+    tests/test_peer_gpu.py > gpurun_out/r06o_tests_plain.log 2>&1
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
