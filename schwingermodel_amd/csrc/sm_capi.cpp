@@ -768,6 +768,12 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     } else if (c->peer) {
         // connected by sm_peer_connect (the loopback: here, to itself)
     } else if (c->sharded()) {
+        // RCCL's mixing of graph-captured and eager launches on one communicator
+        // costs every launch a cross-stream dependency; nothing here is captured
+        // (RCCL loopback, ms per CG iteration: 4096x512 0.0911 against 0.0944,
+        // 4096x1024 0.1542 against 0.1613; profiles/r06_j_rccl_launch_env.jsonl).
+        // A caller's own setting wins.
+        setenv("NCCL_GRAPH_MIXING_SUPPORT", "0", 0);
         ncclUniqueId id;
         memcpy(&id, unique_id, sizeof id);
         ncclResult_t r = ncclCommInitRank(&c->comm, nshard, id, shard);

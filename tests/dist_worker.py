@@ -597,6 +597,37 @@ def run_commworld(name, result_path, dist, rank, world):
     dist.destroy_process_group()
 
 
+def run_fallback(name, result_path, dist, rank, world):
+    """mode "fallback" (CPU, gloo): bench.make_shard's agreement over real
+    ranks with stand-in shards. `name`: "ok", "setup:<rank>" (creating the
+    peer shard raises on that rank only) or "check" (the peer check fails).
+    Every rank must end on the same transport: peer, or RCCL with a reason."""
+    sys.path.insert(0, REPO)
+    import argparse
+    import bench
+
+    class FakeShard:
+        def __init__(self, rt, Nx, Nt, sigma, transport=None):
+            if transport == "peer" and name.startswith("setup:") and rank == int(name.split(":")[1]):
+                raise RuntimeError("stand-in peer setup failure")
+            self.kind = transport or "rccl"
+
+        def close(self):
+            pass
+
+    bench.Shard = FakeShard
+    bench.peer_check = lambda rt, sh, m0: {"ok": name != "check"}
+    rt = {"world": world, "rank": rank, "transport": "peer"}
+    sh, chk = bench.make_shard(argparse.Namespace(transport="peer"), rt, 64, 64, 0.1, -0.1)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, {"kind": sh.kind, "check": chk})
+    if rank == 0:
+        with open(result_path, "w") as f:
+            json.dump({"world": world, "ranks": gathered}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     mode, name, result_path = sys.argv[1], sys.argv[2], sys.argv[3]
     import datetime
@@ -617,6 +648,8 @@ def main():
         return run_big(name, result_path, dist, rank, world)
     if mode == "commworld":
         return run_commworld(name, result_path, dist, rank, world)
+    if mode == "fallback":
+        return run_fallback(name, result_path, dist, rank, world)
     from conftest import bits_equal, load_fixture
     import schwingermodel_amd as sm
     from schwingermodel_amd import dist as smd

@@ -35,6 +35,21 @@ def test_bench_rccl_world_check(tmp_path, name, world, expect):
             assert r["ok"][key] == expect and r["ok"]["transport"] == name.split(":")[0], r
 
 
+@pytest.mark.parametrize("case,world", [("ok", 2), ("setup:1", 2), ("setup:0", 3), ("check", 2)])
+def test_bench_peer_fallback_agreement(tmp_path, case, world):
+    """bench.py's N > 1 default: the peer transport after its check against the
+    host-staged one, RCCL on EVERY rank if the setup failed on any rank or the
+    check failed (a mixed world would deadlock its first collective)."""
+    rep = run_world("fallback", case, world, tmp_path, timeout=120)
+    kinds = {r["kind"] for r in rep["ranks"]}
+    if case == "ok":
+        assert kinds == {"peer"} and all(r["check"]["ok"] for r in rep["ranks"]), rep
+    else:
+        assert kinds == {"rccl"}, rep
+        for r in rep["ranks"]:
+            assert r["check"]["fallback"] == "rccl" and r["check"]["reason"], r
+
+
 @pytest.mark.parametrize("fixture,world", [("l64x64_b2_m0", 2), ("l32x48_b3_m-0p10", 2),
                                            ("l32x48_hot_m0", 4), ("l16x16_b2_m-0p19", 8)])
 def test_sharded_operator_matches_reference(tmp_path, fixture, world):
