@@ -1306,7 +1306,10 @@ static int cg_ra_pass_peer(sm_ctx *c, const double2 *d1, const double2 *d2, doub
     const int lb = launch_cg_ra(c->stream, c->g, fc, c->kshards(), d1, d2, dn, c->cg_x, c->U, f1, f2, face4_recv_U(c),
                                 c->cg_mass, j, c->sc, c->partials, 0, fc.TBk, nullptr, ua, c->Uang_face, fs, 0,
                                 c->tick, nparts, c->gsum, sums, 1, c->link_fmt, fsh, c->peer_view_dev,
-                                ++c->peer_coll_seq, c->peer_store);
+                                ++c->peer_coll_seq, c->peer_store,
+                                // the shape's march schedule where a one-shard pass of this grid takes it
+                                // (the ticketed tail, not the redundant scalars of small grids)
+                                nparts > c->cg_ra_red_max_blocks ? 1 : 0);
     if (lb) c->cg_link_bytes_last = lb;
     c->cg_flush_pass = j;
     c->cg_flush_sums = 1;

@@ -715,7 +715,8 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
 
 template <int SH, int RED, int UC, int F>
 static void ra_go(int xp, int tk, dim3 grid, dim3 block, size_t lds, hipStream_t s, const RAArgs &a, int rev = 0) {
-    if constexpr (F == 2 && SH == 0 && RED == 0) {
+    // march schedules: one-shard tail passes, and the peer transport's one-launch t-shard pass
+    if constexpr (F == 2 && ((SH == 0 && RED == 0) || (SH == 1 && RED == 2))) {
         if (tk && rev == 1) {
             if (xp) hipLaunchKernelGGL((cg_ra_kernel<SH, 1, F, RED, UC, 1, 1>), grid, block, lds, s, a);
             else hipLaunchKernelGGL((cg_ra_kernel<SH, 0, F, RED, UC, 1, 1>), grid, block, lds, s, a);
@@ -758,7 +759,7 @@ int launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsha
                   int tb0, int tbn, const double2 *prev_partials, const double *Uang, const double *fUang,
                   double2 *fsend, int pbase, unsigned *tick, int ntiles, double2 *gsum, double2 *out3,
                   int red_sums, int link_fmt, double2 *fsendh, const PeerView *peer, unsigned long long pseq,
-                  int pstore) {
+                  int pstore, int sched) {
     if (tbn <= 0) return 0;
     RAArgs a;
     a.d1 = d1; a.d2 = d2; a.dn = dn; a.x = x; a.U = U;
@@ -812,9 +813,23 @@ int launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsha
     }
     const bool sh = nshard > 1;
     if (red_sums && sh && f == 2 && tk) {  // t-shards: scalars from pass j-1's all-reduced sums (sc->sumr)
-        if (uc == 2) ra_go<1, 2, 2, 2>(xp, tk, grid, block, lds, s, a);
-        else if (uc) ra_go<1, 2, 1, 2>(xp, tk, grid, block, lds, s, a);
-        else ra_go<1, 2, 0, 2>(xp, tk, grid, block, lds, s, a);
+        // the peer transport's pass is one launch over every t-block, so it can
+        // take the shape's march schedule (sched: where a one-shard pass of the
+        // same grid would, i.e. with the ticketed tail) as a one-shard pass does (odd passes
+        // in reverse tile order, marching backwards; rev 2: x-adjacent chunks
+        // in opposite directions); the split RCCL / host-staged launches cannot
+        int prev = 0;
+        if (sched && tb0 == 0 && tbn == c.TBk && c.rev_odd == 1 && (pass & 1)) {
+            prev = 1;
+            a.flip = 1;
+        } else if (sched && tb0 == 0 && tbn == c.TBk && c.rev_odd == 2) {
+            prev = 2;
+            a.flip = (int)(pass & 1);
+            a.alt = 1;
+        }
+        if (uc == 2) ra_go<1, 2, 2, 2>(xp, tk, grid, block, lds, s, a, prev);
+        else if (uc) ra_go<1, 2, 1, 2>(xp, tk, grid, block, lds, s, a, prev);
+        else ra_go<1, 2, 0, 2>(xp, tk, grid, block, lds, s, a, prev);
         return link_bytes;
     }
     // one shard with the ticketed tail: odd passes take the tiles in reverse

@@ -195,6 +195,15 @@ o() {
     tests/test_peer_gpu.py > gpurun_out/r06o_tests_plain.log 2>&1
 }
 
+# p: the peer pass with the shape's march schedule -- peer tests, the loopback probe, then the full gate
+p() {
+  timeout -k 10 900 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_peer_gpu.py \
+    > gpurun_out/r06p_tests.log 2>&1 &&
+  timeout -k 10 400 python -u tools/loopback_probe.py --shapes 4096x512,4096x1024,4096x2048 --iters 200 --rounds 3 \
+    --applies 5 --contexts one,peer > gpurun_out/r06p_loopback.log 2>&1 &&
+  gate p
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
