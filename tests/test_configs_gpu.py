@@ -81,16 +81,21 @@ def test_config_single_gpu_cg(oracle, N, sigma, m0, modes, xtol):
 
 
 @pytest.mark.multiproc
+@pytest.mark.parametrize("transport", ["hosted", "peer"])
 @pytest.mark.parametrize("case,world,xtol", [
     ("big:4096x4096:0.2374:-0.06:full", 8, 1e-12),   # config 4: Wt = 512 per shard
     ("big:8192x8192:0.4242:-0.19:cg", 8, 2.2e-12),   # config 5: 8192 x 1024 per shard
 ])
-def test_config_sharded_vs_one_shard(tmp_path, case, world, xtol):
+def test_config_sharded_vs_one_shard(tmp_path, case, world, xtol, transport):
     """xtol against the one-shard solve: config 5's is the reference's own
     spread between two decompositions (2.2e-12, manifest
     reference_decomposition_spread), the band a different summation order of
-    the dots moves x by after 4556 iterations near m_crit."""
-    rep = run_world("big", case, world, tmp_path, timeout=160)
+    the dots moves x by after 4556 iterations near m_crit. transport: the
+    host-staged one, or the peer transport (the bench's multi-GPU default:
+    eight processes on the one GPU mapping each other's regions, one hardware
+    queue each as in tests/test_peer_gpu.py)."""
+    env = {"SM_WORKER_TRANSPORT": "peer", "GPU_MAX_HW_QUEUES": "1"} if transport == "peer" else None
+    rep = run_world("big", case, world, tmp_path, timeout=240, extra_env=env)
     print(json.dumps({k: v for k, v in rep.items() if k != "bitwise"}))
     for k, ok in rep["bitwise"].items():
         assert ok is True, (k, rep)

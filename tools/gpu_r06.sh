@@ -204,6 +204,12 @@ p() {
   gate p
 }
 
+# q: configs 4 and 5 at full size over the peer transport (8 processes on the one GPU)
+q() {
+  timeout -k 10 900 python -u -m pytest -x -v -s --timeout 600 --timeout-method thread tests/test_configs_gpu.py \
+    -k "sharded and peer" > gpurun_out/r06q_tests.log 2>&1
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
