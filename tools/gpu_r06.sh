@@ -219,13 +219,16 @@ fin() {
   python3 -c "import schwingermodel_amd as s; print(s.lib.sm_build_id().decode())" > gpurun_out/build_id_$T.txt &&
   timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver_$T.log 2>&1 &&
   timeout -k 10 400 python3 bench.py > gpurun_out/bench_$T.log 2>&1 &&
-  timeout -k 10 300 python3 bench.py --gpus 2 --transport hosted --steps 50 --warmup 10 --no-weak > gpurun_out/bench2_$T.log 2>&1 &&
+  timeout -k 10 300 python3 bench.py --gpus 2 --device 0 --steps 50 --warmup 10 --no-weak > gpurun_out/bench2_$T.log 2>&1 &&
+  GPU_MAX_HW_QUEUES=1 timeout -k 10 400 python3 bench.py --gpus 8 --device 0 --steps 50 --warmup 10 --no-weak \
+    --no-cpu-baseline > gpurun_out/bench8_$T.log 2>&1 &&
   timeout -k 10 300 python3 bench.py --config 5 > gpurun_out/bench_c5_$T.log 2>&1 &&
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_stats_$T -o run -- python3 bench.py --steps 200 --warmup 20 --applies 20 --no-cpu-baseline --no-weak --evolved-trajectories 0 > gpurun_out/prof_stats_$T.log 2>&1 &&
   python3 tools/step_gap.py gpurun_out/prof_stats_$T/run_kernel_trace.csv --last 200 > gpurun_out/step_gap_$T.log 2>&1 &&
   timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch_$T -o run -- $P > gpurun_out/prof_fetch_$T.log 2>&1 &&
   timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write_$T -o run -- $P > gpurun_out/prof_write_$T.log 2>&1 &&
-  timeout -k 10 300 python -u tools/loopback_probe.py --shapes 4096x512,4096x1024,4096x2048,4096x4096 --iters 100 --rounds 2 > gpurun_out/loopback_$T.log 2>&1 &&
+  timeout -k 10 400 python -u tools/loopback_probe.py --shapes 4096x512,4096x1024,4096x2048,4096x4096 --iters 100 --rounds 2 \
+    --contexts one,loopback,peer > gpurun_out/loopback_$T.log 2>&1 &&
   timeout -k 10 300 python -u tools/probe_trials.py --n 10 --hold 5 > gpurun_out/probe_trials_$T.jsonl 2>&1
 }
 
