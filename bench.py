@@ -598,6 +598,24 @@ WIRES = {"rccl": " (RCCL halos over xGMI)", "peer": " (device-initiated stores o
          "hosted": " (host-staged halos)"}
 
 
+def timed_solve_check(sh, m0):
+    """N > 1: the timed solve checked against itself after the timing. The CG's
+    recursive residual (sqrt <r,r> from the device scalars, the same on every
+    shard) must agree with the true residual ||phi - D D^dag x|| / ||phi|| of
+    the x the passes built: a face or a sum lost or stale in any timed pass
+    on any shard breaks that agreement, whatever the transport. After ~200
+    iterations at tol 0 the two differ by rounding (~1e-13 of ||phi||) against
+    a residual of ~1e-3, so the bar (1e-6 relative) is loose and still catches
+    any wrong pass."""
+    sm = sh.sm
+    res = sm.CGResult()
+    sm.check(sm.lib.sm_cg_finish(sh.L.ctx, ctypes.byref(res)))
+    rec = res.residual / res.phi_norm if res.phi_norm else float("nan")
+    true = true_relres(sh, m0)
+    ok = abs(true - rec) <= 1e-6 * rec
+    return {"recursive_relres": rec, "true_relres": true, "ok": bool(ok)}
+
+
 def base_line(args, rt, cfg, Nx, Nt, sh):
     world = rt["world"]
     return {
@@ -631,6 +649,7 @@ def run_config34(args, rt, cfg_id):
     apply_time = time_applies(rt, sh, m0, args.applies)
     t_cg, cg_bps = time_cg_steps(rt, sh, m0, args.cg_path, args.warmup, args.steps, args.no_link_angles, begun=True)
     apply_s = apply_time()
+    solve_check = timed_solve_check(sh, m0) if world > 1 else None
     t_cg, apply_s = max_over_ranks(rt, [t_cg, apply_s])
     if "probe_kept_us" in placement:
         # the probe times short bursts; the timed run sustains its own pass time
@@ -697,7 +716,11 @@ def run_config34(args, rt, cfg_id):
     })
     if tcheck is not None:
         line["comm"]["transport_check"] = tcheck
+    if solve_check is not None:
+        line["comm"]["timed_solve_check"] = solve_check
     print(json.dumps(line), flush=True)
+    if solve_check is not None and not solve_check["ok"]:
+        raise SystemExit("[bench] the timed sharded solve's recursive and true residuals disagree")
 
 
 def run_config5(args, rt):

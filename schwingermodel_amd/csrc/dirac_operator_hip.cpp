@@ -96,9 +96,9 @@ int mpi_allreduce(void *, double *buf, long n) {
 std::string transport_choice(int local_leaders, int ndev) {
     const char *e = std::getenv("SM_DROPIN_TRANSPORT");
     std::string t = e ? e : "auto";
-    if (t == "auto") t = local_leaders > ndev ? "mpi" : "rccl";
-    if (t != "mpi" && t != "rccl") {
-        std::cerr << "[sm_hip] SM_DROPIN_TRANSPORT must be auto, rccl or mpi" << std::endl;
+    if (t == "auto") t = local_leaders > ndev ? "mpi" : "peer";
+    if (t != "mpi" && t != "rccl" && t != "peer") {
+        std::cerr << "[sm_hip] SM_DROPIN_TRANSPORT must be auto, peer, rccl or mpi" << std::endl;
         MPI_Abort(MPI_COMM_WORLD, 1);
     }
     return t;
@@ -131,11 +131,19 @@ Shim &shim() {
     const int device = local % ndev;
     if (g.nshard == 1) {
         call(sm_create(&g.ctx, LV::Nx, LV::Nt, 1, 0, device, nullptr), "sm_create");
-    } else if (transport_choice(nlocal, ndev) == "mpi") {
+    } else if (const std::string t = transport_choice(nlocal, ndev); t == "mpi") {
         g.tr.user = nullptr;
         g.tr.exchange = mpi_exchange;
         g.tr.allreduce_sum = mpi_allreduce;
         call(sm_create_hosted(&g.ctx, LV::Nx, LV::Nt, g.nshard, g.shard, device, &g.tr), "sm_create_hosted");
+    } else if (t == "peer") {
+        // the device-initiated transport: the leaders all-gather their regions'
+        // IPC handles over MPI (in shard order: g.lead ranks are coords[1])
+        const int nb = sm_peer_handle_bytes();
+        std::vector<char> mine((size_t)nb), all((size_t)nb * g.nshard);
+        call(sm_create_peer(&g.ctx, LV::Nx, LV::Nt, g.nshard, g.shard, device, mine.data(), nb), "sm_create_peer");
+        MPI_Allgather(mine.data(), nb, MPI_BYTE, all.data(), nb, MPI_BYTE, g.lead);
+        call(sm_peer_connect(g.ctx, all.data(), nb), "sm_peer_connect");
     } else {
         unsigned char uid[128] = {0};
         if (g.shard == 0) call(sm_comm_unique_id(uid, sizeof uid), "sm_comm_unique_id");

@@ -83,6 +83,33 @@ def test_dropin_multirank_matches_reference(tmp_path, rx, rt):
 
 
 @pytest.mark.multiproc
+@pytest.mark.parametrize("rx,rt", [(1, 2), (2, 4)])
+def test_dropin_multirank_peer_transport(tmp_path, rx, rt):
+    """The same fixture driver with the shim's t-column leaders on the peer
+    transport (SM_DROPIN_TRANSPORT=peer: sm_create_peer, the region handles
+    all-gathered with MPI_Allgather, sm_peer_connect) -- the binding
+    INTEGRATION.md shows -- here with the leaders sharing this one GPU (one
+    hardware queue each, as in tests/test_peer_gpu.py)."""
+    exe = os.path.join(REF, "sm_dropin_32x48")
+    if not os.path.exists(exe) or not os.path.exists(MPIEXEC):
+        pytest.skip("drop-in binary or MPICH not available")
+    meta, a = load_fixture("l32x48_b3_m-0p10")
+    for k in ("U", "psi", "chi"):
+        a[k].tofile(tmp_path / f"{k}.bin")
+    e = dict(env(), SM_DROPIN_TRANSPORT="peer", GPU_MAX_HW_QUEUES="1")
+    r = subprocess.run([MPIEXEC, "-n", str(rx * rt), exe, "fixture", str(tmp_path), str(rx), str(rt),
+                        repr(meta["m0"]), "1e-10", "10000"], capture_output=True, text=True, env=e, timeout=150)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    out = {k: np.fromfile(tmp_path / f"{k}.bin", dtype=np.float64)
+           for k in ("ref_Dpsi", "ref_Ddagchi", "ref_DDdagpsi", "ref_force", "ref_cgx")}
+    for k in ("ref_Dpsi", "ref_Ddagchi", "ref_DDdagpsi", "ref_force"):
+        assert bits_equal(out[k], a[k]), k
+    x, xr = out["ref_cgx"], a["ref_cgx"]
+    assert np.linalg.norm(x - xr) / np.linalg.norm(xr) <= 1e-12
+    assert '"cg_converged": 1' in r.stdout
+
+
+@pytest.mark.multiproc
 def test_reference_hmc_program_multirank(tmp_path):
     """The reference HMC program (src/main.cpp) on 2 x 2 MPI ranks over the
     shim: two t-column leaders drive two t-shards on this GPU (MPI host-staged
