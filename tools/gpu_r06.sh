@@ -210,6 +210,15 @@ q() {
     -k "sharded and peer" > gpurun_out/r06q_tests.log 2>&1
 }
 
+# r: the drop-in shim's tests (the peer transport through MPI_Allgather included) and the 2-rank peer bench
+#    rehearsal with the timed-solve residual check
+r() {
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_dropin_gpu.py \
+    > gpurun_out/r06r_tests.log 2>&1 &&
+  timeout -k 10 300 python3 bench.py --gpus 2 --device 0 --steps 50 --warmup 10 --no-weak --no-cpu-baseline \
+    > gpurun_out/r06r_bench2.log 2>&1
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
