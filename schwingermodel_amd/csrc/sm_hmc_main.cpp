@@ -29,6 +29,7 @@
 #include <iostream>
 #include <sstream>
 #include <string>
+#include <vector>
 
 #include "sm_hip.h"
 
@@ -123,13 +124,26 @@ int main(int argc, char **argv) {
     MPI_Comm_rank(node, &local);
     MPI_Comm_free(&node);
     if (sm_device_count(&ndev) != SM_OK || ndev < 1) die("no GPU");
-    unsigned char uid[256] = {0};
-    if (size > 1) {
-        if (rank == 0 && sm_comm_unique_id(uid, sizeof uid) != SM_OK) die("sm_comm_unique_id");
-        MPI_Bcast(uid, sizeof uid, MPI_BYTE, 0, MPI_COMM_WORLD);
-    }
+    // shards over the device-initiated peer transport (the region handles
+    // all-gathered over MPI), or RCCL with SM_HMC_TRANSPORT=rccl
+    const char *te = std::getenv("SM_HMC_TRANSPORT");
+    const std::string transport = te ? te : "peer";
+    if (transport != "peer" && transport != "rccl") die("SM_HMC_TRANSPORT must be peer or rccl");
     sm_ctx *ctx = nullptr;
-    if (sm_create(&ctx, Nx, Nt, size, rank, local % ndev, size > 1 ? uid : nullptr) != SM_OK) die("sm_create");
+    if (size > 1 && transport == "peer") {
+        const int nb = sm_peer_handle_bytes();
+        std::vector<char> mine((size_t)nb), all((size_t)nb * size);
+        if (sm_create_peer(&ctx, Nx, Nt, size, rank, local % ndev, mine.data(), nb) != SM_OK) die("sm_create_peer");
+        MPI_Allgather(mine.data(), nb, MPI_BYTE, all.data(), nb, MPI_BYTE, MPI_COMM_WORLD);
+        if (sm_peer_connect(ctx, all.data(), nb) != SM_OK) die("sm_peer_connect");
+    } else {
+        unsigned char uid[256] = {0};
+        if (size > 1) {
+            if (rank == 0 && sm_comm_unique_id(uid, sizeof uid) != SM_OK) die("sm_comm_unique_id");
+            MPI_Bcast(uid, sizeof uid, MPI_BYTE, 0, MPI_COMM_WORLD);
+        }
+        if (sm_create(&ctx, Nx, Nt, size, rank, local % ndev, size > 1 ? uid : nullptr) != SM_OK) die("sm_create");
+    }
 
     std::string start_time_str;
     if (rank == 0) {

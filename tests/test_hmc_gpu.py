@@ -128,3 +128,38 @@ def test_sm_hmc_program(tmp_path, sm):
     L.close()
     # the printed Ep (6 significant digits) is the mean plaquette of the saved confs
     assert abs(np.mean(sps) / S - ep) <= 1e-5 * abs(ep)
+
+
+@pytest.mark.multiproc
+def test_sm_hmc_program_two_shards_peer(tmp_path, sm):
+    """The CLI as 2 MPI ranks sharing this GPU over the peer transport (the
+    region handles all-gathered with MPI_Allgather): t-sharded trajectories,
+    and the saved confs gathered to shard 0 through its mailbox
+    (sm_gather_gauge): as many as measured, 28-B records, and the printed Ep is
+    the mean plaquette of the confs as saved."""
+    exe = os.path.join(REPO, "schwingermodel_amd", "sm_hmc")
+    mpiexec = "/opt/conda/bin/mpiexec"
+    if not os.path.exists(exe) or not os.path.exists(mpiexec):
+        pytest.fail("sm_hmc or MPICH missing")
+    N, Nmeas = 32, 4
+    params = f"1\n2\n0.1\n6\n0.5\n2\n3\n{Nmeas}\n1\n1\n"
+    env = dict(os.environ, HOSTNAME="box", GPU_MAX_HW_QUEUES="1")
+    r = subprocess.run([mpiexec, "-n", "2", exe, str(N), str(N), "77"], input=params, capture_output=True,
+                       text=True, cwd=tmp_path, env=env, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    ep = float(re.search(r"Ep = (\S+) dEp", r.stdout).group(1))
+    confs = sorted(tmp_path.glob(f"2D_U1_Ns{N}_Nt{N}_b20000_m01000_*.ctxt"))
+    assert len(confs) == Nmeas, os.listdir(tmp_path)
+    S = N * N
+    L = sm.Lattice(N, N)
+    sps = []
+    for c in confs:
+        assert c.stat().st_size == S * 2 * 28
+        U = np.empty(4 * S)
+        sm.check(sm.lib.sm_conf_read(str(c).encode(), N, N, ptr(U[:2 * S]), ptr(U[2 * S:])))
+        sm.check(sm.lib.sm_upload_gauge(L.ctx, ptr(U[:2 * S]), ptr(U[2 * S:])))
+        sp, act = ctypes.c_double(), ctypes.c_double()
+        sm.check(sm.lib.sm_plaquette(L.ctx, 2.0, ctypes.byref(sp), ctypes.byref(act), None))
+        sps.append(sp.value)
+    L.close()
+    assert abs(np.mean(sps) / S - ep) <= 1e-5 * abs(ep)

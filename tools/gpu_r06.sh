@@ -219,6 +219,12 @@ r() {
     > gpurun_out/r06r_bench2.log 2>&1
 }
 
+# s: the HMC program as 2 MPI ranks over the peer transport (conf gather through shard 0's mailbox)
+s() {
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_hmc_gpu.py \
+    -k "program" > gpurun_out/r06s_tests.log 2>&1
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
