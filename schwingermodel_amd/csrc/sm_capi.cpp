@@ -521,6 +521,7 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //   rccl_order=0        no ordering events between RCCL operations on the two
 //                       streams (A/B only: the one communicator then relies on
 //                       RCCL's own ordering)
+//   peer_wait_ms=N      peer transport: time limit of one wait (default 10000)
 //   peer_store=0|1|2    peer transport: the CG pass's face stores as 16-B
 //                       write-through buffer stores (0), 8-B atomic stores (1)
 //                       or plain stores into the uncached ring (2)
@@ -583,6 +584,9 @@ static int apply_test_opts(sm_ctx *c) {
             c->apply_split = iv ? 1 : 0;
         } else if (k == "rccl_order") {
             c->rccl_ordered = iv ? 1 : 0;
+        } else if (k == "peer_wait_ms") {
+            if (iv < 1) return fail(SM_ERR_ARG, "SM_TEST_OPTS: peer_wait_ms must be >= 1");
+            c->peer_wait_ticks = 100000ull * (unsigned long long)iv;  // 100-MHz wall clock
         } else if (k == "peer_store") {
             if (iv < 0 || iv > 2) return fail(SM_ERR_ARG, "SM_TEST_OPTS: peer_store must be 0, 1 or 2");
             c->peer_store = iv;
@@ -807,6 +811,7 @@ static int peer_set_view(sm_ctx *c) {
     v.down = c->loop ? 0 : down_rank(c);
     v.up = c->loop ? 0 : up_rank(c);
     v.Nx = c->g.Nx;
+    v.wait_ticks = c->peer_wait_ticks;
     v.base[v.me] = c->peer_region;
     HIP_TRY(hipMemcpyAsync(c->peer_view_dev, &v, sizeof v, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));

@@ -137,6 +137,7 @@ struct sm_ctx {
     unsigned long long peer_coll_seq = 0, peer_face_seq = 0;  // the next collective / face exchange is seq + 1
     unsigned *peer_tick = nullptr;  // zeroed ticket counter of the transport kernels
     int peer_store = 0;             // CG pass face stores: 0 16-B write-through, 1 8-B atomic, 2 plain (test option)
+    unsigned long long peer_wait_ticks = sm::kPeerWaitTicks;  // one wait's time limit (test option peer_wait_ms)
     bool hosted = false;            // host-callback transport instead of RCCL
     sm_host_transport tr{};
     double *h_face = nullptr;       // pinned: send_lo, send_hi, recv_lo, recv_hi (4 x up to 8Nx doubles)

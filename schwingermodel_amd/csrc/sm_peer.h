@@ -34,7 +34,7 @@ namespace sm {
 constexpr int kPeerMaxRanks = 16;
 constexpr long kPeerHdrBytes = 4096;
 constexpr long kMailDoubles = 48;  // per x and side: up to 3 fields x 16 doubles (a 4-deep face)
-constexpr unsigned long long kPeerWaitTicks = 1000000000ull;  // 10 s at 100 MHz
+constexpr unsigned long long kPeerWaitTicks = 1000000000ull;  // 10 s at 100 MHz (PeerView::wait_ticks default)
 
 struct PeerHdr {
     unsigned long long coll[kPeerMaxRanks];  // all-reduce seq published by rank r
@@ -50,6 +50,7 @@ struct PeerView {
     char *base[kPeerMaxRanks];
     int me, n, down, up;
     long Nx;
+    unsigned long long wait_ticks;  // time limit of one wait (100-MHz ticks; kPeerWaitTicks unless a test sets it)
 };
 
 __host__ __device__ inline long peer_ring_off(long Nx, int slot) { return kPeerHdrBytes + (long)slot * 16 * Nx * 16; }
@@ -97,12 +98,17 @@ __device__ __forceinline__ void peer_publish(unsigned long long *flag, unsigned 
 // Wait (one thread) until *flag >= seq; false (and err recorded) after the
 // time limit. The polls are system-scope loads (they bypass this device's
 // caches); what the sender published is read afterwards with sys_ld, or by a
-// later kernel from this region's uncached memory.
-__device__ __forceinline__ bool peer_wait(unsigned long long *flag, unsigned long long seq, unsigned long long *err) {
+// later kernel from this region's uncached memory. Once a wait of this shard
+// has timed out (err set), every later wait gives up at once: the results are
+// already void, and the caller reaches sm_peer_status / sm_cg_finish's error
+// after one time limit, not one per pass.
+__device__ __forceinline__ bool peer_wait(unsigned long long *flag, unsigned long long seq, unsigned long long *err,
+                                          unsigned long long limit) {
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return false;
     const unsigned long long t0 = wall_clock64();
     while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
         __builtin_amdgcn_s_sleep(1);
-        if (wall_clock64() - t0 > kPeerWaitTicks) {
+        if (wall_clock64() - t0 > limit) {
             __hip_atomic_store(err, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return false;
         }
@@ -124,7 +130,7 @@ __device__ __forceinline__ void peer_allreduce_thread(const PeerView &v, unsigne
     for (int r = 0; r < v.n; ++r) peer_publish(&peer_hdr(v, r)->coll[v.me], seq);
     PeerHdr *mine = peer_hdr(v, v.me);
     for (int r = 0; r < v.n; ++r)
-        if (!peer_wait(&mine->coll[r], seq, &mine->err)) break;
+        if (!peer_wait(&mine->coll[r], seq, &mine->err, v.wait_ticks)) break;
     for (int i = 0; i < n; ++i) {
         double acc = sys_ld(&mine->gather[slot][0][i]);
         for (int r = 1; r < v.n; ++r) acc = acc + sys_ld(&mine->gather[slot][r][i]);

@@ -39,7 +39,7 @@ __device__ __forceinline__ void peer_face_handoff(const PeerView &v, unsigned lo
         peer_publish(&peer_hdr(v, v.down)->face[1], seq);
         peer_publish(&peer_hdr(v, v.up)->face[0], seq);
         PeerHdr *me = peer_hdr(v, v.me);
-        if (peer_wait(&me->face[0], seq, &me->err)) peer_wait(&me->face[1], seq, &me->err);
+        if (peer_wait(&me->face[0], seq, &me->err, v.wait_ticks)) peer_wait(&me->face[1], seq, &me->err, v.wait_ticks);
     }
 }
 

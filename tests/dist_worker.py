@@ -628,6 +628,52 @@ def run_fallback(name, result_path, dist, rank, world):
     dist.destroy_process_group()
 
 
+def run_peerfail(name, result_path, dist, rank, world):
+    """mode "peerfail" (one GPU, peer transport): every rank connects, then only
+    rank 0 applies D and solves; the others stay alive (their regions mapped)
+    but never take part. Rank 0's waits must hit the time limit
+    (SM_TEST_OPTS peer_wait_ms), sm_peer_status must report it, and the solve
+    that follows must fail fast (every later wait gives up at once) instead of
+    hanging. The other ranks leave only after rank 0 is done."""
+    import time
+    import schwingermodel_amd as sm
+    from schwingermodel_amd import dist as smd
+    from conftest import load_fixture
+    meta, a = load_fixture(name)
+    Nx, Nt = meta["Nx"], meta["Nt"]
+    S = Nx * Nt
+    t0, Wt = ctypes.c_int(), ctypes.c_int()
+    sm.check(sm.lib.sm_shard_plan(Nt, world, rank, ctypes.byref(t0), ctypes.byref(Wt)))
+    V = Nx * Wt.value
+    ctx, _ = smd.create_shard_context(Nx, Nt, transport="peer", device=int(os.environ.get("SM_DEVICE", "0")))
+    U = shard_field(a["U"], Nx, Nt, t0.value, Wt.value)
+    psi = shard_field(a["psi"], Nx, Nt, t0.value, Wt.value)
+    P = lambda x: ctypes.c_void_p(x.ctypes.data)  # noqa: E731
+    out = {}
+    if rank == 0:
+        sm.check(sm.lib.sm_upload_gauge(ctx, P(U[0]), P(U[1])))  # (the ghost-link exchange times out here)
+        o0, o1 = np.empty(V, complex), np.empty(V, complex)
+        t = time.time()
+        sm.lib.sm_dirac(ctx, P(psi[0]), P(psi[1]), P(o0), P(o1), meta["m0"], 0)
+        seq = ctypes.c_ulonglong(0)
+        out["status_rc"] = sm.lib.sm_peer_status(ctx, ctypes.byref(seq))
+        out["status_msg"] = sm.lib.sm_last_error().decode()
+        out["timed_out_seq"] = seq.value
+        out["apply_s"] = time.time() - t
+        x0, x1 = np.empty(V, complex), np.empty(V, complex)
+        res = sm.CGResult()
+        t = time.time()
+        out["cg_rc"] = sm.lib.sm_cg(ctx, P(psi[0]), P(psi[1]), P(x0), P(x1), meta["m0"], 1e-10, 200, ctypes.byref(res))
+        out["cg_msg"] = sm.lib.sm_last_error().decode()
+        out["cg_s"] = time.time() - t
+        with open(result_path, "w") as f:
+            json.dump(out, f)
+    dist.barrier()
+    sm.lib.sm_destroy(ctx)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     mode, name, result_path = sys.argv[1], sys.argv[2], sys.argv[3]
     import datetime
@@ -650,6 +696,8 @@ def main():
         return run_commworld(name, result_path, dist, rank, world)
     if mode == "fallback":
         return run_fallback(name, result_path, dist, rank, world)
+    if mode == "peerfail":
+        return run_peerfail(name, result_path, dist, rank, world)
     from conftest import bits_equal, load_fixture
     import schwingermodel_amd as sm
     from schwingermodel_amd import dist as smd

@@ -213,3 +213,18 @@ def test_peer_world_md(tmp_path, fixture, world):
     assert abs(dH - t["single"][0]) <= 1e-6 * max(1.0, abs(t["single"][0]))
     assert acc == t["single"][1] and r == t["single"][2]
     assert t["U_rel"] <= 1e-8
+
+
+@pytest.mark.multiproc
+def test_peer_wait_time_limit(tmp_path):
+    """A shard whose neighbour never takes part does not hang: its wait gives up
+    at the time limit (here 2 s, SM_TEST_OPTS peer_wait_ms), sm_peer_status
+    names the sequence number, and the solve that follows on the same context
+    fails within seconds (every later wait gives up at once) with the peer
+    error instead of waiting 10 s per pass."""
+    env = dict(PEER, **sm_opts(peer_wait_ms=2000))
+    rep = run_world("peerfail", "l32x48_b3_m-0p10", 2, tmp_path, timeout=120, extra_env=env)
+    assert rep["status_rc"] != 0 and "timed out" in rep["status_msg"] and rep["timed_out_seq"] > 0, rep
+    assert rep["apply_s"] < 30, rep
+    assert rep["cg_rc"] != 0 and "peer transport" in rep["cg_msg"], rep
+    assert rep["cg_s"] < 30, rep
