@@ -27,15 +27,19 @@ WORLD_SIZE spawns the N ranks itself, before anything touches the GPU.
 torch.distributed (gloo) is control plane only: the RCCL unique id / the peer
 regions' IPC handles, barriers and the max-over-ranks timing.
 
-Transports (N > 1): `--transport peer` (the default) is the device-initiated
-one (include/sm_hip.h sm_create_peer: kernels store faces and sums straight
-into the other GPUs' regions over xGMI); before timing, every rank checks it
-against the host-staged transport on the same shard (D and D^dag bitwise, 30
-CG iterations to 1e-12) and the run falls back to RCCL if that check or the
-setup fails anywhere (the line says which ran and why). `--transport rccl`
-forces RCCL; `--transport hosted` runs the shards over the host-staged
-transport (several ranks may share one GPU; tests / rehearsal; `--device 0`
-puts peer ranks on one GPU too).
+Transports (N > 1): `--transport rccl` (the default, north_star's "RCCL halo
+exchange over xGMI") carries the headline `value`; the same run then times
+the device-initiated peer transport on the same workload as the extra key
+`peer_transport` (include/sm_hip.h sm_create_peer: kernels store faces and
+sums straight into the other GPUs' regions over xGMI; `--no-peer` skips it).
+Before timing the peer transport every rank checks it against the
+host-staged transport on the same shard (D and D^dag bitwise, 30 CG
+iterations to 1e-12); after timing, both transports' timed solves are
+checked against themselves (recursive against true residual).
+`--transport peer` makes the peer transport the headline (falling back to
+RCCL if its check or setup fails anywhere); `--transport hosted` runs the
+shards over the host-staged transport (several ranks may share one GPU;
+tests / rehearsal; `--device 0` puts peer ranks on one GPU too).
 """
 import argparse
 import ctypes
@@ -88,9 +92,11 @@ def parse(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="host cores for the CPU baseline (default: this process's CPU share)")
     ap.add_argument("--cpu-iters", type=int, default=50, help="CG iterations of the CPU baseline sample")
-    ap.add_argument("--transport", choices=["peer", "rccl", "hosted"], default="peer",
-                    help="multi-GPU wire: the device-initiated peer transport (checked against the host-staged "
-                         "one first, RCCL if that fails), RCCL, or the host-staged test transport")
+    ap.add_argument("--transport", choices=["rccl", "peer", "hosted"], default="rccl",
+                    help="multi-GPU wire of the headline: RCCL, the device-initiated peer transport (checked "
+                         "against the host-staged one first, RCCL if that fails), or the host-staged test transport")
+    ap.add_argument("--no-peer", action="store_true",
+                    help="N > 1 with --transport rccl (or hosted): skip the extra timing of the peer transport")
     ap.add_argument("--device", type=int, default=None, help="override the rank -> GPU mapping")
     ap.add_argument("--cg-path", choices=list(CG_PATH_ID), default="recompute")
     ap.add_argument("--rank-timeout", type=float, default=900.0,
@@ -389,10 +395,11 @@ def peer_check(rt, sh, m0, iters=30):
             "cg_iterations": iters, "cg_x_rel": rel, "ok": ok}
 
 
-def make_shard(args, rt, Nx, Nt, sigma, m0):
+def make_shard(args, rt, Nx, Nt, sigma, m0, fallback=True):
     """This rank's shard over args.transport; for the peer transport (N > 1)
     after peer_check, falling back to RCCL on every rank if the setup or the
-    check failed on any. Returns (shard, check report or None)."""
+    check failed on any (fallback=False: no shard, (None, report)). Returns
+    (shard, check report or None)."""
     if rt["world"] == 1 or args.transport != "peer":
         return Shard(rt, Nx, Nt, sigma), None
     err, sh, chk = "", None, None
@@ -409,10 +416,41 @@ def make_shard(args, rt, Nx, Nt, sigma, m0):
         err = "peer setup failed on another rank"
     if not err:
         return sh, chk
-    print(f"[bench] rank {rt['rank']}: {err}; falling back to RCCL", file=sys.stderr, flush=True)
+    print(f"[bench] rank {rt['rank']}: {err}" + ("; falling back to RCCL" if fallback else ""), file=sys.stderr,
+          flush=True)
     if sh is not None:
         sh.close()
+    if not fallback:
+        return None, dict(chk or {}, ok=False, reason=err)
     return Shard(rt, Nx, Nt, sigma, "rccl"), dict(chk or {}, fallback="rccl", reason=err)
+
+
+def time_peer(args, rt, Nx, Nt, sigma, m0):
+    """N > 1 beside the RCCL headline: the same workload over the peer
+    transport (checked first; nothing is timed if the check fails), the CG
+    steps and the Dirac apply timed exactly as the headline's, and the timed
+    solve checked against itself."""
+    import argparse
+    a = argparse.Namespace(**vars(args))
+    a.transport = "peer"
+    sh, chk = make_shard(a, rt, Nx, Nt, sigma, m0, fallback=False)
+    if sh is None:
+        return {"transport_check": chk}
+    try:
+        begin_cg(sh, m0, args.cg_path, args.no_link_angles)
+        apply_time = time_applies(rt, sh, m0, args.applies)
+        t_cg, _ = time_cg_steps(rt, sh, m0, args.cg_path, args.warmup, args.steps, args.no_link_angles, begun=True)
+        apply_s = apply_time()
+        solve = timed_solve_check(sh, m0)
+        t_cg, apply_s = max_over_ranks(rt, [t_cg, apply_s])
+        (bad,) = max_over_ranks(rt, [float(not solve["ok"])])
+    finally:
+        sh.close()
+    return {"value": round(args.steps / t_cg, 3), "ms_per_step": round(1e3 * t_cg / args.steps, 4),
+            "unit": f"CG iterations/s (one {Nx}x{Nt} lattice over all GPUs)",
+            "dirac_apply_us": round(apply_s * 1e6, 2),
+            "dirac_apply_GBps": round(BYTES_PER_SITE_APPLY * sh.V / apply_s / 1e9, 1),
+            "transport_check": chk, "timed_solve_check": dict(solve, ok_all_ranks=bad == 0.0)}
 
 
 def _fill(sm, Nx, Nt, t0, Wt, sigma, U, chi, nthreads=8):
@@ -670,6 +708,10 @@ def run_config34(args, rt, cfg_id):
                 "unit": f"CG iterations/s of a {Nx}x{Nt // 8}-site slab per GPU, whole job (it/s x N)",
                 "scaling": "weak"}
         shw.close()
+    peer = None
+    # (also beside the host-staged headline: the one-GPU rehearsal of this path)
+    if world > 1 and args.transport in ("rccl", "hosted") and not args.no_peer:
+        peer = time_peer(args, rt, Nx, Nt, cfg["sigma"], m0)
     if rank != 0:
         return
     it_per_s = args.steps / t_cg
@@ -718,6 +760,8 @@ def run_config34(args, rt, cfg_id):
         line["comm"]["transport_check"] = tcheck
     if solve_check is not None:
         line["comm"]["timed_solve_check"] = solve_check
+    if peer is not None:
+        line["peer_transport"] = peer
     print(json.dumps(line), flush=True)
     if solve_check is not None and not solve_check["ok"]:
         raise SystemExit("[bench] the timed sharded solve's recursive and true residuals disagree")

@@ -25,7 +25,8 @@
 // include/mpi_setup.h:50-52 when ranks_x = 1).
 //
 // Transport between the leaders (SM_DROPIN_TRANSPORT): "rccl" (RCCL over
-// xGMI, one GPU per leader), "mpi" (host-staged: faces and the 6-double scalar
+// xGMI, one GPU per leader), "peer" (the device-initiated transport, the
+// region handles all-gathered over MPI), "mpi" (host-staged: faces and the 6-double scalar
 // sums through MPI_Sendrecv / MPI_Reduce + MPI_Bcast on the leaders'
 // communicator, so several leaders may share one GPU), or "auto" (default):
 // rccl when every node has at least as many GPUs as leaders, else mpi.
@@ -96,7 +97,7 @@ int mpi_allreduce(void *, double *buf, long n) {
 std::string transport_choice(int local_leaders, int ndev) {
     const char *e = std::getenv("SM_DROPIN_TRANSPORT");
     std::string t = e ? e : "auto";
-    if (t == "auto") t = local_leaders > ndev ? "mpi" : "peer";
+    if (t == "auto") t = local_leaders > ndev ? "mpi" : "rccl";
     if (t != "mpi" && t != "rccl" && t != "peer") {
         std::cerr << "[sm_hip] SM_DROPIN_TRANSPORT must be auto, peer, rccl or mpi" << std::endl;
         MPI_Abort(MPI_COMM_WORLD, 1);

@@ -124,10 +124,10 @@ int main(int argc, char **argv) {
     MPI_Comm_rank(node, &local);
     MPI_Comm_free(&node);
     if (sm_device_count(&ndev) != SM_OK || ndev < 1) die("no GPU");
-    // shards over the device-initiated peer transport (the region handles
-    // all-gathered over MPI), or RCCL with SM_HMC_TRANSPORT=rccl
+    // shards over RCCL, or over the device-initiated peer transport with
+    // SM_HMC_TRANSPORT=peer (the region handles all-gathered over MPI)
     const char *te = std::getenv("SM_HMC_TRANSPORT");
-    const std::string transport = te ? te : "peer";
+    const std::string transport = te ? te : "rccl";
     if (transport != "peer" && transport != "rccl") die("SM_HMC_TRANSPORT must be peer or rccl");
     sm_ctx *ctx = nullptr;
     if (size > 1 && transport == "peer") {

@@ -132,8 +132,9 @@ def test_sm_hmc_program(tmp_path, sm):
 
 @pytest.mark.multiproc
 def test_sm_hmc_program_two_shards_peer(tmp_path, sm):
-    """The CLI as 2 MPI ranks sharing this GPU over the peer transport (the
-    region handles all-gathered with MPI_Allgather): t-sharded trajectories,
+    """The CLI as 2 MPI ranks sharing this GPU over the peer transport
+    (SM_HMC_TRANSPORT=peer: the region handles all-gathered with
+    MPI_Allgather; RCCL, the default, refuses two ranks on one GPU): t-sharded trajectories,
     and the saved confs gathered to shard 0 through its mailbox
     (sm_gather_gauge): as many as measured, 28-B records, and the printed Ep is
     the mean plaquette of the confs as saved."""
@@ -143,7 +144,7 @@ def test_sm_hmc_program_two_shards_peer(tmp_path, sm):
         pytest.fail("sm_hmc or MPICH missing")
     N, Nmeas = 32, 4
     params = f"1\n2\n0.1\n6\n0.5\n2\n3\n{Nmeas}\n1\n1\n"
-    env = dict(os.environ, HOSTNAME="box", GPU_MAX_HW_QUEUES="1")
+    env = dict(os.environ, HOSTNAME="box", GPU_MAX_HW_QUEUES="1", SM_HMC_TRANSPORT="peer")
     r = subprocess.run([mpiexec, "-n", "2", exe, str(N), str(N), "77"], input=params, capture_output=True,
                        text=True, cwd=tmp_path, env=env, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]

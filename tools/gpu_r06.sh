@@ -225,6 +225,17 @@ s() {
     -k "program" > gpurun_out/r06s_tests.log 2>&1
 }
 
+# t: the N > 1 bench paths rehearsed on one GPU: the host-staged headline with the peer transport timed beside it
+#    (the code path of the RCCL default), 2 and 4 ranks; the peer headline, 2 ranks
+t() {
+  timeout -k 10 400 python3 bench.py --gpus 2 --device 0 --transport hosted --steps 50 --warmup 10 --no-weak \
+    --no-cpu-baseline > gpurun_out/r06t_bench2_hosted.log 2>&1 &&
+  GPU_MAX_HW_QUEUES=1 timeout -k 10 400 python3 bench.py --gpus 4 --device 0 --transport hosted --steps 50 --warmup 10 \
+    --no-weak --no-cpu-baseline > gpurun_out/r06t_bench4_hosted.log 2>&1 &&
+  timeout -k 10 400 python3 bench.py --gpus 2 --device 0 --transport peer --steps 50 --warmup 10 --no-weak \
+    --no-cpu-baseline > gpurun_out/r06t_bench2_peer.log 2>&1
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
@@ -234,9 +245,10 @@ fin() {
   python3 -c "import schwingermodel_amd as s; print(s.lib.sm_build_id().decode())" > gpurun_out/build_id_$T.txt &&
   timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver_$T.log 2>&1 &&
   timeout -k 10 400 python3 bench.py > gpurun_out/bench_$T.log 2>&1 &&
-  timeout -k 10 300 python3 bench.py --gpus 2 --device 0 --steps 50 --warmup 10 --no-weak > gpurun_out/bench2_$T.log 2>&1 &&
-  GPU_MAX_HW_QUEUES=1 timeout -k 10 400 python3 bench.py --gpus 8 --device 0 --steps 50 --warmup 10 --no-weak \
-    --no-cpu-baseline > gpurun_out/bench8_$T.log 2>&1 &&
+  timeout -k 10 300 python3 bench.py --gpus 2 --device 0 --transport hosted --steps 50 --warmup 10 --no-weak \
+    > gpurun_out/bench2_$T.log 2>&1 &&
+  GPU_MAX_HW_QUEUES=1 timeout -k 10 400 python3 bench.py --gpus 8 --device 0 --transport peer --steps 50 --warmup 10 \
+    --no-weak --no-cpu-baseline > gpurun_out/bench8_$T.log 2>&1 &&
   timeout -k 10 300 python3 bench.py --config 5 > gpurun_out/bench_c5_$T.log 2>&1 &&
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_stats_$T -o run -- python3 bench.py --steps 200 --warmup 20 --applies 20 --no-cpu-baseline --no-weak --evolved-trajectories 0 > gpurun_out/prof_stats_$T.log 2>&1 &&
   python3 tools/step_gap.py gpurun_out/prof_stats_$T/run_kernel_trace.csv --last 200 > gpurun_out/step_gap_$T.log 2>&1 &&
