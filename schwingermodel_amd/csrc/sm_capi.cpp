@@ -521,6 +521,8 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //   rccl_order=0        no ordering events between RCCL operations on the two
 //                       streams (A/B only: the one communicator then relies on
 //                       RCCL's own ordering)
+//   rccl_sums=1         RCCL contexts: the CG pass's scalar sums through
+//                       ncclAllReduce instead of the in-pass peer all-reduce
 //   peer_wait_ms=N      peer transport: time limit of one wait (default 10000)
 //   peer_store=0|1|2    peer transport: the CG pass's face stores as 16-B
 //                       write-through buffer stores (0), 8-B atomic stores (1)
@@ -584,6 +586,8 @@ static int apply_test_opts(sm_ctx *c) {
             c->apply_split = iv ? 1 : 0;
         } else if (k == "rccl_order") {
             c->rccl_ordered = iv ? 1 : 0;
+        } else if (k == "rccl_sums") {
+            c->peer_sums_wish = iv ? 0 : 1;
         } else if (k == "peer_wait_ms") {
             if (iv < 1) return fail(SM_ERR_ARG, "SM_TEST_OPTS: peer_wait_ms must be >= 1");
             c->peer_wait_ticks = 100000ull * (unsigned long long)iv;  // 100-MHz wall clock
@@ -627,6 +631,8 @@ static int apply_test_opts(sm_ctx *c) {
     }
     return SM_OK;
 }
+
+static int rccl_peer_sums_setup(sm_ctx *c);
 
 static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device,
                          const void *unique_id, const sm_host_transport *tr, bool loop = false, bool peer = false) {
@@ -786,9 +792,110 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
             sm_destroy(c);
             return fail(SM_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
         }
+        if (int rc = rccl_peer_sums_setup(c); rc != SM_OK) {
+            sm_destroy(c);
+            return rc;
+        }
     }
     *out = c;
     return SM_OK;
+}
+
+// RCCL contexts, the CG pass's scalar sums: the recompute-Ad pass's last block
+// all-reduces the shard's three sums itself (cg_ticketed_tail, the peer
+// transport's in-pass all-reduce) through a 4-KiB uncached header per shard,
+// instead of an ncclAllReduce after every pass; the halo exchange stays RCCL
+// (north_star). The header handles are all-gathered over the communicator
+// itself, and every shard's success (allocation, IPC open, a handshake
+// all-reduce) is agreed by an ncclAllReduce (min), so all shards take the
+// same path; any failure leaves the context on ncclAllReduce. Never fails
+// the context.
+static int rccl_peer_sums_setup(sm_ctx *c) {
+    c->peer_sums = false;
+    if (!c->peer_sums_wish || !c->comm) return SM_OK;
+    const int P = c->loop ? 1 : c->nshard, me = c->loop ? 0 : c->shard;
+    const size_t hb = sizeof(hipIpcMemHandle_t);
+    int ok = 1;
+    int *flag = nullptr;
+    char *dh = nullptr;
+    std::vector<char> hh(hb * P, 0);
+    auto agree = [&]() -> int {  // min over shards of ok
+        HIP_TRY(hipMemcpyAsync(flag, &ok, sizeof ok, hipMemcpyHostToDevice, c->stream));
+        NCCL_TRY(ncclAllReduce(flag, flag, 1, ncclInt32, ncclMin, c->comm, c->stream));
+        HIP_TRY(hipMemcpyAsync(&ok, flag, sizeof ok, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return SM_OK;
+    };
+    HIP_TRY(hipMalloc(&flag, sizeof(int)));
+    if (hipMalloc(&dh, hb * P) != hipSuccess ||
+        hipExtMallocWithFlags((void **)&c->peer_region, kPeerHdrBytes, hipDeviceMallocUncached) != hipSuccess ||
+        hipMemset(c->peer_region, 0, kPeerHdrBytes) != hipSuccess ||
+        (!c->peer_view_dev && hipMalloc(&c->peer_view_dev, sizeof(PeerView)) != hipSuccess) ||
+        hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t *>(hh.data() + hb * me), c->peer_region) != hipSuccess)
+        ok = 0;
+    (void)hipGetLastError();
+    int rc = SM_OK;
+    if (dh) {  // the handles, all-gathered in place over the communicator
+        if (hipMemcpy(dh, hh.data(), hb * P, hipMemcpyHostToDevice) != hipSuccess) ok = 0;
+        rc = ncclAllGather(dh + hb * me, dh, hb, ncclUint8, c->comm, c->stream) == ncclSuccess ? SM_OK : SM_ERR_RCCL;
+        if (rc == SM_OK && (hipStreamSynchronize(c->stream) != hipSuccess ||
+                            hipMemcpy(hh.data(), dh, hb * P, hipMemcpyDeviceToHost) != hipSuccess))
+            ok = 0;
+    } else {
+        ok = 0;
+    }
+    for (int r = 0; rc == SM_OK && ok && r < P; ++r) {
+        if (r == me) continue;
+        void *p = nullptr;
+        hipIpcMemHandle_t h;
+        memcpy(&h, hh.data() + hb * r, hb);
+        if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+            ok = 0;
+            (void)hipGetLastError();
+        } else {
+            c->peer_open[r] = (char *)p;
+        }
+    }
+    if (rc == SM_OK) rc = agree();
+    if (rc == SM_OK && ok) {
+        PeerView &v = c->peer_view;
+        v.me = me;
+        v.n = P;
+        v.down = c->loop ? 0 : down_rank(c);
+        v.up = c->loop ? 0 : up_rank(c);
+        v.Nx = c->g.Nx;
+        v.wait_ticks = c->peer_wait_ticks;
+        for (int r = 0; r < P; ++r) v.base[r] = r == me ? c->peer_region : c->peer_open[r];
+        double *chk = (double *)(c->sums + 3);
+        const double mine = (double)me;
+        double got = -1.0;
+        unsigned long long err = 0;
+        if (hipMemcpy(c->peer_view_dev, &v, sizeof v, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(chk, &mine, sizeof mine, hipMemcpyHostToDevice) != hipSuccess)
+            ok = 0;
+        launch_peer_allreduce(c->stream, chk, 1, v, ++c->peer_coll_seq);  // handshake (time-limited)
+        if (hipStreamSynchronize(c->stream) != hipSuccess || hipMemcpy(&got, chk, sizeof got, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(&err, c->peer_region + offsetof(PeerHdr, err), sizeof err, hipMemcpyDeviceToHost) != hipSuccess)
+            ok = 0;
+        if (err || got != 0.5 * P * (P - 1)) ok = 0;
+        (void)hipGetLastError();
+        rc = agree();
+    }
+    (void)hipFree(flag);
+    if (dh) (void)hipFree(dh);
+    if (rc == SM_OK && ok) {
+        c->peer_sums = true;
+        return SM_OK;
+    }
+    for (char *&p : c->peer_open)
+        if (p) {
+            (void)hipIpcCloseMemHandle(p);
+            p = nullptr;
+        }
+    if (c->peer_region) (void)hipFree(c->peer_region);
+    c->peer_region = nullptr;
+    (void)hipGetLastError();
+    return rc;
 }
 
 int sm_create(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device,
@@ -882,7 +989,7 @@ int sm_create_peer_loopback(sm_ctx **out, int Nx, int Nt_global, int device) {
 int sm_peer_status(sm_ctx *c, unsigned long long *timed_out_seq) {
     if (!c) return fail(SM_ERR_ARG, "null context");
     unsigned long long err = 0;
-    if (c->peer && c->peer_region) {
+    if ((c->peer || c->peer_sums) && c->peer_region) {
         HIP_TRY(hipStreamSynchronize(c->stream));
         HIP_TRY(hipMemcpy(&err, c->peer_region + offsetof(PeerHdr, err), sizeof err, hipMemcpyDeviceToHost));
     }
@@ -1423,11 +1530,16 @@ static int cg_ra_pass(sm_ctx *c) {
     // parity), so no scalar kernel sits between the all-reduce and the next pass
     const bool red = tail && c->cg_red_shards;
     double2 *sums = red ? &c->sc->sumr[j & 1][0] : c->sc->sum3;  // this shard's sums (all-reduced below)
+    // RCCL contexts with peer sums (rccl_peer_sums_setup): the pass's last block
+    // all-reduces the sums itself, one collective number for both launches
+    const bool psums = c->peer_sums && red;
+    const PeerView *pv = psums ? c->peer_view_dev : nullptr;
+    const unsigned long long pseq = psums ? ++c->peer_coll_seq : 0;
     auto pass = [&](const CGFusedCfg &cf, int tb0, int tbn, hipStream_t st, int pbase, double2 *fsend) {
         const int lb = launch_cg_ra(st, c->g, cf, c->kshards(), d1, d2, dn, c->cg_x, c->U, f1, f2, face4_recv_U(c),
                                     c->cg_mass, j, c->sc, c->partials, tb0, tbn, nullptr, ua, c->Uang_face, fsend,
                                     pbase, tail ? c->tick : nullptr, nparts_pass, c->gsum, sums, red ? 1 : 0,
-                                    c->link_fmt);
+                                    c->link_fmt, nullptr, pv, pseq, 2 /* faces: plain stores, local */);
         if (lb) c->cg_link_bytes_last = lb;
     };
     HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
@@ -1462,7 +1574,7 @@ static int cg_ra_pass(sm_ctx *c) {
     if (!pipe || deferred) rccl_joined(c, c->stream, c->comm_stream);
     if (!split) pass(fc, 0, fc.TBk, c->stream, 0, nullptr);
     if (!tail) launch_cg1_local_sum(c->stream, nparts_pass, c->partials, c->sc);
-    TRY(allreduce_dev(c, (double *)sums, 6));
+    if (!psums) TRY(allreduce_dev(c, (double *)sums, 6));
     if (red) {
         c->cg_flush_pass = j;
         c->cg_flush_sums = 1;
@@ -1533,7 +1645,7 @@ int sm_cg_finish(sm_ctx *c, sm_cg_result *res) {
     }
     c->cg_active = 0;
     TRY(sm_cg_status(c, res));
-    if (c->peer) return sm_peer_status(c, nullptr);  // a timed-out wait makes the solve an error
+    if (c->peer || c->peer_sums) return sm_peer_status(c, nullptr);  // a timed-out wait makes the solve an error
     return SM_OK;
 }
 

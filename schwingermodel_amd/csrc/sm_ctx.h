@@ -138,6 +138,12 @@ struct sm_ctx {
     unsigned *peer_tick = nullptr;  // zeroed ticket counter of the transport kernels
     int peer_store = 0;             // CG pass face stores: 0 16-B write-through, 1 8-B atomic, 2 plain (test option)
     unsigned long long peer_wait_ticks = sm::kPeerWaitTicks;  // one wait's time limit (test option peer_wait_ms)
+    // RCCL contexts: the recompute-Ad pass's scalar sums all-reduced in its own last
+    // block through 4-KiB peer headers (sm_peer.h) instead of an ncclAllReduce per
+    // pass; the halos stay RCCL (sm_capi.cpp rccl_peer_sums_setup). Test option
+    // rccl_sums=1 keeps the ncclAllReduce.
+    bool peer_sums = false;
+    int peer_sums_wish = 1;
     bool hosted = false;            // host-callback transport instead of RCCL
     sm_host_transport tr{};
     double *h_face = nullptr;       // pinned: send_lo, send_hi, recv_lo, recv_hi (4 x up to 8Nx doubles)

@@ -236,6 +236,18 @@ t() {
     --no-cpu-baseline > gpurun_out/r06t_bench2_peer.log 2>&1
 }
 
+# u: RCCL contexts with the CG sums all-reduced in the pass (peer headers) -- the RCCL loopback tests, then
+#    the loopback probe against rccl_sums=1 (ncclAllReduce per pass), twice
+u() {
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_rccl_loopback_gpu.py \
+    tests/test_cg_paths_gpu.py -k "loopback or tshard" > gpurun_out/r06u_tests.log 2>&1 || return 1
+  local L="python -u tools/loopback_probe.py --shapes 4096x512,4096x1024,4096x2048 --iters 200 --rounds 3 --applies 5 --contexts one,loopback"
+  for i in 1 2; do
+    timeout -k 10 300 $L > gpurun_out/r06u_psums_$i.log 2>&1 &&
+    SM_TEST_OPTS=rccl_sums=1 timeout -k 10 300 $L > gpurun_out/r06u_ncclsums_$i.log 2>&1 || return 1
+  done
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
