@@ -542,7 +542,11 @@ def comm_world(args, rt, sh):
     why = check_rccl_world(transport, rt["world"], nmin, nmax)
     if why:
         raise SystemExit(f"[bench] {why}: refusing to report this run")
-    return {"transport": transport, ("peer_ranks" if transport == "peer" else "rccl_ranks"): [nmin, nmax]}
+    ip = ctypes.c_int(0)
+    if hasattr(sh.L, "ctx"):
+        sh.sm.check(sh.sm.lib.sm_cg_sums_in_pass(sh.L.ctx, ctypes.byref(ip)))
+    return {"transport": transport, ("peer_ranks" if transport == "peer" else "rccl_ranks"): [nmin, nmax],
+            "cg_sums": "in-pass" if ip.value else "collective"}
 
 
 def cg_bytes_per_site(sh, cg_path):

@@ -155,6 +155,11 @@ int sm_set_stream(sm_ctx *ctx, void *hip_stream);
  * 1 / 0 without one (the RCCL world of a host-staged or one-shard context is
  * this process alone). Any output pointer may be NULL. */
 int sm_comm_info(const sm_ctx *ctx, int *transport, int *nranks, int *rank);
+/* 1 if the recompute-Ad CG pass of a sharded context all-reduces its scalar
+ * sums in its own last block (the peer transport; RCCL contexts whose shards
+ * agreed on the peer headers at creation), 0 if it calls the transport's
+ * all-reduce after each pass. */
+int sm_cg_sums_in_pass(const sm_ctx *ctx, int *in_pass);
 int sm_synchronize(sm_ctx *ctx);
 /* Launch-geometry knobs of the stencil kernels (tuning / A-B benchmarks):
  * bt = t-columns per block (64, 128, 256), xchunk = rows marched per block,

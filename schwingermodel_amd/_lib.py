@@ -105,6 +105,7 @@ def _load():
         "sm_get_placement_probe": ([], ci),
         "sm_placement_buffer_name": ([ci], ctypes.c_char_p),
         "sm_comm_info": ([vp, ctypes.POINTER(ci), ctypes.POINTER(ci), ctypes.POINTER(ci)], ci),
+        "sm_cg_sums_in_pass": ([vp, ctypes.POINTER(ci)], ci),
         "sm_cg_link_codes": ([vp, ci, ctypes.POINTER(ci)], ci),
         "sm_cg_link_angles": ([vp, ci, ctypes.POINTER(ci)], ci),
         "sm_link_code_check": ([vp, vp, ctypes.POINTER(cd), ctypes.POINTER(ctypes.c_long)], ci),

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -523,6 +524,8 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //                       RCCL's own ordering)
 //   rccl_sums=1         RCCL contexts: the CG pass's scalar sums through
 //                       ncclAllReduce instead of the in-pass peer all-reduce
+//   hosted_psums=1      host-staged contexts: the CG pass's sums in-pass as on
+//                       RCCL contexts (the multi-shard test of that path)
 //   peer_wait_ms=N      peer transport: time limit of one wait (default 10000)
 //   peer_store=0|1|2    peer transport: the CG pass's face stores as 16-B
 //                       write-through buffer stores (0), 8-B atomic stores (1)
@@ -588,6 +591,8 @@ static int apply_test_opts(sm_ctx *c) {
             c->rccl_ordered = iv ? 1 : 0;
         } else if (k == "rccl_sums") {
             c->peer_sums_wish = iv ? 0 : 1;
+        } else if (k == "hosted_psums") {
+            c->hosted_psums = iv ? 1 : 0;
         } else if (k == "peer_wait_ms") {
             if (iv < 1) return fail(SM_ERR_ARG, "SM_TEST_OPTS: peer_wait_ms must be >= 1");
             c->peer_wait_ticks = 100000ull * (unsigned long long)iv;  // 100-MHz wall clock
@@ -633,6 +638,7 @@ static int apply_test_opts(sm_ctx *c) {
 }
 
 static int rccl_peer_sums_setup(sm_ctx *c);
+static int hosted_peer_sums_setup(sm_ctx *c);
 
 static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device,
                          const void *unique_id, const sm_host_transport *tr, bool loop = false, bool peer = false) {
@@ -775,6 +781,10 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     }
     if (c->hosted) {
         c->tr = *tr;
+        if (int rc = hosted_peer_sums_setup(c); rc != SM_OK) {
+            sm_destroy(c);
+            return rc;
+        }
     } else if (c->peer) {
         // connected by sm_peer_connect (the loopback: here, to itself)
     } else if (c->sharded()) {
@@ -805,45 +815,28 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
 // all-reduces the shard's three sums itself (cg_ticketed_tail, the peer
 // transport's in-pass all-reduce) through a 4-KiB uncached header per shard,
 // instead of an ncclAllReduce after every pass; the halo exchange stays RCCL
-// (north_star). The header handles are all-gathered over the communicator
-// itself, and every shard's success (allocation, IPC open, a handshake
-// all-reduce) is agreed by an ncclAllReduce (min), so all shards take the
-// same path; any failure leaves the context on ncclAllReduce. Never fails
-// the context.
-static int rccl_peer_sums_setup(sm_ctx *c) {
+// (north_star). The header handles are all-gathered over the context's own
+// transport (the communicator; a host-staged context, test option
+// hosted_psums=1, uses its all-reduce callback on byte values), and every
+// shard's success (allocation, IPC open, a handshake all-reduce) is agreed by
+// a min over shards, so all shards take the same path; any failure leaves
+// the context on its transport's all-reduce. Every shard makes every
+// collective call of this function whatever failed locally. Never fails the
+// context on a local failure.
+static int peer_sums_setup(sm_ctx *c, const std::function<int(char *, size_t)> &gather,
+                           const std::function<int(int *)> &agree) {
     c->peer_sums = false;
-    if (!c->peer_sums_wish || !c->comm) return SM_OK;
     const int P = c->loop ? 1 : c->nshard, me = c->loop ? 0 : c->shard;
     const size_t hb = sizeof(hipIpcMemHandle_t);
     int ok = 1;
-    int *flag = nullptr;
-    char *dh = nullptr;
     std::vector<char> hh(hb * P, 0);
-    auto agree = [&]() -> int {  // min over shards of ok
-        HIP_TRY(hipMemcpyAsync(flag, &ok, sizeof ok, hipMemcpyHostToDevice, c->stream));
-        NCCL_TRY(ncclAllReduce(flag, flag, 1, ncclInt32, ncclMin, c->comm, c->stream));
-        HIP_TRY(hipMemcpyAsync(&ok, flag, sizeof ok, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        return SM_OK;
-    };
-    HIP_TRY(hipMalloc(&flag, sizeof(int)));
-    if (hipMalloc(&dh, hb * P) != hipSuccess ||
-        hipExtMallocWithFlags((void **)&c->peer_region, kPeerHdrBytes, hipDeviceMallocUncached) != hipSuccess ||
+    if (hipExtMallocWithFlags((void **)&c->peer_region, kPeerHdrBytes, hipDeviceMallocUncached) != hipSuccess ||
         hipMemset(c->peer_region, 0, kPeerHdrBytes) != hipSuccess ||
         (!c->peer_view_dev && hipMalloc(&c->peer_view_dev, sizeof(PeerView)) != hipSuccess) ||
         hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t *>(hh.data() + hb * me), c->peer_region) != hipSuccess)
         ok = 0;
     (void)hipGetLastError();
-    int rc = SM_OK;
-    if (dh) {  // the handles, all-gathered in place over the communicator
-        if (hipMemcpy(dh, hh.data(), hb * P, hipMemcpyHostToDevice) != hipSuccess) ok = 0;
-        rc = ncclAllGather(dh + hb * me, dh, hb, ncclUint8, c->comm, c->stream) == ncclSuccess ? SM_OK : SM_ERR_RCCL;
-        if (rc == SM_OK && (hipStreamSynchronize(c->stream) != hipSuccess ||
-                            hipMemcpy(hh.data(), dh, hb * P, hipMemcpyDeviceToHost) != hipSuccess))
-            ok = 0;
-    } else {
-        ok = 0;
-    }
+    int rc = gather(hh.data(), hb);
     for (int r = 0; rc == SM_OK && ok && r < P; ++r) {
         if (r == me) continue;
         void *p = nullptr;
@@ -856,7 +849,7 @@ static int rccl_peer_sums_setup(sm_ctx *c) {
             c->peer_open[r] = (char *)p;
         }
     }
-    if (rc == SM_OK) rc = agree();
+    if (rc == SM_OK) rc = agree(&ok);
     if (rc == SM_OK && ok) {
         PeerView &v = c->peer_view;
         v.me = me;
@@ -874,15 +867,14 @@ static int rccl_peer_sums_setup(sm_ctx *c) {
             hipMemcpy(chk, &mine, sizeof mine, hipMemcpyHostToDevice) != hipSuccess)
             ok = 0;
         launch_peer_allreduce(c->stream, chk, 1, v, ++c->peer_coll_seq);  // handshake (time-limited)
-        if (hipStreamSynchronize(c->stream) != hipSuccess || hipMemcpy(&got, chk, sizeof got, hipMemcpyDeviceToHost) != hipSuccess ||
+        if (hipStreamSynchronize(c->stream) != hipSuccess ||
+            hipMemcpy(&got, chk, sizeof got, hipMemcpyDeviceToHost) != hipSuccess ||
             hipMemcpy(&err, c->peer_region + offsetof(PeerHdr, err), sizeof err, hipMemcpyDeviceToHost) != hipSuccess)
             ok = 0;
         if (err || got != 0.5 * P * (P - 1)) ok = 0;
         (void)hipGetLastError();
-        rc = agree();
+        rc = agree(&ok);
     }
-    (void)hipFree(flag);
-    if (dh) (void)hipFree(dh);
     if (rc == SM_OK && ok) {
         c->peer_sums = true;
         return SM_OK;
@@ -896,6 +888,62 @@ static int rccl_peer_sums_setup(sm_ctx *c) {
     c->peer_region = nullptr;
     (void)hipGetLastError();
     return rc;
+}
+
+static int rccl_peer_sums_setup(sm_ctx *c) {
+    c->peer_sums = false;
+    if (!c->peer_sums_wish || !c->comm) return SM_OK;
+    const int P = c->loop ? 1 : c->nshard, me = c->loop ? 0 : c->shard;
+    char *dh = nullptr;  // the handles on the device for the all-gather
+    int *flag = nullptr;
+    HIP_TRY(hipMalloc(&dh, sizeof(hipIpcMemHandle_t) * P));
+    if (hipMalloc(&flag, sizeof(int)) != hipSuccess) {
+        (void)hipFree(dh);
+        return fail(SM_ERR_HIP, "peer sums: allocation failed");
+    }
+    auto gather = [&](char *bytes, size_t nb) -> int {  // in place, over the communicator
+        HIP_TRY(hipMemcpy(dh, bytes, nb * P, hipMemcpyHostToDevice));
+        NCCL_TRY(ncclAllGather(dh + nb * me, dh, nb, ncclUint8, c->comm, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipMemcpy(bytes, dh, nb * P, hipMemcpyDeviceToHost));
+        return SM_OK;
+    };
+    auto agree = [&](int *ok) -> int {  // min over shards
+        HIP_TRY(hipMemcpyAsync(flag, ok, sizeof *ok, hipMemcpyHostToDevice, c->stream));
+        NCCL_TRY(ncclAllReduce(flag, flag, 1, ncclInt32, ncclMin, c->comm, c->stream));
+        HIP_TRY(hipMemcpyAsync(ok, flag, sizeof *ok, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return SM_OK;
+    };
+    const int rc = peer_sums_setup(c, gather, agree);
+    (void)hipFree(dh);
+    (void)hipFree(flag);
+    return rc;
+}
+
+// The same for a host-staged context (test option hosted_psums=1): the RCCL
+// path's in-pass sums over its split launches with several shards on one GPU.
+// The handle bytes travel as small integers through the all-reduce callback
+// (each slot nonzero on one shard only: the sums are exact).
+static int hosted_peer_sums_setup(sm_ctx *c) {
+    c->peer_sums = false;
+    if (!c->hosted_psums) return SM_OK;
+    const int P = c->nshard, me = c->shard;
+    auto gather = [&](char *bytes, size_t nb) -> int {
+        std::vector<double> v(nb * P, 0.0);
+        for (size_t i = 0; i < nb; ++i) v[nb * me + i] = (double)(unsigned char)bytes[nb * me + i];
+        if (c->tr.allreduce_sum(c->tr.user, v.data(), (long)v.size()) != 0)
+            return fail(SM_ERR_ARG, "host transport allreduce failed");
+        for (size_t i = 0; i < nb * P; ++i) bytes[i] = (char)(unsigned char)v[i];
+        return SM_OK;
+    };
+    auto agree = [&](int *ok) -> int {
+        double v = *ok ? 1.0 : 0.0;
+        if (c->tr.allreduce_sum(c->tr.user, &v, 1) != 0) return fail(SM_ERR_ARG, "host transport allreduce failed");
+        *ok = v == (double)P;
+        return SM_OK;
+    };
+    return peer_sums_setup(c, gather, agree);
 }
 
 int sm_create(sm_ctx **out, int Nx, int Nt_global, int nshard, int shard, int device,
@@ -1183,6 +1231,12 @@ int sm_comm_info(const sm_ctx *c, int *transport, int *nranks, int *rank) {
     if (transport) *transport = t;
     if (nranks) *nranks = n;
     if (rank) *rank = r;
+    return SM_OK;
+}
+
+int sm_cg_sums_in_pass(const sm_ctx *c, int *in_pass) {
+    if (!c || !in_pass) return fail(SM_ERR_ARG, "null argument");
+    *in_pass = c->peer || c->peer_sums ? 1 : 0;
     return SM_OK;
 }
 

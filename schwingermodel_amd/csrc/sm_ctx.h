@@ -144,6 +144,7 @@ struct sm_ctx {
     // rccl_sums=1 keeps the ncclAllReduce.
     bool peer_sums = false;
     int peer_sums_wish = 1;
+    int hosted_psums = 0;           // host-staged contexts: the same in-pass sums (test option hosted_psums=1)
     bool hosted = false;            // host-callback transport instead of RCCL
     sm_host_transport tr{};
     double *h_face = nullptr;       // pinned: send_lo, send_hi, recv_lo, recv_hi (4 x up to 8Nx doubles)

@@ -750,6 +750,9 @@ def main():
         ci = [ctypes.c_int(-1) for _ in range(3)]
         sm.check(sm.lib.sm_comm_info(ctx, *(ctypes.byref(v) for v in ci)))
         local["comm_info"] = tuple(v.value for v in ci)  # host-staged: transport 1, no RCCL world
+        ip = ctypes.c_int(-1)
+        sm.check(sm.lib.sm_cg_sums_in_pass(ctx, ctypes.byref(ip)))
+        local["sums_in_pass"] = ip.value
         sm.check(sm.lib.sm_upload_gauge(ctx, P(U[0]), P(U[1])))
         for key, src, fn in (("ref_Dpsi", psi, 0), ("ref_Ddagchi", chi, 1), ("ref_DDdagpsi", psi, 2)):
             out0, out1 = np.empty(V, complex), np.empty(V, complex)
@@ -791,6 +794,7 @@ def main():
             report["dots"] = [list(d["dot"]) for d in gathered]
         if "comm_info" in local:
             report["comm_info"] = [list(d["comm_info"]) for d in gathered]
+            report["sums_in_pass"] = [d.get("sums_in_pass") for d in gathered]
         with open(result_path, "w") as f:
             json.dump(report, f)
     dist.barrier()

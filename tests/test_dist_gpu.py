@@ -35,6 +35,7 @@ def test_sharded_gpu_path_matches_reference(tmp_path, fixture, world):
     assert len({tuple(d) for d in rep["dots"]}) == 1  # identical global dot on every shard
     # sm_comm_info: host-staged transport, no RCCL world (bench.py's rccl_ranks = 1)
     assert rep["comm_info"] == [[1, 1, 0]] * world, rep["comm_info"]
+    assert rep["sums_in_pass"] == [0] * world  # host-staged default: the transport's all-reduce
 
 
 @pytest.mark.parametrize("fixture,world", [("l32x48_b3_m-0p10", 4), ("gen:48x1024:0.3:-0.05", 2)])

@@ -173,6 +173,7 @@ def test_peer_world_matches_reference(tmp_path, fixture, world):
     assert all(rep["cg_converged"])
     assert len({tuple(d) for d in rep["dots"]}) == 1
     assert rep["comm_info"] == [[3, world, r] for r in range(world)], rep["comm_info"]
+    assert rep["sums_in_pass"] == [1] * world, rep["sums_in_pass"]
 
 
 @pytest.mark.multiproc
@@ -228,3 +229,25 @@ def test_peer_wait_time_limit(tmp_path):
     assert rep["apply_s"] < 30, rep
     assert rep["cg_rc"] != 0 and "peer transport" in rep["cg_msg"], rep
     assert rep["cg_s"] < 30, rep
+
+
+@pytest.mark.multiproc
+@pytest.mark.parametrize("fixture,world", [("gen:48x1024:0.3:-0.05", 2), ("gen:32x960:0.4242:0.0", 4),
+                                           ("l64x64_b5_m-0p06", 4), ("l16x16_b2_m-0p19", 4)])
+def test_in_pass_sums_on_split_launches(tmp_path, fixture, world):
+    """The RCCL path's in-pass CG sums (rccl_peer_sums_setup: the pass's last
+    block all-reduces through peer headers, no all-reduce call per pass) with
+    several shards, on the host-staged transport that runs the same split
+    interior / edge launches (test option hosted_psums=1; RCCL itself refuses
+    two ranks on one GPU): the reference's iterations and solution, and
+    bitwise operators (the sums path does not touch them)."""
+    env = dict(sm_opts(hosted_psums=1, cg=5), GPU_MAX_HW_QUEUES="1")
+    rep = run_world("gpu", fixture, world, tmp_path, timeout=200, extra_env=env)
+    c = rep["checks"]
+    for k in ("ref_Dpsi", "ref_Ddagchi", "ref_DDdagpsi", "ref_force"):
+        assert c[k] is True, (k, c)
+    assert c["ref_cgx"] <= 1e-12
+    ref = rep["ref_cg_iters"]
+    assert len(set(rep["cg_iters"])) == 1 and abs(rep["cg_iters"][0] - ref) <= max(1, ref // 100)
+    assert all(rep["cg_converged"])
+    assert rep["sums_in_pass"] == [1] * world, rep["sums_in_pass"]  # the in-pass sums really ran

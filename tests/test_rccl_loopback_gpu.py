@@ -97,6 +97,9 @@ def test_loopback_comm_info(sm):
     loop = sm.Lattice(32, 48, loopback=True)
     try:
         assert loop.comm_info() == ("rccl", 1, 0)
+        ip = ctypes.c_int(-1)
+        sm.check(sm.lib.sm_cg_sums_in_pass(loop.ctx, ctypes.byref(ip)))
+        assert ip.value == 1  # the CG pass's sums in-pass (peer header), the halos over RCCL
     finally:
         loop.close()
     one = sm.Lattice(32, 48)

@@ -248,6 +248,14 @@ u() {
   done
 }
 
+# v: the in-pass sums over split launches with several shards (hosted_psums), then the peer tests, RCCL loopback
+v() {
+  timeout -k 10 900 python -u -m pytest -x -v --timeout 250 --timeout-method thread tests/test_peer_gpu.py \
+    tests/test_rccl_loopback_gpu.py > gpurun_out/r06v_tests.log 2>&1 &&
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 250 --timeout-method thread tests/test_dist_gpu.py \
+    -k "sharded_gpu_path" > gpurun_out/r06v_tests2.log 2>&1
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
