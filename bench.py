@@ -546,7 +546,7 @@ def comm_world(args, rt, sh):
     if hasattr(sh.L, "ctx"):
         sh.sm.check(sh.sm.lib.sm_cg_sums_in_pass(sh.L.ctx, ctypes.byref(ip)))
     return {"transport": transport, ("peer_ranks" if transport == "peer" else "rccl_ranks"): [nmin, nmax],
-            "cg_sums": "in-pass" if ip.value else "collective"}
+            "cg_sums": "in-pass" if ip.value else ("collective" if rt["world"] > 1 else "one shard")}
 
 
 def cg_bytes_per_site(sh, cg_path):
