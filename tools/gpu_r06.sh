@@ -256,6 +256,19 @@ v() {
     -k "sharded_gpu_path" > gpurun_out/r06v_tests2.log 2>&1
 }
 
+# w: kernel-trace timelines of the t-shard CG pass at 4096 x 512 through the RCCL loopback (split launches, the
+#    face exchange, in-pass sums) and the peer loopback (one launch)
+w() {
+  local L="python3 -u tools/loopback_probe.py --shapes 4096x512 --iters 60 --rounds 1 --applies 1 --warmup 5"
+  for ctx in loopback peer; do
+    rm -rf gpurun_out/r06w_$ctx
+    timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r06w_$ctx -o run -- $L --contexts $ctx \
+      > gpurun_out/r06w_$ctx.log 2>&1 &&
+    python3 tools/trace_pass.py gpurun_out/r06w_$ctx/run_kernel_trace.csv --last 40 > gpurun_out/r06w_${ctx}_trace.txt 2>&1 \
+      || return 1
+  done
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
