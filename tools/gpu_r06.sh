@@ -269,6 +269,19 @@ w() {
   done
 }
 
+# x: the stream-ordering events without / with the system-scope fence on the RCCL loopback (twice each), the
+#    RCCL loopback tests, then the traces of w (ran on a build with test option ev_fence, since reverted: no effect)
+x() {
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_rccl_loopback_gpu.py \
+    > gpurun_out/r06x_tests.log 2>&1 || return 1
+  local L="python -u tools/loopback_probe.py --shapes 4096x512,4096x1024,4096x2048 --iters 200 --rounds 3 --applies 20 --contexts one,loopback"
+  for i in 1 2; do
+    timeout -k 10 300 $L > gpurun_out/r06x_nofence_$i.log 2>&1 &&
+    SM_TEST_OPTS=ev_fence=1 timeout -k 10 300 $L > gpurun_out/r06x_fence_$i.log 2>&1 || return 1
+  done
+  w
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
