@@ -282,6 +282,28 @@ x() {
   w
 }
 
+# y: the link codes stored per site (code_ilv=1) against the two planes -- its tests and the link tests with
+#    the option on, four interleaved bench pairs (200 steps), then the pass's L2 counters both ways (ran on build
+#    17ede56d9968562b with test option code_ilv, since removed: reads unchanged, 0.4 % slower)
+y() {
+  python3 -c "import schwingermodel_amd as s; print(s.lib.sm_build_id().decode())" > gpurun_out/r06y_build_id.txt &&
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py \
+    -k "link" > gpurun_out/r06y_tests.log 2>&1 &&
+  SM_TEST_OPTS=code_ilv=1 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+    tests/test_gpu_parity.py tests/test_cg_paths_gpu.py -k "link or cg_vs_reference or tshard" \
+    > gpurun_out/r06y_tests_ilv.log 2>&1 || return 1
+  local B="python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-weak --evolved-trajectories 0"
+  for i in 1 2 3 4; do
+    SM_TEST_OPTS=code_ilv=1 timeout -k 10 300 $B > gpurun_out/r06y_ilv_$i.log 2>&1 &&
+    timeout -k 10 300 $B > gpurun_out/r06y_planes_$i.log 2>&1 || return 1
+  done
+  for m in 0 1; do
+    SM_TEST_OPTS=code_ilv=$m timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum \
+      --output-format csv -d gpurun_out/r06y_tcc_$m -o run -- python3 tools/tune_shapes.py 4096x4096:1,64,1 \
+      --iters 30 --rounds 1 > gpurun_out/r06y_tcc_$m.log 2>&1 || return 1
+  done
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
