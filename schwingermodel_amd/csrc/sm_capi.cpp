@@ -546,6 +546,8 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //                       sm_set_placement_probe sets the default)
 //   probe_min_mib=N     smallest field (MiB) whose context runs the probe
 //   link_angles=0|1     recompute-Ad pass reads the links as one-double codes
+//   kernel_events=0|1   t-shard CG pass: hand-offs between the streams on events
+//                       recorded by the launches themselves (1, the default) or markers
 //   bt=64|128|256       Dirac apply t-columns per block
 //   eo_fused=0, eo_cg_td=0, eo_cg_folded=1   even-odd operator / CG forms
 //   debug_cg=1          CG host loops print their status (stderr)
@@ -601,6 +603,8 @@ static int apply_test_opts(sm_ctx *c) {
             c->peer_store = iv;
         } else if (k == "ra_strip") {
             cg_ra_set_strip(c->racfg, c->g, iv);
+        } else if (k == "kernel_events") {
+            c->kernel_events = iv ? 1 : 0;
         } else if (k == "ra_xbal") {
             c->racfg.xbal = iv ? 1 : 0;
         } else if (k == "ra_remap") {
@@ -744,6 +748,7 @@ static int create_common(sm_ctx **out, int Nx, int Nt_global, int nshard, int sh
     chk(hipMalloc(&c->faces4, sizeof(double2) * 64 * (size_t)Nx));
     chk(hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming));
     chk(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
+    chk(hipEventCreateWithFlags(&c->ev_int, hipEventDisableTiming));
     chk(hipEventCreateWithFlags(&c->ev_rccl, hipEventDisableTiming));
     chk(hipMalloc(&c->partials, sizeof(double2) * 2 * (size_t)np));
     chk(hipMalloc(&c->sums, sizeof(double2) * 4));
@@ -1083,7 +1088,7 @@ int sm_destroy(sm_ctx *c) {
     if (c->h_face) (void)hipHostFree(c->h_face);
     if (c->h_red) (void)hipHostFree(c->h_red);
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
-    for (hipEvent_t ev : {c->ev_ready, c->ev_halo, c->ev_rccl})
+    for (hipEvent_t ev : {c->ev_ready, c->ev_halo, c->ev_int, c->ev_rccl})
         if (ev) (void)hipEventDestroy(ev);
     if (c->comm_stream && c->own_comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -1589,15 +1594,30 @@ static int cg_ra_pass(sm_ctx *c) {
     const bool psums = c->peer_sums && red;
     const PeerView *pv = psums ? c->peer_view_dev : nullptr;
     const unsigned long long pseq = psums ? ++c->peer_coll_seq : 0;
-    auto pass = [&](const CGFusedCfg &cf, int tb0, int tbn, hipStream_t st, int pbase, double2 *fsend) {
+    auto pass = [&](const CGFusedCfg &cf, int tb0, int tbn, hipStream_t st, int pbase, double2 *fsend,
+                    hipEvent_t stop = nullptr) {
         const int lb = launch_cg_ra(st, c->g, cf, c->kshards(), d1, d2, dn, c->cg_x, c->U, f1, f2, face4_recv_U(c),
                                     c->cg_mass, j, c->sc, c->partials, tb0, tbn, nullptr, ua, c->Uang_face, fsend,
                                     pbase, tail ? c->tick : nullptr, nparts_pass, c->gsum, sums, red ? 1 : 0,
-                                    c->link_fmt, nullptr, pv, pseq, 2 /* faces: plain stores, local */);
+                                    c->link_fmt, nullptr, pv, pseq, 2 /* faces: plain stores, local */, 0, stop);
         if (lb) c->cg_link_bytes_last = lb;
     };
-    HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
-    HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
+    // Kernel-carried events (kernel_events): when this pass enqueues nothing on
+    // the main stream after its interior launch (in-pass sums, ticketed tail,
+    // scalars in the next pass), that launch records ev_int itself, and the
+    // next pass's comm stream waits on it -- everything the edge launch needs
+    // from the main stream -- instead of on a marker recorded behind it; the
+    // edge launch likewise records ev_halo. ~3 us off each pass's critical
+    // path (tools/stream_gap_probe.hip). Any other pass (the first of an
+    // sm_cg_iterate call, or one enqueueing more) records the marker.
+    const bool kev = c->kernel_events && split && psums && red && tail && !deferred;
+    if (kev && c->ev_int_pass == j - 1 && !first) {
+        HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_int, 0));
+    } else {
+        HIP_TRY(hipEventRecord(c->ev_ready, c->stream));
+        HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->ev_ready, 0));
+    }
+    c->ev_int_pass = -1;
     rccl_joined(c, c->comm_stream, c->stream);
     // d_{j-1}'s faces: already in slot j & 1 if pass j-1 sent them (pipe), or
     // packed by pass j-1's edge launch and sent now (deferred)
@@ -1611,9 +1631,12 @@ static int cg_ra_pass(sm_ctx *c) {
     c->cg_faces_packed = 0;
     // edge t-blocks (tb_hi, TBk) and [0, tb_lo), wrapping: one launch on the
     // comm stream behind the faces, concurrent with the interior launch
-    if (split) pass(ec, tb_hi + 1, nedge, c->comm_stream, nint * fc.XB, pipe ? face4_send(c, 0) : nullptr);
-    HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
-    if (split) pass(fc, tb_lo, nint, c->stream, 0, nullptr);
+    if (split)
+        pass(ec, tb_hi + 1, nedge, c->comm_stream, nint * fc.XB, pipe ? face4_send(c, 0) : nullptr,
+             kev ? c->ev_halo : nullptr);
+    if (!kev) HIP_TRY(hipEventRecord(c->ev_halo, c->comm_stream));
+    if (split) pass(fc, tb_lo, nint, c->stream, 0, nullptr, kev ? c->ev_int : nullptr);
+    if (kev) c->ev_int_pass = j;
     if (deferred) {  // d_j's faces stay packed until pass j+1
         c->cg_faces_for = j + 1;
         c->cg_faces_packed = 1;
@@ -1664,6 +1687,7 @@ int sm_cg_iterate(sm_ctx *c, int niter) {
         }
         c->cg_issued++;
     }
+    c->ev_int_pass = -1;  // whatever follows on the main stream is not behind ev_int
     if (c->cg_fused >= 4 && c->cg_flush_pass >= 0) {  // redundant scalars: evaluate the last pass for the host
         const long J = c->cg_flush_pass;
         const int nparts = c->cg_flush_nparts;

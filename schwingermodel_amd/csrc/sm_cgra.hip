@@ -53,6 +53,8 @@
 // The order is fixed, so results stay run-to-run reproducible.
 #include <type_traits>
 
+#include <hip/hip_ext.h>
+
 #include "sm_device.h"
 #include "sm_internal.h"
 #include "sm_linkcode.h"
@@ -713,30 +715,41 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
     return c;
 }
 
+// stop != null: the launch itself records the event at the kernel's end
+// (hipExtLaunchKernelGGL), so a stream that waits for this kernel needs no
+// marker packet behind it on the launching stream (~3 us per cross-stream
+// hand-off, tools/stream_gap_probe.hip)
+template <typename K>
+static void ra_launch(K kern, dim3 grid, dim3 block, size_t lds, hipStream_t s, const RAArgs &a, hipEvent_t stop) {
+    if (stop) hipExtLaunchKernelGGL(kern, grid, block, (uint32_t)lds, s, nullptr, stop, 0u, a);
+    else hipLaunchKernelGGL(kern, grid, block, lds, s, a);
+}
+
 template <int SH, int RED, int UC, int F>
-static void ra_go(int xp, int tk, dim3 grid, dim3 block, size_t lds, hipStream_t s, const RAArgs &a, int rev = 0) {
+static void ra_go(int xp, int tk, dim3 grid, dim3 block, size_t lds, hipStream_t s, const RAArgs &a, int rev = 0,
+                  hipEvent_t stop = nullptr) {
     // march schedules: one-shard tail passes, and the peer transport's one-launch t-shard pass
     if constexpr (F == 2 && ((SH == 0 && RED == 0) || (SH == 1 && RED == 2))) {
         if (tk && rev == 1) {
-            if (xp) hipLaunchKernelGGL((cg_ra_kernel<SH, 1, F, RED, UC, 1, 1>), grid, block, lds, s, a);
-            else hipLaunchKernelGGL((cg_ra_kernel<SH, 0, F, RED, UC, 1, 1>), grid, block, lds, s, a);
+            if (xp) ra_launch(cg_ra_kernel<SH, 1, F, RED, UC, 1, 1>, grid, block, lds, s, a, stop);
+            else ra_launch(cg_ra_kernel<SH, 0, F, RED, UC, 1, 1>, grid, block, lds, s, a, stop);
             return;
         }
         if (tk && rev == 2) {
-            if (xp) hipLaunchKernelGGL((cg_ra_kernel<SH, 1, F, RED, UC, 1, 2>), grid, block, lds, s, a);
-            else hipLaunchKernelGGL((cg_ra_kernel<SH, 0, F, RED, UC, 1, 2>), grid, block, lds, s, a);
+            if (xp) ra_launch(cg_ra_kernel<SH, 1, F, RED, UC, 1, 2>, grid, block, lds, s, a, stop);
+            else ra_launch(cg_ra_kernel<SH, 0, F, RED, UC, 1, 2>, grid, block, lds, s, a, stop);
             return;
         }
     }
     if constexpr (F == 2) {
         if (tk) {
-            if (xp) hipLaunchKernelGGL((cg_ra_kernel<SH, 1, F, RED, UC, 1>), grid, block, lds, s, a);
-            else hipLaunchKernelGGL((cg_ra_kernel<SH, 0, F, RED, UC, 1>), grid, block, lds, s, a);
+            if (xp) ra_launch(cg_ra_kernel<SH, 1, F, RED, UC, 1>, grid, block, lds, s, a, stop);
+            else ra_launch(cg_ra_kernel<SH, 0, F, RED, UC, 1>, grid, block, lds, s, a, stop);
             return;
         }
     }
-    if (xp) hipLaunchKernelGGL((cg_ra_kernel<SH, 1, F, RED, UC, 0>), grid, block, lds, s, a);
-    else hipLaunchKernelGGL((cg_ra_kernel<SH, 0, F, RED, UC, 0>), grid, block, lds, s, a);
+    if (xp) ra_launch(cg_ra_kernel<SH, 1, F, RED, UC, 0>, grid, block, lds, s, a, stop);
+    else ra_launch(cg_ra_kernel<SH, 0, F, RED, UC, 0>, grid, block, lds, s, a, stop);
 }
 
 template <int UC>
@@ -759,7 +772,7 @@ int launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsha
                   int tb0, int tbn, const double2 *prev_partials, const double *Uang, const double *fUang,
                   double2 *fsend, int pbase, unsigned *tick, int ntiles, double2 *gsum, double2 *out3,
                   int red_sums, int link_fmt, double2 *fsendh, const PeerView *peer, unsigned long long pseq,
-                  int pstore, int sched) {
+                  int pstore, int sched, hipEvent_t stop) {
     if (tbn <= 0) return 0;
     RAArgs a;
     a.d1 = d1; a.d2 = d2; a.dn = dn; a.x = x; a.U = U;
@@ -827,9 +840,9 @@ int launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsha
             a.flip = (int)(pass & 1);
             a.alt = 1;
         }
-        if (uc == 2) ra_go<1, 2, 2, 2>(xp, tk, grid, block, lds, s, a, prev);
-        else if (uc) ra_go<1, 2, 1, 2>(xp, tk, grid, block, lds, s, a, prev);
-        else ra_go<1, 2, 0, 2>(xp, tk, grid, block, lds, s, a, prev);
+        if (uc == 2) ra_go<1, 2, 2, 2>(xp, tk, grid, block, lds, s, a, prev, stop);
+        else if (uc) ra_go<1, 2, 1, 2>(xp, tk, grid, block, lds, s, a, prev, stop);
+        else ra_go<1, 2, 0, 2>(xp, tk, grid, block, lds, s, a, prev, stop);
         return link_bytes;
     }
     // one shard with the ticketed tail: odd passes take the tiles in reverse

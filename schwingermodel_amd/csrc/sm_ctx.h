@@ -102,6 +102,14 @@ struct sm_ctx {
     hipStream_t comm_stream = nullptr;  // halo exchange overlapped with interior compute (hosted: == stream)
     bool own_comm_stream = false;       // comm_stream created by (and destroyed with) this context
     hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
+    // t-shard CG pass (split launches): the interior launch records ev_int at
+    // its own end (hipExtLaunchKernelGGL), and the next pass's comm stream
+    // waits on it instead of a marker behind it on the main stream; valid for
+    // pass ev_int_pass only (-1: record the marker). kernel_events = 0 keeps
+    // the markers (test option).
+    hipEvent_t ev_int = nullptr;
+    long ev_int_pass = -1;
+    int kernel_events = 1;
     hipEvent_t ev_rccl = nullptr;   // orders an RCCL operation after the previous one on the other stream
     hipStream_t rccl_last = nullptr;  // stream of the last RCCL operation (sm_capi.cpp rccl_order)
     int rccl_ordered = 1;           // test option rccl_order=0: no ordering events (A/B)

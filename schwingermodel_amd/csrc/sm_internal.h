@@ -151,7 +151,7 @@ int launch_cg_ra(hipStream_t s, const Geometry &g, const CGFusedCfg &c, int nsha
                  const double *fUang = nullptr, double2 *fsend = nullptr, int pbase = 0,
                  unsigned *tick = nullptr, int ntiles = 0, double2 *gsum = nullptr, double2 *out3 = nullptr,
                  int red_sums = 0, int link_fmt = 1, double2 *fsendh = nullptr, const PeerView *peer = nullptr,
-                 unsigned long long pseq = 0, int pstore = 0, int sched = 0);
+                 unsigned long long pseq = 0, int pstore = 0, int sched = 0, hipEvent_t stop = nullptr);
 // Resident blocks per CU of the t-shard pass kernel at c's block size (0 if
 // the runtime cannot tell); link_fmt 0 = complex links, 1 / 2 = the code forms.
 int cg_ra_shard_blocks_per_cu(const CGFusedCfg &c, int link_fmt);

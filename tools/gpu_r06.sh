@@ -304,6 +304,19 @@ y() {
   done
 }
 
+# z: the t-shard CG pass's stream hand-offs on events recorded by the launches themselves (kernel_events=1,
+#    the new default) against markers (0): the RCCL loopback and in-pass-sums tests, the loopback twice each way
+z() {
+  python3 -c "import schwingermodel_amd as s; print(s.lib.sm_build_id().decode())" > gpurun_out/r06z_build_id.txt &&
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_rccl_loopback_gpu.py \
+    tests/test_cg_paths_gpu.py tests/test_peer_gpu.py -k "loopback or tshard or in_pass" > gpurun_out/r06z_tests.log 2>&1 || return 1
+  local L="python -u tools/loopback_probe.py --shapes 4096x512,4096x1024,4096x2048 --iters 200 --rounds 3 --applies 5 --contexts one,loopback"
+  for i in 1 2; do
+    timeout -k 10 300 $L > gpurun_out/r06z_kev1_$i.log 2>&1 &&
+    SM_TEST_OPTS=kernel_events=0 timeout -k 10 300 $L > gpurun_out/r06z_kev0_$i.log 2>&1 || return 1
+  done
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
