@@ -317,6 +317,22 @@ z() {
   done
 }
 
+# aa: the RCCL / host-staged t-shard CG pass as one launch (test option rccl_onelaunch, since removed: faces
+#     exchanged behind the pass on the comm stream, the next pass's face-reading waves waiting for a flag) -- the
+#     RCCL loopback, t-shard schedule and in-pass-sums tests, then the loopback against the split launches, twice.
+#     Ran on builds 6bdcb069660ca470 (slower) and 920ae3ae89b8fbc1 (a wait timed out: DESIGN §7)
+aa() {
+  python3 -c "import schwingermodel_amd as s; print(s.lib.sm_build_id().decode())" > gpurun_out/r06aa_build_id.txt &&
+  timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_rccl_loopback_gpu.py \
+    tests/test_cg_paths_gpu.py tests/test_peer_gpu.py tests/test_dist_gpu.py -k "loopback or tshard or in_pass or sharded" \
+    > gpurun_out/r06aa_tests.log 2>&1 || return 1
+  local L="python -u tools/loopback_probe.py --shapes 4096x512,4096x1024,4096x2048 --iters 200 --rounds 3 --applies 5 --contexts one,loopback,peer"
+  for i in 1 2; do
+    timeout -k 10 300 $L > gpurun_out/r06aa_one_$i.log 2>&1 &&
+    SM_TEST_OPTS=rccl_onelaunch=0 timeout -k 10 300 $L > gpurun_out/r06aa_split_$i.log 2>&1 || return 1
+  done
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
