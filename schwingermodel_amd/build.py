@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libsm_hip.so")
-SOURCES = ["sm_kernels.hip", "sm_cgfused.hip", "sm_cgra.hip", "sm_eotd.hip", "sm_gauge.hip", "sm_eo.hip", "sm_peer.hip", "sm_capi.cpp", "sm_place.cpp", "sm_conf.cpp", "sm_md.cpp", "sm_hmc.cpp",
+SOURCES = ["sm_kernels.hip", "sm_cgfused.hip", "sm_cgra.hip", "sm_eotd.hip", "sm_gauge.hip", "sm_eo.hip", "sm_peer.hip", "sm_capi.cpp", "sm_comm.cpp", "sm_place.cpp", "sm_conf.cpp", "sm_md.cpp", "sm_hmc.cpp",
            "sm_eo.cpp"]
 HEADERS = ["sm_internal.h", "sm_fields.h", "sm_device.h", "sm_ctx.h", "sm_linkcode.h", "sm_peer.h"]
 

@@ -111,7 +111,7 @@ struct sm_ctx {
     long ev_int_pass = -1;
     int kernel_events = 1;
     hipEvent_t ev_rccl = nullptr;   // orders an RCCL operation after the previous one on the other stream
-    hipStream_t rccl_last = nullptr;  // stream of the last RCCL operation (sm_capi.cpp rccl_order)
+    hipStream_t rccl_last = nullptr;  // stream of the last RCCL operation (sm_comm.cpp rccl_order)
     int rccl_ordered = 1;           // test option rccl_order=0: no ordering events (A/B)
     // t-shards: the edge block-columns run on the comm stream right after the
     // halo, concurrently with the interior launch on the main stream.
@@ -148,7 +148,7 @@ struct sm_ctx {
     unsigned long long peer_wait_ticks = sm::kPeerWaitTicks;  // one wait's time limit (test option peer_wait_ms)
     // RCCL contexts: the recompute-Ad pass's scalar sums all-reduced in its own last
     // block through 4-KiB peer headers (sm_peer.h) instead of an ncclAllReduce per
-    // pass; the halos stay RCCL (sm_capi.cpp rccl_peer_sums_setup). Test option
+    // pass; the halos stay RCCL (sm_comm.cpp rccl_peer_sums_setup). Test option
     // rccl_sums=1 keeps the ncclAllReduce.
     bool peer_sums = false;
     int peer_sums_wish = 1;
@@ -242,7 +242,7 @@ int exchange_faces_multi(sm_ctx *c, hipStream_t s, int n, double2 *const *slo, d
                          double2 *const *rlo, double2 *const *rhi, size_t cnt);
 // RCCL contexts hold ONE communicator; every RCCL operation runs on the
 // stream it is issued on, ordered on the GPU after the previous RCCL
-// operation (sm_capi.cpp rccl_order), in host issue order -- the same
+// operation (sm_comm.cpp rccl_order), in host issue order -- the same
 // sequence on every rank. n face exchanges in one group:
 // send_up[i] -> up rank's recv_down[i], send_down[i] -> down rank's recv_up[i].
 int rccl_p2p_group(sm_ctx *c, hipStream_t s, int n, const double2 *const *send_up, double2 *const *recv_down,
@@ -268,6 +268,23 @@ double2 *face2_recv(sm_ctx *c, int which);  // 0: d, 1: r, 2: U, 3: Ad
 double2 *face4_recv_U(sm_ctx *c);           // 4-deep ghost links (recompute-Ad CG)
 bool cg_ra_ok(const sm_ctx *c);             // the recompute-Ad pass fits this shard (Wt >= 4 when sharded)
 int exchange_ghost_U(sm_ctx *c);
+// (sm_comm.cpp) the peer transport connected; the in-pass CG sums' headers of an
+// RCCL / host-staged context (agreed over the shards; never fail on a local
+// failure); the peer view and its handshake; the recompute-Ad pass's 4-deep
+// faces: send buffers, receive slot of pass `pass`, pack + exchange into recv
+int up_rank(const sm_ctx *c);    // t + 1 neighbour shard (periodic)
+int down_rank(const sm_ctx *c);  // t - 1 neighbour shard
+int peer_ready(const sm_ctx *c);
+int rccl_peer_sums_setup(sm_ctx *c);
+int hosted_peer_sums_setup(sm_ctx *c);
+int peer_set_view(sm_ctx *c);
+double2 *face4_send(sm_ctx *c, int hi);
+double2 *face4_recv_d(sm_ctx *c, long pass);
+int halo4(sm_ctx *c, hipStream_t s, const double2 *field, double2 *recv);
+// the fused CG kernel's 2-deep faces of nf <= 3 fields in one transport round
+// (receive buffers faces[f]); halo2: one field on the main stream
+int halo2_multi(sm_ctx *c, hipStream_t s, const double2 *const *fields, double2 *const *faces, int nf);
+int halo2(sm_ctx *c, const double2 *field, double2 *face);
 
 // Streamed CG buffers and the placement probe (sm_place.cpp)
 size_t stream_alloc_bytes(size_t bytes, size_t floor_bytes = size_t(2) << 30);

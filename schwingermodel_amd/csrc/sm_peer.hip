@@ -89,7 +89,7 @@ void launch_peer_exchange(hipStream_t s, const PeerXfer &x, const PeerView &v, u
 // proj_face_value) stored straight into the neighbours' apply slot seq % 4:
 // side 0 into the down neighbour's hi (its t = Wt), side 1 into the up
 // neighbour's lo (its t = -1); then the handoff. The receiver's stencil reads
-// its own slot (sm_capi.cpp halo) in the next kernel.
+// its own slot (sm_comm.cpp halo) in the next kernel.
 __global__ void __launch_bounds__(256) peer_pack_proj_kernel(int Nx, int Wt, long V, const double2 *f,
                                                              const double2 *U, int kind, PeerView v,
                                                              unsigned long long seq, unsigned *tick) {
