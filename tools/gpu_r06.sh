@@ -333,6 +333,38 @@ aa() {
   done
 }
 
+# ab: (build 7947ebe3c99e0868 + tools/exp_stream_build.py) where the CG pass's reads above its algorithmic bytes go -- the pass's L2 read requests with each stream
+#     pinned to one row per tile (counter-only libraries from tools/exp_stream_build.py; wrong values) against
+#     the product library, 4096^2; then the x-halo rows alone (d1h, d2h, uh, allh)
+ab() {
+  for v in ${AB_VARIANTS:-base d1 d2 u x d1h d2h uh allh}; do
+    (
+      if [ "$v" != base ]; then export SM_LIB_PATH=$PWD/tools/exp/libsm_hip_s_$v.so; fi
+      timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum --output-format csv \
+        -d gpurun_out/r06ab_tcc_$v -o run -- python3 tools/tune_shapes.py 4096x4096:1,64,1 --iters 30 --rounds 1 \
+        > gpurun_out/r06ab_tcc_$v.log 2>&1
+    ) || return 1
+  done
+}
+
+# ac: 2-wave blocks on x-adjacent chunks of one t-window (test option ra_xpair=1, since removed: slower, more
+#     reads; ran on build 45632ff9269128ae) at 4096^2 -- its tests, four interleaved bench pairs (200 steps), then
+#     the pass's L2 read requests both ways
+ac() {
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_cg_paths_gpu.py \
+    -k "xpair or ticketed" > gpurun_out/r06ac_tests.log 2>&1 || return 1
+  local B="python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-weak --evolved-trajectories 0"
+  for i in 1 2 3 4; do
+    SM_TEST_OPTS=ra_xpair=1 timeout -k 10 300 $B > gpurun_out/r06ac_xpair_$i.log 2>&1 &&
+    timeout -k 10 300 $B > gpurun_out/r06ac_default_$i.log 2>&1 || return 1
+  done
+  for m in 0 1; do
+    SM_TEST_OPTS=ra_xpair=$m timeout -s KILL 150 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum \
+      --output-format csv -d gpurun_out/r06ac_tcc_$m -o run -- python3 bench.py --steps 30 --warmup 5 --applies 5 \
+      --no-cpu-baseline --no-weak --evolved-trajectories 0 > gpurun_out/r06ac_tcc_$m.log 2>&1 || return 1
+  done
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
