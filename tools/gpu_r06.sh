@@ -365,6 +365,13 @@ ac() {
   done
 }
 
+# ad: one dispatch round of long chunks at 4096^2 (27 x 152 / 26 x 160 rows: 1998 / 1924 one-wave tiles for
+#     2048 slots; the x-halo rows are 5 % of a chunk instead of 12.5 %) against 64 / 128-row chunks, interleaved
+ad() {
+  timeout -k 10 400 python3 -u tools/tune_shapes.py 4096x4096:1,64,1 4096x4096:1,152,1 4096x4096:1,160,1 \
+    4096x4096:1,152,1,0,1 4096x4096:1,128,1 4096x4096:1,256,1 --iters 100 --rounds 4 > gpurun_out/r06ad_shapes.log 2>&1
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
