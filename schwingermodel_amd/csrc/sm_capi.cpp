@@ -259,6 +259,7 @@ int sm_comm_unique_id(void *id_out, int id_bytes) {
 //                       sm_set_placement_probe sets the default)
 //   probe_min_mib=N     smallest field (MiB) whose context runs the probe
 //   link_angles=0|1     recompute-Ad pass reads the links as one-double codes
+//   ra_xchunk=N         recompute-Ad pass: N rows per tile (with ra_xbal=1: ceil(Nx/N) balanced chunks)
 //   kernel_events=0|1   t-shard CG pass: hand-offs between the streams on events
 //                       recorded by the launches themselves (1, the default) or markers
 //   bt=64|128|256       Dirac apply t-columns per block
@@ -318,6 +319,10 @@ static int apply_test_opts(sm_ctx *c) {
             cg_ra_set_strip(c->racfg, c->g, iv);
         } else if (k == "kernel_events") {
             c->kernel_events = iv ? 1 : 0;
+        } else if (k == "ra_xchunk") {  // rows per tile of the recompute-Ad pass (XB follows)
+            if (iv < 2 || iv > c->g.Nx) return fail(SM_ERR_ARG, "SM_TEST_OPTS: ra_xchunk must be 2..Nx");
+            c->racfg.xchunk = iv;
+            c->racfg.XB = (c->g.Nx + iv - 1) / iv;
         } else if (k == "ra_xbal") {
             c->racfg.xbal = iv ? 1 : 0;
         } else if (k == "ra_remap") {

@@ -687,10 +687,16 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
     // 2049 / 2044 all forward; 8192^2 (config 5, 4-wave blocks): 7.92-7.95 s
     // for 1 against 8.24 s for 2 and 8.48 s all forward
     // (profiles/r03_ij_march_schedule_ab.jsonl, r03_n_c5_march_schedule.jsonl).
+    // Round 6: 4096^2 takes 40 balanced chunks (102-103 rows; 74 x 40 = 2960
+    // one-wave tiles) instead of 64 chunks of 64 rows: 2327-2336 against
+    // 2277-2284 it/s in four interleaved bench pairs, each its own context
+    // and placement probe (profiles/r06_ag_chunks40_bench_ab.jsonl). The
+    // optimum is sharp -- 38 / 42 chunks are 2-8 % slower than 64 rows
+    // (r06_af_chunk_count_scan.jsonl) -- so it is a measured point, not a rule.
     c.rev_odd = 1;
-    static const int kShapes[][5] = {  // Nx, Wt, waves per block, rows per block, march schedule
-        {4096, 4096, 1, 64, 2}, {4096, 2048, 1, 32, 1}, {4096, 1024, 1, 40, 1}, {4096, 512, 1, 48, 1},
-        {8192, 8192, 4, 32, 1}, {8192, 1024, 1, 32, 1}, {2048, 2048, 1, 64, 1},
+    static const int kShapes[][6] = {  // Nx, Wt, waves per block, rows per block, march schedule, balanced chunks
+        {4096, 4096, 1, 103, 2, 1}, {4096, 2048, 1, 32, 1, 0}, {4096, 1024, 1, 40, 1, 0}, {4096, 512, 1, 48, 1, 0},
+        {8192, 8192, 4, 32, 1, 0},  {8192, 1024, 1, 32, 1, 0}, {2048, 2048, 1, 64, 1, 0},
     };
     bool known = false;
     for (const auto &k : kShapes)
@@ -698,6 +704,7 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
             c.wpb = k[2];
             c.xchunk = k[3];
             c.rev_odd = k[4];
+            c.xbal = k[5];
             known = true;
         }
     if (!known && g.Nx >= 2048 && g.Wt >= 256) {

@@ -372,6 +372,30 @@ ad() {
     4096x4096:1,152,1,0,1 4096x4096:1,128,1 4096x4096:1,256,1 --iters 100 --rounds 4 > gpurun_out/r06ad_shapes.log 2>&1
 }
 
+# ae: whole dispatch rounds at 4096^2 (74 wave columns x balanced chunks: 55 chunks = 4070 tiles ~ 2 rounds of 2048,
+#     52 = 3848, 40 = 2960, 27 = 1998) against the default 64-row chunks, interleaved
+ae() {
+  timeout -k 10 500 python3 -u tools/tune_shapes.py 4096x4096:1,64,1 4096x4096:1,75,1,0,1 4096x4096:1,76,1 \
+    4096x4096:1,79,1,0,1 4096x4096:1,103,1,0,1 4096x4096:1,152,1 --iters 100 --rounds 5 > gpurun_out/r06ae_shapes.log 2>&1
+}
+
+# af: balanced chunk counts 34..48 at 4096^2 (the 40-chunk form won in ae) against the default, interleaved
+af() {
+  timeout -k 10 600 python3 -u tools/tune_shapes.py 4096x4096:1,64,1 4096x4096:1,121,1,0,1 4096x4096:1,114,1,0,1 \
+    4096x4096:1,108,1,0,1 4096x4096:1,103,1,0,1 4096x4096:1,98,1,0,1 4096x4096:1,94,1,0,1 4096x4096:1,90,1,0,1 \
+    4096x4096:1,86,1,0,1 --iters 100 --rounds 5 > gpurun_out/r06af_shapes.log 2>&1
+}
+
+# ag: 40 balanced chunks (102-103 rows) at 4096^2 as the context's geometry from creation (the placement probe
+#     then tunes for it: SM_TEST_OPTS ra_xchunk=103,ra_xbal=1) against the default, four interleaved bench pairs
+ag() {
+  local B="python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-weak --evolved-trajectories 0"
+  for i in 1 2 3 4; do
+    SM_TEST_OPTS=ra_xchunk=103,ra_xbal=1 timeout -k 10 300 $B > gpurun_out/r06ag_c40_$i.log 2>&1 &&
+    timeout -k 10 300 $B > gpurun_out/r06ag_default_$i.log 2>&1 || return 1
+  done
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
