@@ -693,9 +693,13 @@ CGFusedCfg cg_ra_config(const Geometry &g) {
     // and placement probe (profiles/r06_ag_chunks40_bench_ab.jsonl). The
     // optimum is sharp -- 38 / 42 chunks are 2-8 % slower than 64 rows
     // (r06_af_chunk_count_scan.jsonl) -- so it is a measured point, not a rule.
+    // 4096 x 512 (config 4's 8-GPU shard) takes 28 rows instead of 48: RCCL
+    // loopback 0.0849 / 0.0856 against 0.0889 / 0.0885 ms per iteration, one
+    // shard 0.0697 / 0.0700 against 0.0716 / 0.0718 (two interleaved scans,
+    // r06_aj_tshard_rows_4096x512.jsonl).
     c.rev_odd = 1;
     static const int kShapes[][6] = {  // Nx, Wt, waves per block, rows per block, march schedule, balanced chunks
-        {4096, 4096, 1, 103, 2, 1}, {4096, 2048, 1, 32, 1, 0}, {4096, 1024, 1, 40, 1, 0}, {4096, 512, 1, 48, 1, 0},
+        {4096, 4096, 1, 103, 2, 1}, {4096, 2048, 1, 32, 1, 0}, {4096, 1024, 1, 40, 1, 0}, {4096, 512, 1, 28, 1, 0},
         {8192, 8192, 4, 32, 1, 0},  {8192, 1024, 1, 32, 1, 0}, {2048, 2048, 1, 64, 1, 0},
     };
     bool known = false;

@@ -396,6 +396,31 @@ ag() {
   done
 }
 
+# ah: the Dirac apply's rows per block at 4096^2 (bt 256, XCD map, two-row lookahead), interleaved -- the CG pass's
+#     chunk count had one sharp optimum (af)
+ah() {
+  timeout -k 10 400 python3 -u tools/tune_dslash.py --bt 256 --xchunk 24,26,28,30,32,34,36,40,43,48,52,64 --remap 1 \
+    --variant 1 --rounds 5 --applies 20 > gpurun_out/r06ah_apply_rows.log 2>&1
+}
+
+# ai: rows per block of the t-shard CG pass at 4096 x 512 (config 4's 8-GPU shard): one shard and the RCCL loopback
+ai() {
+  for x in 48 32 40 56 64 73 86 103 128; do
+    timeout -k 10 200 python -u tools/loopback_probe.py --shapes 4096x512 --iters 200 --rounds 3 --applies 2 \
+      --contexts one,loopback --geom 1,$x > gpurun_out/r06ai_rows_$x.log 2>&1 || return 1
+  done
+}
+
+# aj: the t-shard pass at 4096 x 512 around 32 rows per block, twice, interleaved (RCCL loopback and one shard)
+aj() {
+  for i in 1 2; do
+    for x in 48 24 28 32 36; do
+      timeout -k 10 200 python -u tools/loopback_probe.py --shapes 4096x512 --iters 200 --rounds 3 --applies 2 \
+        --contexts one,loopback --geom 1,$x > gpurun_out/r06aj_rows_${x}_$i.log 2>&1 || return 1
+    done
+  done
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
