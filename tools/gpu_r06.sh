@@ -421,6 +421,18 @@ aj() {
   done
 }
 
+# ak: rows per block of the t-shard CG pass at 4096 x 1024 and 4096 x 2048 (4 and 2 GPUs), RCCL loopback and one shard
+ak() {
+  for x in 40 28 32 48; do
+    timeout -k 10 200 python -u tools/loopback_probe.py --shapes 4096x1024 --iters 200 --rounds 3 --applies 2 \
+      --contexts one,loopback --geom 1,$x > gpurun_out/r06ak_1024_rows_$x.log 2>&1 || return 1
+  done
+  for x in 32 24 28 40; do
+    timeout -k 10 200 python -u tools/loopback_probe.py --shapes 4096x2048 --iters 100 --rounds 3 --applies 2 \
+      --contexts one,loopback --geom 1,$x > gpurun_out/r06ak_2048_rows_$x.log 2>&1 || return 1
+  done
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
