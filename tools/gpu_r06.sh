@@ -433,6 +433,13 @@ ak() {
   done
 }
 
+# al: balanced chunk counts of the 8192^2 pass (config 5; 4-wave blocks, 37 t-blocks) against its 32-row chunks
+al() {
+  timeout -k 10 600 python3 -u tools/tune_shapes.py 8192x8192:4,32,1 8192x8192:4,35,1,0,1 8192x8192:4,41,1,0,1 \
+    8192x8192:4,52,1,0,1 8192x8192:4,64,1 8192x8192:4,103,1,0,1 8192x8192:1,64,1 --iters 30 --rounds 3 \
+    > gpurun_out/r06al_shapes_8192.log 2>&1
+}
+
 # fin: the round-end evidence set after the gate (tag $1): benches, config 5, rocprof stats + step gap, FETCH / WRITE
 #      passes, the loopback, and the placement probe over 10 contexts
 fin() {
